@@ -1,0 +1,193 @@
+"""Typed configuration for the MI355X-native Penny serving stack.
+
+Wire-level names (env vars, Kafka topics, Mongo collections) are kept identical to the
+reference so a deployment can switch without touching its environment:
+
+* Kafka: ``KAFKA_SERVER``/``KAFKA_USERNAME``/``KAFKA_PASSWORD`` -> SASL_SSL+PLAIN when both
+  credentials are set, PLAINTEXT otherwise (reference ``config.py:8-23``); topics
+  ``user_message``/``ai_response`` and group ``message_consumer`` (``config.py:26-28``).
+* Mongo: ``MONGODB_URI``, collections ``contexts``/``messages`` (``config.py:31-33``).
+* Model keys kept for compatibility (``config.py:36-47``) although every model now runs
+  locally on the GPU; ``QDRANT_COLLECTION_NAME`` names the on-device corpus.
+
+Engine knobs (model, TP degree, KV block size, graph buckets, retrieval corpus, ...) are
+new; each has a ``PENNY_*`` env override.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from .utils.env import load_dotenv
+
+load_dotenv()
+
+# --------------------------------------------------------------------------------------
+# Wire-compatible constants (reference config.py:26-47)
+# --------------------------------------------------------------------------------------
+USER_MESSAGE_TOPIC = "user_message"
+AI_RESPONSE_TOPIC = "ai_response"
+GROUP_ID = "message_consumer"
+MONGO_DATABASE_NAME = "conversations"
+CONTEXT_COLLECTION_NAME = "contexts"
+MESSAGE_COLLECTION_NAME = "messages"
+QDRANT_COLLECTION_NAME = "transactions"
+
+# Reference operating parameters
+MESSAGE_TIMEOUT_S = 100.0          # main.py:138
+IDLE_SLEEP_S = 0.01                # main.py:156
+LOOP_ERROR_BACKOFF_S = 1.0         # main.py:157-159
+KAFKA_POLL_TIMEOUT_S = 0.1         # kafka_client.py:47
+KAFKA_SESSION_TIMEOUT_MS = "45000"  # kafka_client.py:15
+DEFAULT_TEMPERATURE = 0.5          # llm_agent.py:37,44
+RETRIEVAL_DEFAULT_LIMIT = 10000    # tools/qdrant_tool.py:145
+RETRIEVAL_HNSW_EF = 128            # tools/qdrant_tool.py:99 (we search exactly; kept for API parity)
+
+
+def _env(name: str, default: str = "") -> str:
+    return os.getenv(name, default)
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.getenv(name)
+    return int(v) if v not in (None, "") else default
+
+
+def _env_float(name: str, default: float) -> float:
+    v = os.getenv(name)
+    return float(v) if v not in (None, "") else default
+
+
+def _env_bool(name: str, default: bool) -> bool:
+    v = os.getenv(name)
+    if v in (None, ""):
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+def build_kafka_config() -> Dict[str, str]:
+    """librdkafka config dict with the reference's SASL/PLAINTEXT switch (config.py:8-23)."""
+    cfg: Dict[str, str] = {"bootstrap.servers": _env("KAFKA_SERVER", "")}
+    user, pw = _env("KAFKA_USERNAME", ""), _env("KAFKA_PASSWORD", "")
+    if user and pw:
+        cfg.update({
+            "security.protocol": "SASL_SSL",
+            "sasl.mechanisms": "PLAIN",
+            "sasl.username": user,
+            "sasl.password": pw,
+        })
+    else:
+        cfg["security.protocol"] = "PLAINTEXT"
+    return cfg
+
+
+KAFKA_CONFIG = build_kafka_config()
+MONGODB_URI = _env("MONGODB_URI", "")
+OPENAI_KEY = _env("OPENAI_API_KEY", "")
+OPENAI_MODEL_NAME = _env("OPENAI_MODEL_NAME", "")
+OPENAI_EMBEDDINGS_MODEL_NAME = _env("OPENAI_EMBEDDINGS_MODEL_NAME", "")
+GEMINI_KEY = _env("GEMINI_API_KEY", "")
+GEMINI_MODEL_NAME = _env("GEMINI_MODEL", "")
+QDRANT_URL = _env("QDRANT_URL", "")
+QDRANT_API_KEY = _env("QDRANT_API_KEY", "")
+
+
+# --------------------------------------------------------------------------------------
+# Engine configuration (new)
+# --------------------------------------------------------------------------------------
+@dataclass
+class EngineConfig:
+    """Knobs for one inference-engine replica (one TP group)."""
+
+    model: str = "llama3-8b"                # registry key in models.configs
+    dtype: str = "bf16"
+    weights: Optional[str] = None           # safetensors dir; None -> random init
+    tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
+    tp_size: int = 1
+    kv_block_size: int = 64                 # tokens per KV block (one MFMA KV tile)
+    kv_mem_fraction: float = 0.80           # of free HBM after weights (288 GB per MI355X)
+    num_kv_blocks: Optional[int] = None     # explicit override (tests)
+    max_num_seqs: int = 256                 # running-batch cap
+    max_num_batched_tokens: int = 16384     # per-step token budget (chunked prefill)
+    max_model_len: int = 8192
+    enable_prefix_caching: bool = True
+    use_cuda_graph: bool = True             # hipGraph capture of decode steps
+    graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256)
+    seed: int = 0
+    device: str = "cuda"
+    step_timeout_s: float = 60.0            # GPU-step watchdog
+
+    @classmethod
+    def from_env(cls, **overrides) -> "EngineConfig":
+        c = cls(
+            model=_env("PENNY_MODEL", cls.model),
+            weights=os.getenv("PENNY_WEIGHTS") or None,
+            tokenizer=os.getenv("PENNY_TOKENIZER") or None,
+            tp_size=_env_int("PENNY_TP", cls.tp_size),
+            kv_block_size=_env_int("PENNY_KV_BLOCK", cls.kv_block_size),
+            kv_mem_fraction=_env_float("PENNY_KV_FRACTION", cls.kv_mem_fraction),
+            max_num_seqs=_env_int("PENNY_MAX_SEQS", cls.max_num_seqs),
+            max_num_batched_tokens=_env_int("PENNY_MAX_BATCHED_TOKENS", cls.max_num_batched_tokens),
+            max_model_len=_env_int("PENNY_MAX_MODEL_LEN", cls.max_model_len),
+            enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
+            use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
+            device=_env("PENNY_DEVICE", cls.device),
+        )
+        return dataclasses.replace(c, **overrides)
+
+
+@dataclass
+class RetrievalConfig:
+    embed_model: str = "bge-base-en"
+    corpus_size: int = 1_000_000
+    num_users: int = 10_000
+    limit_default: int = RETRIEVAL_DEFAULT_LIMIT
+    max_limit_tokens: int = 3000            # token-budget clamp for stuffed transactions
+    device: str = "cuda"
+
+    @classmethod
+    def from_env(cls, **overrides) -> "RetrievalConfig":
+        c = cls(
+            embed_model=_env("PENNY_EMBED_MODEL", cls.embed_model),
+            corpus_size=_env_int("PENNY_CORPUS_SIZE", cls.corpus_size),
+            num_users=_env_int("PENNY_CORPUS_USERS", cls.num_users),
+            device=_env("PENNY_DEVICE", cls.device),
+        )
+        return dataclasses.replace(c, **overrides)
+
+
+@dataclass
+class ServingConfig:
+    host: str = "0.0.0.0"
+    port: int = 8000
+    max_concurrent_turns: int = 256         # replaces the reference's 1-turn-per-worker
+    message_timeout_s: float = MESSAGE_TIMEOUT_S
+    temperature: float = DEFAULT_TEMPERATURE
+    max_response_tokens: int = 512
+    max_decide_tokens: int = 96
+    history_token_budget: int = 4096        # oldest messages dropped past this
+    backend: str = "engine"                 # "engine" | "stub"
+
+    @classmethod
+    def from_env(cls, **overrides) -> "ServingConfig":
+        c = cls(
+            port=_env_int("PORT", cls.port),
+            max_concurrent_turns=_env_int("PENNY_MAX_CONCURRENT_TURNS", cls.max_concurrent_turns),
+            max_response_tokens=_env_int("PENNY_MAX_RESPONSE_TOKENS", cls.max_response_tokens),
+            backend=_env("PENNY_BACKEND", cls.backend),
+        )
+        return dataclasses.replace(c, **overrides)
+
+
+from .utils.logging import get_logger  # noqa: E402  (re-export, reference config.py:49)
+
+logger = get_logger(__name__)
+
+__all__ = [
+    "USER_MESSAGE_TOPIC", "AI_RESPONSE_TOPIC", "GROUP_ID", "MONGO_DATABASE_NAME",
+    "CONTEXT_COLLECTION_NAME", "MESSAGE_COLLECTION_NAME", "QDRANT_COLLECTION_NAME",
+    "KAFKA_CONFIG", "MONGODB_URI", "EngineConfig", "RetrievalConfig", "ServingConfig",
+    "build_kafka_config", "get_logger",
+]

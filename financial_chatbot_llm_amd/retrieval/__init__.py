@@ -1,0 +1,7 @@
+"""On-device retrieval: embedders, vector stores and the micro-batched service (R2 + R3)."""
+from .embedder import BgeEmbedder, HashEmbedder
+from .service import RetrievalService
+from .store import Corpus, DeviceVectorStore, Hit, NumpyVectorStore, synthetic_payload, user_name
+
+__all__ = ["BgeEmbedder", "HashEmbedder", "RetrievalService", "Corpus", "DeviceVectorStore", "Hit",
+           "NumpyVectorStore", "synthetic_payload", "user_name"]

@@ -1,0 +1,115 @@
+"""FastAPI surface (reference ``main.py:24-53``) plus the services factory.
+
+Endpoints:
+* ``GET /health`` -> ``{"status": "healthy"}`` (``main.py:51-53``; Docker HEALTHCHECK target).
+* ``POST /process_message`` -- the reference's commented-out sync endpoint (``main.py:39-49``),
+  re-enabled: ``{conversation_id, message, user_id}`` -> ``{response, retrieved_transactions_count}``.
+* ``POST /v1/chat/stream`` -- server-sent events of the agent's updates for one turn (no Kafka);
+  used for latency probing.
+* ``GET /metrics`` -- Prometheus text: turns/s, TTFT p50/p99, ITL, KV utilisation, ...
+* ``/docs``, ``/redoc``, ``/openapi.json`` come from FastAPI as in the reference.
+
+The lifespan pings Mongo (raising aborts startup), subscribes the Kafka consumer and starts
+the background consumer (``main.py:24-30``).  Unlike gunicorn-per-worker replicas of the
+reference (``main.py:18-22``), ONE process owns the GPU engine and serves every connection.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+from contextlib import asynccontextmanager
+from dataclasses import dataclass
+from typing import Any, Optional
+
+from fastapi import FastAPI
+from fastapi.responses import PlainTextResponse, StreamingResponse
+from pydantic import BaseModel
+
+from .. import config
+from ..utils.logging import get_logger
+from ..utils.metrics import METRICS
+from .worker import ChatWorker
+
+logger = get_logger(__name__)
+
+
+@dataclass
+class Services:
+    db: Any
+    kafka: Any
+    agent: Any
+    engine: Any = None
+    retrieval: Any = None
+    serving: Optional[config.ServingConfig] = None
+
+
+class MessagePayload(BaseModel):
+    conversation_id: str
+    message: str
+    user_id: str
+
+
+def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
+    serving = services.serving or config.ServingConfig()
+    state = {"worker": None, "task": None}
+
+    @asynccontextmanager
+    async def lifespan(app: FastAPI):
+        await services.db.check_connection()
+        worker = ChatWorker(services.db, services.kafka, services.agent,
+                            max_concurrent_turns=serving.max_concurrent_turns,
+                            message_timeout_s=serving.message_timeout_s)
+        state["worker"] = worker
+        app.state.worker = worker
+        if start_consumer:
+            services.kafka.setup_consumer()
+            state["task"] = asyncio.create_task(worker.consume_messages())
+        try:
+            yield
+        finally:
+            worker.stop()
+            if state["task"] is not None:
+                state["task"].cancel()
+                try:
+                    await state["task"]
+                except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                    pass
+            services.kafka.close()
+            if services.engine is not None and hasattr(services.engine, "shutdown"):
+                services.engine.shutdown()
+
+    app = FastAPI(title="Finance Chatbot LLM Worker",
+                  description="A python worker for processing LLM requests",
+                  version="1.0.0", lifespan=lifespan)
+    app.state.services = services
+
+    @app.get("/health")
+    async def health_check():
+        return {"status": "healthy"}
+
+    @app.get("/metrics", response_class=PlainTextResponse)
+    async def metrics():
+        if services.engine is not None and hasattr(services.engine, "stats"):
+            for k, v in services.engine.stats().items():
+                METRICS.set_gauge(f"engine_{k}", float(v))
+        return METRICS.render_prometheus()
+
+    @app.post("/process_message")
+    async def process_message_endpoint(payload: MessagePayload):
+        user_context, _ = await services.db.get_context(payload.conversation_id)
+        chat_history = await services.db.get_history(payload.conversation_id)
+        res = await services.agent.query(payload.message, payload.user_id, user_context, chat_history)
+        return {"response": res["response"], "retrieved_transactions_count": res["retrieved_transactions_count"]}
+
+    @app.post("/v1/chat/stream")
+    async def chat_stream(payload: MessagePayload):
+        user_context, user_id = await services.db.get_context(payload.conversation_id)
+        chat_history = await services.db.get_history(payload.conversation_id)
+
+        async def gen():
+            async for upd in services.agent.stream_with_status(payload.message, user_id, user_context, chat_history):
+                yield f"data: {json.dumps(upd)}\n\n"
+
+        return StreamingResponse(gen(), media_type="text/event-stream")
+
+    return app

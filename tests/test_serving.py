@@ -1,0 +1,120 @@
+"""Integration: Kafka-fake turn -> streamed chunks -> complete -> Mongo-fake save."""
+import asyncio
+import json
+
+import httpx
+
+from financial_chatbot_llm_amd import config
+from financial_chatbot_llm_amd.adapters import InMemoryBroker
+from financial_chatbot_llm_amd.agent import StubLLM
+from financial_chatbot_llm_amd.serving import ChatWorker, create_app
+from financial_chatbot_llm_amd.serving.factory import build_stub_services
+from financial_chatbot_llm_amd.tools import ToolCall
+from helpers import TODAY, seeded_db, seeded_store
+
+
+def services(llm, convs=(("c1", "u1"),), **kw):
+    emb, store = seeded_store()
+    broker = InMemoryBroker()
+    db = seeded_db(convs)
+    return build_stub_services(broker=broker, db=db, llm=llm, store=store, embedder=emb, today_fn=lambda: TODAY, **kw)
+
+
+def send(svc, cid, text, uid="u1", ts=1):
+    svc.db.put_user_message(cid, text, uid, ts)
+    svc.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key=cid,
+                               value=json.dumps({"message": text, "conversation_id": cid, "user_id": uid}))
+
+
+async def run_worker(svc, n_msgs, timeout_s=100.0):
+    svc.kafka.setup_consumer()
+    w = ChatWorker(svc.db, svc.kafka, svc.agent, message_timeout_s=timeout_s)
+    return w
+
+
+def drive(svc, msgs, timeout_s=100.0):
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent, message_timeout_s=timeout_s)
+        task = asyncio.create_task(w.consume_messages())
+        for m in msgs:
+            send(svc, *m)
+        for _ in range(400):
+            await asyncio.sleep(0.01)
+            if len(w.traces) >= len(msgs) and not w._tasks:
+                break
+        w.stop()
+        await task
+        return w
+    return asyncio.run(main())
+
+
+def out(svc, cid=None):
+    return svc.kafka.broker.values(config.AI_RESPONSE_TOPIC, cid)
+
+
+def test_full_turn_streams_then_completes_and_saves():
+    svc = services(StubLLM(decisions=[ToolCall("retrieve_transactions", {"search_query": "grocery"})],
+                           responses=["one two three four five"], chunk_words=2))
+    drive(svc, [("c1", "What did I spend on groceries?")])
+    ev = out(svc, "c1")
+    assert [e.get("type") for e in ev] == ["response_chunk"] * 3 + ["complete"]
+    assert "".join(e["message"] for e in ev[:-1]) == "one two three four five"
+    assert ev[-1]["message"] == "What did I spend on groceries?" and ev[-1]["user_id"] == "u1"
+    saved = list(svc.db.messages_collection.find({"conversation_id": "c1", "sender": "AIMessage"}))
+    assert saved[0]["message"] == "one two three four five" and saved[0]["user_id"] == "u1"
+
+
+def test_missing_context_sends_nothing():
+    svc = services(StubLLM())
+    drive(svc, [("nope", "hi", "u9")])
+    assert out(svc) == []
+
+
+def test_agent_error_sends_error_event():
+    svc = services(StubLLM(decisions=[None], responses=["a b c d e f"], chunk_words=1, fail_stream=True))
+    drive(svc, [("c1", "hello")])
+    ev = out(svc, "c1")
+    assert ev[-1]["error"] is True and ev[-1]["message"] == "" and "type" not in ev[-1]
+    assert svc.db.messages_collection.count_documents({"sender": "AIMessage"}) == 0
+
+
+def test_timeout_event():
+    svc = services(StubLLM(decisions=[None], decide_delay_s=0.5))
+    drive(svc, [("c1", "hello")], timeout_s=0.05)
+    ev = out(svc, "c1")
+    assert ev[-1]["message"] == "Request timed out. Please try again." and ev[-1]["error"] is True
+
+
+def test_concurrent_conversations_and_per_key_order():
+    convs = [(f"c{i}", f"u{i}") for i in range(6)]
+    svc = services(StubLLM(stream_delay_s=0.005), convs=convs)
+    msgs = [(c, "hello", u) for c, u in convs] + [("c0", "second", "u0", 2)]
+    w = drive(svc, msgs)
+    assert len(w.traces) == 7 and not any(t.error for t in w.traces)
+    ev0 = out(svc, "c0")
+    completes = [e for e in ev0 if e.get("type") == "complete"]
+    assert [c["message"] for c in completes] == ["hello", "second"]
+    # each turn's chunks arrive before its complete (no interleaving within a conversation)
+    first_complete = ev0.index(completes[0])
+    assert all(e.get("type") == "response_chunk" for e in ev0[:first_complete])
+
+
+def test_http_surface():
+    svc = services(StubLLM(responses=["answer text"]))
+    svc.db.put_user_message("c1", "invest?", "u1", 1)
+    app = create_app(svc, start_consumer=False)
+
+    async def main():
+        async with app.router.lifespan_context(app):
+            transport = httpx.ASGITransport(app=app)
+            async with httpx.AsyncClient(transport=transport, base_url="http://t") as cl:
+                r = await cl.get("/health")
+                assert r.json() == {"status": "healthy"}
+                r = await cl.post("/process_message", json={"conversation_id": "c1", "message": "invest?", "user_id": "u1"})
+                assert r.json()["response"] == "answer text"
+                r = await cl.get("/openapi.json")
+                assert r.json()["info"]["title"] == "Finance Chatbot LLM Worker"
+                r = await cl.get("/metrics")
+                assert r.status_code == 200
+    asyncio.run(main())
