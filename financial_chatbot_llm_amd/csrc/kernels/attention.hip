@@ -1,0 +1,439 @@
+// K6 (paged prefill / varlen, causal or bidirectional) and K7 (paged split-K decode) attention
+// for gfx950, on v_mfma_f32_16x16x32_bf16 with f32 online softmax.
+//
+// Orientation (see kv_layout.h): scores are computed TRANSPOSED, S^T = K . Q^T, so a lane holds
+// one query column and 16 keys in registers; the P.V product is O^T = V^T . P^T and takes P
+// straight from those registers (no LDS round trip for P), with V stored dim-major in the cache.
+//
+// GQA packing: the G = Hq/Hkv query heads that share a kv head are packed into the MFMA's 16
+// query columns (decode) or into the 128 "rows" of a prefill tile (rows = token*G + head), so
+// every K/V byte staged is used by all G heads.
+//
+// Prefill: one workgroup = 4 waves = 128 (token, head) rows of one sequence and one kv head.
+// K and V^T blocks (64 keys) are staged through XOR-swizzled LDS, double-buffered: the global
+// loads for block j+1 are issued before block j's MFMAs and written to LDS after them
+// (async-STAGE split, cdna_hip_programming.md T14), one barrier per block.  Swizzles make every
+// ds_read_b128 of the fragment reads conflict-free (K rows of 256 B: chunk ^= key&15; 128-B rows
+// (V^T, or K at D=64): chunk ^= (row>>1)&7).
+//
+// Decode: one workgroup = 4 waves = one (sequence, kv head, partition of PB blocks).  Each wave
+// streams whole 64-key blocks straight into VGPRs (decode is HBM-bound; an LDS hop is pure
+// overhead: the 'GEMV / M <= 16' row of the guide), the 4 waves merge through LDS, and a second
+// kernel merges partitions (flash-decoding split-K) when a sequence spans several.
+#include "common.h"
+#include "kv_layout.h"
+
+#define LOG2E 1.4426950408889634f
+
+union Frag {
+  uint4 u;
+  bf16x8 v;
+};
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// byte offset of 16-B chunk `c` of row `r` in a swizzled LDS tile with ROWB-byte rows
+template <int ROWB>
+__device__ __forceinline__ int swz(int r, int c) {
+  if constexpr (ROWB == 256) {
+    return r * 256 + ((c ^ (r & 15)) << 4);
+  } else {
+    static_assert(ROWB == 128, "row width");
+    return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Prefill
+// ------------------------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(256) prefill_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+  constexpr int KC = D / 32;        // k-chunks of the QK^T product
+  constexpr int DT = D / 16;        // 16-row dim tiles of O^T
+  constexpr int KROWB = D * 2;      // K row bytes in LDS
+  constexpr int KBYTES = KV_BS * D * 2;
+  constexpr int VBYTES = D * KV_BS * 2;
+  constexpr int KCH = KBYTES / 16 / 256;  // staged 16-B chunks per thread
+  constexpr int VCH = VBYTES / 16 / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
+
+  const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
+  const int G = Hq / Hkv;
+  const int TQ = 128 / G;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  const int tok0 = tile * TQ;
+  if (tok0 >= qlen) return;
+  const int ctx = ctx_lens[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+
+  // query rows owned by this lane (one per column tile)
+  int tok[2], head[2], qpos[2];
+  Frag qf[2][KC];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int r = w * 32 + ct * 16 + col;
+    tok[ct] = tok0 + r / G;
+    head[ct] = h * G + r % G;
+    const bool valid = tok[ct] < qlen;
+    qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
+    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  const int last_tok = min(tok0 + TQ, qlen) - 1;
+  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
+  const int nblk = (kv_end + KV_BS - 1) / KV_BS;
+  const int* bt = block_tables + (long)s * max_blocks;
+
+  f32x4 o[2][DT];
+  float m[2], l[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    m[ct] = -INFINITY;
+    l[ct] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  uint4 kst[KCH], vst[VCH];
+  auto stage_load = [&](int j) {
+    const long phys = bt[j];
+    const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) kst[i] = kb[threadIdx.x + i * 256];
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) vst[i] = vb[threadIdx.x + i * 256];
+  };
+  auto stage_write = [&](int buf) {
+    char* kl = smem + buf * (KBYTES + VBYTES);
+    char* vl = kl + KBYTES;
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int id = threadIdx.x + i * 256;
+      const int r = id / (KROWB / 16), c = id % (KROWB / 16);
+      *reinterpret_cast<uint4*>(kl + swz<KROWB>(r, c)) = kst[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int id = threadIdx.x + i * 256;
+      const int r = id >> 3, c = id & 7;
+      *reinterpret_cast<uint4*>(vl + swz<128>(r, c)) = vst[i];
+    }
+  };
+
+  if (nblk > 0) {
+    stage_load(0);
+    stage_write(0);
+  }
+  __syncthreads();
+
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1;
+    if (j + 1 < nblk) stage_load(j + 1);
+    const char* kl = smem + buf * (KBYTES + VBYTES);
+    const char* vl = kl + KBYTES;
+
+    // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
+    f32x4 sc[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        Frag kf;
+        kf.u = *reinterpret_cast<const uint4*>(kl + swz<KROWB>(16 * t + col, 4 * c + g));
+        sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
+        sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
+      }
+    }
+
+    // ---- online softmax (base-2) -------------------------------------------------------
+    Frag pf[2][2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = j * KV_BS + 16 * t + 4 * g + r;
+          const bool ok = key < ctx && (!causal || key <= qpos[ct]);
+          const float v = ok ? sc[ct][t][r] * scale_log2 : -INFINITY;
+          sc[ct][t][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m[ct], mt);
+      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[ct] - mn);
+      float ls = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = (mn == -INFINITY) ? 0.f : exp2f(sc[ct][t][r] - mn);
+          sc[ct][t][r] = p;
+          ls += p;
+        }
+      }
+      l[ct] = l[ct] * alpha + ls;
+      m[ct] = mn;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
+          pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
+        }
+      }
+    }
+
+    // ---- O^T += V^T . P^T ---------------------------------------------------------------
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        Frag vf;
+        vf.u = *reinterpret_cast<const uint4*>(vl + swz<128>(16 * dt + col, 4 * st + g));
+        o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
+        o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
+      }
+    }
+
+    if (j + 1 < nblk) stage_write(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: finish row sums across the 4 lane groups, normalise, store -----------
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float lt = l[ct];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (tok[ct] >= qlen) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x4 v4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode
+// ------------------------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(256) decode_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
+    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, float scale_log2, int Hq,
+    int Hkv, int max_blocks, int pb, int nparts) {
+  constexpr int KC = D / 32, DT = D / 16;
+  __shared__ float s_m[4][16], s_l[4][16];
+  __shared__ float s_o[4][16][D + 4];
+
+  const int b = blockIdx.z, h = blockIdx.y, p = blockIdx.x;
+  const int ctx = ctx_lens[b];
+  const int nblk = (ctx + KV_BS - 1) / KV_BS;
+  const int blk0 = p * pb;
+  if (blk0 >= nblk) return;
+  const int blk1 = min(blk0 + pb, nblk);
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+  const int* bt = block_tables + (long)b * max_blocks;
+
+  Frag qf[KC];
+  {
+    const bool valid = col < G;
+    const bf16* qrow = q + ((long)b * Hq + h * G + (valid ? col : 0)) * D;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      qf[c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  for (int j = blk0 + w; j < blk1; j += 4) {
+    const long phys = bt[j];
+    const bf16* kb = k_cache + (phys * Hkv + h) * (long)(KV_BS * D);
+    const bf16* vb = v_cache + (phys * Hkv + h) * (long)(KV_BS * D);
+    Frag kf[4][KC], vf[DT][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int c = 0; c < KC; ++c)
+        kf[t][c].u = *reinterpret_cast<const uint4*>(kb + (16 * t + col) * D + 32 * c + 8 * g);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        vf[dt][st].u = *reinterpret_cast<const uint4*>(vb + (16 * dt + col) * KV_BS + 32 * st + 8 * g);
+
+    f32x4 sc[4];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KC; ++c) sc[t] = mfma16(kf[t][c].v, qf[c].v, sc[t]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = j * KV_BS + 16 * t + 4 * g + r;
+        const float v = key < ctx ? sc[t][r] * scale_log2 : -INFINITY;
+        sc[t][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    float ls = 0.f;
+    Frag pf[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(sc[t][r] - mn);
+        ls += pv;
+        pf[t >> 1].v[4 * (t & 1) + r] = (bf16)pv;
+      }
+    }
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = mfma16(vf[dt][0].v, pf[0].v, o[dt]);
+      o[dt] = mfma16(vf[dt][1].v, pf[1].v, o[dt]);
+    }
+  }
+
+  // merge the 4 waves through LDS
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (g == 0) {
+    s_m[w][col] = m;
+    s_l[w][col] = l;
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s_o[w][col][16 * dt + 4 * g + r] = o[dt][r];
+  __syncthreads();
+
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int qc = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, s_m[ww][qc]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = s_m[ww][qc] == -INFINITY ? 0.f : exp2f(s_m[ww][qc] - M);
+      L += s_l[ww][qc] * f;
+      O += s_o[ww][qc][d] * f;
+    }
+    const int hq = h * G + qc;
+    if (nparts == 1) {
+      out[((long)b * Hq + hq) * D + d] = (bf16)(O / L);
+    } else {
+      const long pi = ((long)b * Hq + hq) * nparts + p;
+      part_o[pi * D + d] = O;
+      if (d == 0) {
+        part_m[pi] = M;
+        part_l[pi] = L;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const float* __restrict__ part_m,
+                                     const float* __restrict__ part_l, const float* __restrict__ part_o,
+                                     bf16* __restrict__ out, int Hq, int pb, int nparts) {
+  const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
+  const int nblk = (ctx_lens[b] + KV_BS - 1) / KV_BS;
+  const int np = min(nparts, (nblk + pb - 1) / pb);
+  const long base = ((long)b * Hq + hq) * nparts;
+  float M = -INFINITY;
+  for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
+  float L = 0.f, O = 0.f;
+  for (int i = 0; i < np; ++i) {
+    const float f = exp2f(part_m[base + i] - M);
+    L += part_l[base + i] * f;
+    O += part_o[(base + i) * D + d] * f;
+  }
+  if (d < D) out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+}
+
+PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
+                                      const void* k_cache, const void* v_cache, void* out, int num_seqs,
+                                      int max_q_len, int Hq, int Hkv, int D, int max_blocks, float scale, int causal,
+                                      hipStream_t stream) {
+  if (num_seqs <= 0 || max_q_len <= 0) return 0;
+  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  const int G = Hq / Hkv;
+  if (G > 128 || (128 % G)) return (int)hipErrorInvalidValue;
+  const int TQ = 128 / G;
+  dim3 grid((max_q_len + TQ - 1) / TQ, Hkv, num_seqs);
+  const float sl2 = scale * LOG2E;
+  if (D == 128) {
+    hipLaunchKernelGGL(prefill_kernel<128>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens, block_tables,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);
+  } else if (D == 64) {
+    hipLaunchKernelGGL(prefill_kernel<64>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens, block_tables,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
+}
+
+PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const int* block_tables, const void* k_cache,
+                                     const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
+                                     int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts, float scale,
+                                     hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid(nparts, Hkv, B);
+  const float sl2 = scale * LOG2E;
+  if (D == 128) {
+    hipLaunchKernelGGL(decode_kernel<128>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, block_tables,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,
+                       max_blocks, pb, nparts);
+    if (nparts > 1)
+      hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, B), dim3(128), 0, stream, ctx_lens, part_m, part_l,
+                         part_o, (bf16*)out, Hq, pb, nparts);
+  } else if (D == 64) {
+    hipLaunchKernelGGL(decode_kernel<64>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, block_tables,
+                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,
+                       max_blocks, pb, nparts);
+    if (nparts > 1)
+      hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, B), dim3(64), 0, stream, ctx_lens, part_m, part_l,
+                         part_o, (bf16*)out, Hq, pb, nparts);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
+}

@@ -1,0 +1,85 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernel library.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes; block sizes are multiples of 64.
+//  * bf16 tensors are moved 16 B (8 elements) per lane per instruction (uint4), math in f32.
+//  * every launcher is `extern "C"`, takes raw device pointers + a hipStream_t, never
+//    allocates or synchronises (so it can be captured into a hipGraph), and returns the
+//    hipError_t of the launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PENNY_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+static constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+// 8 x bf16 <-> uint4 (16 B) helpers
+union Pack8 {
+  uint4 u;
+  bf16x8 v;
+  bf16 e[8];
+};
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  Pack8 p;
+  p.u = u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)p.e[i];
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  Pack8 p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p.e[i] = (bf16)f[i];
+  return p.u;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `scratch` needs blockDim.x/64 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  __syncthreads();
+  return t;
+}
+
+// splitmix64 -> two uniforms in (0, 1); counter-based so results are launch-order independent.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float u01_from_bits(uint32_t b) {
+  // 24 random mantissa bits, strictly inside (0, 1)
+  return ((float)(b >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+#define PENNY_RETURN_LAUNCH() return (int)hipGetLastError()

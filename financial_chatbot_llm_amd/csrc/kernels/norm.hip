@@ -1,0 +1,167 @@
+// K2 / K14: fused residual-add + RMSNorm (Llama) and residual-add + LayerNorm (BERT).
+//
+// One workgroup per token row; each lane owns CPT 16-byte chunks (8 bf16) of the row, kept
+// in registers between the statistics pass and the normalise pass, so a row is read once and
+// written once (HBM-bound op: 2-3 row passes total vs 5+ for an unfused torch sequence).
+//
+//   rms:      y = bf16(x * rsqrt(mean(x^2) + eps) * w)
+//   add_rms:  r = bf16(x + res); res <- r; y = rms(r)          (in-place residual update)
+//   ln:       y = bf16((x - mu) * rsqrt(var + eps) * g + b)
+//   add_ln:   r = x + res (f32); y = ln(r)                     (BERT post-LN: LN(x + sublayer(x)))
+#include "common.h"
+
+template <int CPT, bool ADD_RES>
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ res,
+                                                       const bf16* __restrict__ w, bf16* __restrict__ y,
+                                                       int H, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nchunk = H >> 3;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
+  uint4* rr = reinterpret_cast<uint4*>(res + (size_t)row * H);
+  float v[CPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = threadIdx.x + c * blockDim.x;
+    if (idx < nchunk) {
+      unpack8(xr[idx], v[c]);
+      if (ADD_RES) {
+        float r[8];
+        unpack8(rr[idx], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = (float)(bf16)(v[c][i] + r[i]);  // residual kept in bf16
+        rr[idx] = pack8(v[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  const float inv = rsqrtf(block_sum(ss, scratch) / (float)H + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * H);
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = threadIdx.x + c * blockDim.x;
+    if (idx < nchunk) {
+      float g[8], o[8];
+      unpack8(wr[idx], g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(v[c][i] * inv) * g[i];
+      yr[idx] = pack8(o);
+    }
+  }
+}
+
+template <int CPT, bool ADD_RES>
+__global__ void __launch_bounds__(1024) layernorm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                         const bf16* __restrict__ g, const bf16* __restrict__ b,
+                                                         bf16* __restrict__ y, int H, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nchunk = H >> 3;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
+  const uint4* rr = reinterpret_cast<const uint4*>(res + (size_t)row * H);
+  float v[CPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = threadIdx.x + c * blockDim.x;
+    if (idx < nchunk) {
+      unpack8(xr[idx], v[c]);
+      if (ADD_RES) {
+        float r[8];
+        unpack8(rr[idx], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] += r[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  const float mu = block_sum(s, scratch) / (float)H;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = threadIdx.x + c * blockDim.x;
+    if (idx < nchunk) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        sq += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(sq, scratch) / (float)H + eps);
+  const uint4* gr = reinterpret_cast<const uint4*>(g);
+  const uint4* br = reinterpret_cast<const uint4*>(b);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * H);
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = threadIdx.x + c * blockDim.x;
+    if (idx < nchunk) {
+      float gg[8], bb[8], o[8];
+      unpack8(gr[idx], gg);
+      unpack8(br[idx], bb);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * inv * gg[i] + bb[i];
+      yr[idx] = pack8(o);
+    }
+  }
+}
+
+static inline void pick_geometry(int H, int* threads, int* cpt) {
+  const int nchunk = H / 8;
+  int t = nchunk >= 256 ? 256 : ((nchunk + 63) / 64) * 64;
+  int c = (nchunk + t - 1) / t;
+  while (c > 8) {
+    t *= 2;
+    c = (nchunk + t - 1) / t;
+  }
+  int p = 1;
+  while (p < c) p <<= 1;
+  *threads = t;
+  *cpt = p;
+}
+
+#define DISPATCH_CPT(CPT_VAL, ...)             \
+  switch (CPT_VAL) {                           \
+    case 1: { constexpr int CPT = 1; __VA_ARGS__; break; } \
+    case 2: { constexpr int CPT = 2; __VA_ARGS__; break; } \
+    case 4: { constexpr int CPT = 4; __VA_ARGS__; break; } \
+    default: { constexpr int CPT = 8; __VA_ARGS__; break; } \
+  }
+
+PENNY_API int penny_rmsnorm(const void* x, void* res, const void* w, void* y, int T, int H, float eps,
+                            int add_residual, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return (int)hipErrorInvalidValue;
+  int threads, cpt;
+  pick_geometry(H, &threads, &cpt);
+  if (add_residual) {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, true>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps));
+  } else {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, false>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps));
+  }
+  PENNY_RETURN_LAUNCH();
+}
+
+PENNY_API int penny_layernorm(const void* x, const void* res, const void* g, const void* b, void* y, int T, int H,
+                              float eps, int add_residual, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return (int)hipErrorInvalidValue;
+  int threads, cpt;
+  pick_geometry(H, &threads, &cpt);
+  if (add_residual) {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((layernorm_kernel<CPT, true>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (const bf16*)res, (const bf16*)g, (const bf16*)b,
+                                         (bf16*)y, H, eps));
+  } else {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((layernorm_kernel<CPT, false>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (const bf16*)res, (const bf16*)g, (const bf16*)b,
+                                         (bf16*)y, H, eps));
+  }
+  PENNY_RETURN_LAUNCH();
+}

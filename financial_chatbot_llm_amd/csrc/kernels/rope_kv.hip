@@ -1,0 +1,89 @@
+// K3 epilogue + K4 + K5: rotary embedding of q/k taken straight from the fused QKV GEMM output,
+// and the paged KV-cache write, in ONE pass over the QKV activations.
+//
+// qkv      [T, (Hq + 2*Hkv) * D] bf16  (q heads, then k heads, then v heads)
+// q_out    [T, Hq, D] bf16              (rotated q, consumed by the attention kernels)
+// k_cache  [num_blocks][Hkv][BS][D]      bf16, key-major rows (MFMA A operand for S^T = K Q^T)
+// v_cache  [num_blocks][Hkv][D][BS]      bf16, dim-major with the key order inside each 32-key
+//                                        group permuted so that the P.V MFMA A-fragment of a lane
+//                                        (8 keys of one dim) is one contiguous 16-B load
+//                                        (see kv_perm() and attention.hip).
+// cos_sin  [max_pos, D] f32: cos(pos * inv_freq[i]) for i < D/2, then sin(...)  (host-precomputed,
+//          so the kernel stays bandwidth-bound: no on-device trig, Appendix B 'Element-wise')
+// Rotation is the HF/"neox" rotate-half form used by Llama-3 checkpoints.
+#include "common.h"
+#include "kv_layout.h"
+
+template <int D>
+__global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restrict__ positions,
+                               const float* __restrict__ cos_sin, const int* __restrict__ slots,
+                               bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
+                               int Hq, int Hkv, int apply_rope) {
+  constexpr int HALF = D / 2;
+  constexpr int RU = HALF / 8;  // rotary units per head (8 pairs each)
+  constexpr int VU = D / 8;     // copy units per v head
+  const int t = blockIdx.x;
+  const int pos = positions[t];
+  const int slot = slots[t];
+  const int width = (Hq + 2 * Hkv) * D;
+  const bf16* row = qkv + (long)t * width;
+  const float* cs = cos_sin + (long)pos * D;
+  const int n_rot = (Hq + Hkv) * RU;
+  const int total = n_rot + Hkv * VU;
+  const long blk = slot >= 0 ? slot / KV_BS : 0;
+  const int off = slot >= 0 ? slot % KV_BS : 0;
+  for (int u = threadIdx.x; u < total; u += blockDim.x) {
+    if (u < n_rot) {
+      const int h = u / RU, c = u % RU;
+      const bf16* src = row + h * D;
+      float x1[8], x2[8];
+      unpack8(*reinterpret_cast<const uint4*>(src + c * 8), x1);
+      unpack8(*reinterpret_cast<const uint4*>(src + HALF + c * 8), x2);
+      if (apply_rope) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float co = cs[c * 8 + i], si = cs[HALF + c * 8 + i];
+          const float a = x1[i], b = x2[i];
+          x1[i] = a * co - b * si;
+          x2[i] = b * co + a * si;
+        }
+      }
+      const uint4 p1 = pack8(x1), p2 = pack8(x2);
+      if (h < Hq) {
+        bf16* dst = q_out + ((long)t * Hq + h) * D;
+        *reinterpret_cast<uint4*>(dst + c * 8) = p1;
+        *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
+      } else if (slot >= 0) {
+        const int kh = h - Hq;
+        bf16* dst = k_cache + ((blk * Hkv + kh) * KV_BS + off) * D;
+        *reinterpret_cast<uint4*>(dst + c * 8) = p1;
+        *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
+      }
+    } else if (slot >= 0) {
+      const int v = u - n_rot;
+      const int h = v / VU, c = v % VU;
+      Pack8 p;
+      p.u = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + h) * D + c * 8);
+      bf16* base = v_cache + (blk * Hkv + h) * (long)D * KV_BS + kv_perm(off);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) base[(long)(c * 8 + i) * KV_BS] = p.e[i];
+    }
+  }
+}
+
+PENNY_API int penny_rope_kv_write(const void* qkv, const int* positions, const float* cos_sin, const int* slots,
+                                  void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
+                                  int apply_rope, hipStream_t stream) {
+  if (T <= 0) return 0;
+  const int threads = 256;
+  if (D == 128) {
+    hipLaunchKernelGGL(rope_kv_kernel<128>, dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions, cos_sin,
+                       slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope);
+  } else if (D == 64) {
+    hipLaunchKernelGGL(rope_kv_kernel<64>, dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions, cos_sin,
+                       slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
+}

@@ -1,0 +1,99 @@
+"""ctypes binding of ``libpenny_kernels.so`` (the gfx950 HIP kernel library).
+
+The library is loaded AFTER ``import torch`` so its ``libamdhip64.so.7`` dependency resolves
+to the HIP runtime torch already mapped (one runtime, one device context, torch's streams are
+valid handles).  Every launcher takes the current torch stream, so calls are ordered with
+torch's own kernels and are captured by ``torch.cuda.graph`` (hipGraph) like any other launch.
+
+Policy: on a GPU tensor a missing or failing library is an ERROR (ops never fall back silently
+on the device -- the round-end check records which native code actually ran).  CPU tensors take
+the fp32 PyTorch reference path in each op module (CI / numerics oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch
+
+_LOCK = threading.Lock()
+_LIB: Optional[ctypes.CDLL] = None
+_ERR: Optional[str] = None
+
+c_int, c_long, c_float, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p
+P = c_void_p
+
+_SIGS = {
+    "penny_rmsnorm": [P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "penny_layernorm": [P, P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "penny_silu_mul": [P, P, c_int, c_int, P],
+    "penny_gelu": [P, c_long, P],
+    "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
+    "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P],
+    "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P],
+    "penny_sample": [P, c_int, c_long, P, P, P, c_int, c_int, P],
+    "penny_filtered_topk": [P, P, P, c_long, c_int, P, P, P, P, c_int, c_int, P, P, P, c_int, P, P, P, P],
+}
+
+
+def lib_path() -> str:
+    from .._build import KERNEL_LIB
+    return KERNEL_LIB
+
+
+def load(build_if_missing: bool = True) -> ctypes.CDLL:
+    global _LIB, _ERR
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = lib_path()
+        if not os.path.exists(path) and build_if_missing:
+            from .._build import build_kernels
+            build_kernels()
+        try:
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            _ERR = str(e)
+            raise RuntimeError(f"penny kernel library unavailable: {e}") from e
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        _LIB = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load(build_if_missing=False)
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hipError {rc}")
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True -> run the HIP kernel.  CPU tensors use the torch reference path."""
+    if t.device.type != "cuda":
+        return False
+    if os.environ.get("PENNY_FORCE_TORCH_OPS") == "1":
+        return False
+    return True

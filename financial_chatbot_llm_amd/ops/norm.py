@@ -1,0 +1,49 @@
+"""K2/K14 normalisation ops: fused residual-add + RMSNorm, residual-add + LayerNorm."""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+
+def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    y = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype)
+    return (y.float() * w.float()).to(x.dtype)
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``residual is None``: y = rms(x).  Otherwise residual <- x + residual (in place, bf16) and
+    y = rms(residual) -- the Llama pre-norm pattern, one HBM pass."""
+    H = x.shape[-1]
+    T = x.numel() // H
+    if N.use_native(x):
+        out = torch.empty_like(x) if out is None else out
+        N.call("penny_rmsnorm", N.ptr(x), N.ptr(residual), N.ptr(w), N.ptr(out), T, H, float(eps),
+               int(residual is not None), N.stream())
+        return out
+    if residual is not None:
+        residual.copy_((x + residual).to(residual.dtype))
+        x = residual
+    y = _rms_ref(x, w, eps)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float,
+               residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = LN(x + residual) (residual optional), f32 statistics, bf16 out."""
+    H = x.shape[-1]
+    T = x.numel() // H
+    if N.use_native(x):
+        out = torch.empty_like(x)
+        N.call("penny_layernorm", N.ptr(x), N.ptr(residual), N.ptr(g), N.ptr(b), N.ptr(out), T, H, float(eps),
+               int(residual is not None), N.stream())
+        return out
+    xf = x.float() + (residual.float() if residual is not None else 0.0)
+    return torch.nn.functional.layer_norm(xf, (H,), g.float(), b.float(), eps).to(x.dtype)

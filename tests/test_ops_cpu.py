@@ -1,0 +1,92 @@
+"""CPU checks of the op reference paths (the oracles for the HIP kernels) and the paged layout."""
+import math
+
+import torch
+
+from financial_chatbot_llm_amd import ops
+from financial_chatbot_llm_amd.ops.attention import KV_BS, KV_PERM, gather_kv_ref, write_kv_ref
+
+
+def test_kv_perm_is_permutation_and_fragment_contiguous():
+    assert sorted(KV_PERM.tolist()) == list(range(KV_BS))
+    # lane group g of k-step s reads 8 contiguous physical keys = {32s+4g+0..3, 32s+16+4g+0..3}
+    inv = {p: k for k, p in enumerate(KV_PERM.tolist())}
+    for s in range(2):
+        for g in range(4):
+            keys = [inv[32 * s + 8 * g + j] for j in range(8)]
+            assert keys == [32 * s + 4 * g + j for j in range(4)] + [32 * s + 16 + 4 * g + j for j in range(4)]
+
+
+def test_paged_roundtrip():
+    Hkv, D, nb = 2, 16, 5
+    kc = torch.zeros(nb, Hkv, KV_BS, D)
+    vc = torch.zeros(nb, Hkv, D, KV_BS)
+    L = 150
+    blocks = torch.tensor([3, 0, 4], dtype=torch.int32)
+    slots = torch.tensor([int(blocks[i // KV_BS]) * KV_BS + i % KV_BS for i in range(L)], dtype=torch.int32)
+    k, v = torch.randn(L, Hkv, D), torch.randn(L, Hkv, D)
+    write_kv_ref(k, v, slots, kc, vc)
+    k2, v2 = gather_kv_ref(kc, vc, blocks, L)
+    assert torch.equal(k, k2) and torch.equal(v, v2)
+
+
+def test_prefill_ref_chunked_equals_full():
+    torch.manual_seed(0)
+    Hq, Hkv, D, L = 4, 2, 32, 90
+    kc = torch.zeros(4, Hkv, KV_BS, D)
+    vc = torch.zeros(4, Hkv, D, KV_BS)
+    blocks = torch.tensor([[2, 1]], dtype=torch.int32)
+    slots = torch.tensor([int(blocks[0, i // KV_BS]) * KV_BS + i % KV_BS for i in range(L)], dtype=torch.int32)
+    write_kv_ref(torch.randn(L, Hkv, D), torch.randn(L, Hkv, D), slots, kc, vc)
+    q = torch.randn(L, Hq, D)
+    s = 1 / math.sqrt(D)
+    full = ops.prefill(q, torch.tensor([0, L], dtype=torch.int32), torch.tensor([L], dtype=torch.int32), blocks,
+                       kc, vc, s)
+    # second chunk only (prefix-cache hit of 60 tokens)
+    tail = ops.prefill(q[60:], torch.tensor([0, L - 60], dtype=torch.int32), torch.tensor([L], dtype=torch.int32),
+                       blocks, kc, vc, s)
+    assert torch.allclose(full[60:], tail, atol=1e-5)
+    dec = ops.decode(q[-1:], torch.tensor([L], dtype=torch.int32), blocks, kc, vc, s)
+    assert torch.allclose(full[-1:], dec, atol=1e-5)
+
+
+def test_rope_matches_complex_rotation():
+    D, T = 8, 3
+    cs = ops.rope_cos_sin(D, 16, 10000.0)
+    Hq, Hkv = 1, 1
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D)
+    pos = torch.tensor([0, 1, 5], dtype=torch.int32)
+    kc = torch.zeros(1, Hkv, KV_BS, D)
+    vc = torch.zeros(1, Hkv, D, KV_BS)
+    q = ops.rope_kv_write(qkv, pos, cs, torch.tensor([0, 1, 2], dtype=torch.int32), kc, vc, Hq, Hkv, D)
+    x = qkv[:, :D]
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2).double() / D))
+    for t in range(T):
+        c = torch.complex(x[t, : D // 2].double(), x[t, D // 2:].double()) * torch.exp(1j * pos[t].double() * inv)
+        assert torch.allclose(q[t, 0], torch.cat([c.real, c.imag]).float(), atol=1e-5)
+
+
+def test_llama3_rope_scaling_changes_low_freqs_only():
+    a = ops.attention.rope_inv_freq(128, 500000.0)
+    b = ops.attention.rope_inv_freq(128, 500000.0, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                                    "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    assert torch.allclose(a[:10], b[:10]) and (b[-5:] < a[-5:]).all()
+
+
+def test_sampler_ref_greedy_and_topk_mask():
+    lg = torch.randn(3, 50)
+    ids = ops.sample(lg, torch.zeros(3), torch.zeros(3, dtype=torch.int64))
+    assert ids.tolist() == lg.argmax(-1).tolist()
+    m = ops.apply_top_k_top_p(lg, torch.tensor([2, 0, 0]), torch.tensor([1.0, 1.0, 1e-6]))
+    assert torch.isfinite(m[0]).sum() == 2 and torch.isfinite(m[1]).sum() == 50 and torch.isfinite(m[2]).sum() == 1
+
+
+def test_filtered_topk_ref():
+    corpus = torch.nn.functional.normalize(torch.randn(100, 16), dim=-1)
+    users = torch.arange(100, dtype=torch.int32) % 4
+    dates = torch.arange(100, dtype=torch.int64)
+    q = corpus[[8, 9]].clone()
+    ids, sc, cnt = ops.filtered_topk(corpus, users, dates, q, torch.tensor([0, 1], dtype=torch.int32),
+                                     torch.tensor([0, 50], dtype=torch.int64), torch.tensor([3, 100]), 100)
+    assert ids[0, 0] == 8 and cnt[0] == 3
+    assert cnt[1] == 12 and (ids[1, :12] >= 50).all() and (ids[1, :12] % 4 == 1).all()
