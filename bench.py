@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Headline benchmark: chat turns/sec + p50 TTFT, Llama-3-8B RAG agent on 1/2/4/8 MI355X.
+
+Metric/config from BASELINE.json.  Each GPU runs one engine replica (data parallel, one process
+per GPU over torch.distributed/RCCL, launched by torchrun) serving its own closed-loop population
+of ``--convs`` synthetic conversations through the FULL serving path (Kafka-fake ingest ->
+agent decide [Llama-3-8B] -> retrieval [bge-base-en + 1M-vector filtered top-k] -> streamed
+respond [Llama-3-8B] -> Kafka-fake egress + Mongo-fake save).  Weights are random-init bf16 of
+the real architectures; data are synthetic (no network).
+
+One step = one wave of ``--convs`` concurrent turns per GPU (weak scaling: per-GPU work fixed).
+``value`` = whole-job completed turns / max-over-ranks wall time of the K timed waves.
+
+    python bench.py --gpus 1 --steps 3 --warmup 1
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 3 --warmup 1
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import time
+
+METRIC = "chat turns/sec + p50 TTFT, Llama-3-8B RAG agent at 1/2/4/8 MI355X"
+
+
+def log(msg: str) -> None:
+    print(f"[bench r{os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--convs", type=int, default=64, help="concurrent conversations per GPU")
+    ap.add_argument("--respond-tokens", type=int, default=128)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--embed-model", default="bge-base-en")
+    ap.add_argument("--corpus", type=int, default=1_000_000)
+    ap.add_argument("--users", type=int, default=10_000)
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args(argv)
+
+
+async def run(args, ps):
+    import torch
+
+    from financial_chatbot_llm_amd.bench.workload import RagWorkload, decide_script
+    from financial_chatbot_llm_amd.config import EngineConfig
+    from financial_chatbot_llm_amd.engine.async_engine import AsyncEngine
+    from financial_chatbot_llm_amd.engine.backend import EngineLLM
+    from financial_chatbot_llm_amd.parallel.dist import barrier
+    from financial_chatbot_llm_amd.retrieval import BgeEmbedder, DeviceVectorStore, RetrievalService
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t0 = time.perf_counter()
+    embedder = BgeEmbedder(args.embed_model, device=str(dev), seed=ps.rank)
+    store = DeviceVectorStore(embedder.dim, device=str(dev))
+    store.load_synthetic(args.corpus, args.users, seed=ps.rank)
+    retrieval = RetrievalService(embedder, store)
+    log(f"retrieval ready ({args.corpus} vectors) in {time.perf_counter() - t0:.1f}s")
+
+    sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
+    ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
+                        max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
+                        graph_batch_sizes=sizes, seed=0, device="cuda")
+    engine = AsyncEngine(ecfg)
+    log(f"engine ready in {time.perf_counter() - t0:.1f}s")
+    llm = EngineLLM(engine, max_model_len=args.max_model_len, decide_script=decide_script,
+                    respond_ignore_eos=True, respond_tokens=args.respond_tokens)
+    wl = RagWorkload(llm, retrieval, args.convs, args.users, args.respond_tokens, rank=ps.rank)
+    wl.kafka.setup_consumer()
+    consumer = asyncio.create_task(wl.worker.consume_messages())
+
+    for w in range(args.warmup):
+        r = await wl.run_wave()
+        log(f"warmup wave {w}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals}")
+
+    torch.cuda.synchronize()
+    barrier()
+    t_start = time.perf_counter()
+    results = []
+    for k in range(args.steps):
+        r = await wl.run_wave()
+        results.append(r)
+        log(f"wave {k}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals} "
+            f"ttft_p50={1e3 * statistics.median(r.ttfts) if r.ttfts else float('nan'):.0f}ms")
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    wl.worker.stop()
+    await consumer
+    stats = engine.stats()
+    engine.shutdown()
+    return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
+            "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
+            "engine": stats}
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    os.environ.setdefault("LOG_LEVEL", "WARNING")
+    import torch
+    import torch.distributed as dist
+
+    from financial_chatbot_llm_amd.parallel.dist import init_distributed
+    ps = init_distributed(tp_size=1)
+    if ps.world_size != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ps.world_size}")
+    res = asyncio.run(run(args, ps))
+    if ps.world_size > 1:
+        allr = [None] * ps.world_size
+        dist.all_gather_object(allr, res)
+    else:
+        allr = [res]
+    if ps.rank == 0:
+        tmax = max(r["elapsed"] for r in allr)
+        turns = sum(r["turns"] for r in allr)
+        ttfts = sorted(t for r in allr for t in r["ttfts"])
+        p50 = statistics.median(ttfts) * 1e3 if ttfts else None
+        p99 = ttfts[min(len(ttfts) - 1, int(0.99 * len(ttfts)))] * 1e3 if ttfts else None
+        value = turns / tmax
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "turns/s", "n_gpus": ps.world_size,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / max(args.steps, 1), 1),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic conversations + 1M-vector synthetic corpus; random-init weights of the real architectures",
+            "config": {"model": "Llama-3-8B", "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
+                       "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
+                       "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
+                       "parallelism": f"dp{ps.world_size}"},
+            "p50_ttft_ms": None if p50 is None else round(p50, 1),
+            "p99_ttft_ms": None if p99 is None else round(p99, 1),
+            "turn_errors": sum(r["errors"] for r in allr),
+            "retrieval_turns": sum(r["retrievals"] for r in allr),
+            "engine_rank0": allr[0]["engine"],
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    if ps.world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

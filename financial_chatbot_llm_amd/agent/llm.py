@@ -43,7 +43,7 @@ class LLMBackend:
 
 
 _RETRIEVAL_CUES = re.compile(
-    r"\b(spen[dt]|spending|transactions?|purchases?|bought|paid|pay|charges?|groceries|grocery|"
+    r"\b(spen[dt]|spending|transactions?|purchases?|bought|paid|charges?|groceries|grocery|"
     r"subscriptions?|expenses?|bills?|merchant|last (week|month)|yesterday|days? ago)\b", re.I)
 _DAYS = re.compile(r"\b(\d+)\s+days?\b", re.I)
 

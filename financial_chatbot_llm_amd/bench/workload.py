@@ -1,0 +1,126 @@
+"""Synthetic RAG chat workload driven through the FULL serving path.
+
+One "step" = one wave of ``C`` concurrent chat turns (one per synthetic conversation):
+
+    user message -> Mongo (history) + Kafka ``user_message``
+      -> ChatWorker.process_message -> LLMAgent
+           decide  : Llama-3 generation over the tool prompt (tool call teacher-forced: random
+                     weights cannot emit valid JSON), prefix-cached
+           retrieve: bge-base-en query embedding (GPU) + filtered top-k over a 1M-vector
+                     HBM corpus (HIP K15)                          [every other turn]
+           respond : streamed Llama-3 generation, fixed length (ignore EOS)
+      -> Kafka ``ai_response`` chunks + complete, reply saved to Mongo
+
+Turns/s counts completed turns (``complete`` event); TTFT is receipt -> first
+``response_chunk`` (SURVEY §6 metric definitions).
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as _dt
+import json
+import random
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from .. import config
+from ..adapters import Database, InMemoryBroker, KafkaClient
+from ..agent import LLMAgent, scripted_decision
+from ..agent.toolcall import format_tool_call
+from ..retrieval import RetrievalService
+from ..retrieval.store import MERCHANTS, user_name
+from ..serving.worker import ChatWorker
+from ..tools import make_plot_tool, make_retrieval_tool
+
+ADVICE_QUESTIONS = [
+    "How should I invest for retirement given my income?",
+    "Should I pay off my student loans faster or invest more?",
+    "How big should my emergency fund be?",
+    "Can you help me build a monthly budget plan?",
+    "Is it a good idea to open a Roth IRA this year?",
+]
+SPEND_QUESTIONS = [
+    "What did I spend on groceries last month?",
+    "How much did I spend on dining in the last 30 days?",
+    "Show me my recent transactions at Amazon.",
+    "How much did I spend two days ago?",
+    "What were my biggest purchases last week?",
+]
+
+
+def context_doc(i: int, user: str, rng: random.Random) -> Dict:
+    accounts = [{"account_id": f"acc-{i}-{k}", "balances": {"available": None, "current": round(rng.uniform(100, 20000), 2),
+                                                           "limit": None, "iso_currency_code": "USD"},
+                 "mask": f"{rng.randint(1000, 9999)}", "name": n, "official_name": n, "subtype": s, "type": t}
+                for k, (n, s, t) in enumerate([("Plaid Checking", "checking", "depository"),
+                                               ("Plaid Saving", "savings", "depository"),
+                                               ("Plaid Credit Card", "credit card", "credit")])]
+    expenses = [{"name": n, "amount": a, "description": d} for n, a, d in
+                [("Rent", rng.randint(1200, 3500), "apartment"), ("Car payment", rng.randint(200, 600), ""),
+                 ("Gym", 45, ""), ("Phone", 70, "family plan")]]
+    return {"conversation_id": f"conv-{i:05d}", "user_id": user, "name": f"User {i}",
+            "income": rng.randint(3000, 15000), "savings_goal": rng.randint(200, 3000),
+            "accounts": accounts, "additional_monthly_expenses": expenses}
+
+
+@dataclass
+class WaveResult:
+    seconds: float
+    ttfts: List[float]
+    turns: int
+    errors: int
+    retrievals: int
+
+
+class RagWorkload:
+    """Owns the fakes, the worker and the synthetic conversations for one GPU replica."""
+
+    def __init__(self, llm, retrieval: RetrievalService, num_convs: int, num_users: int,
+                 respond_tokens: int, seed: int = 0, rank: int = 0):
+        self.rng = random.Random(seed * 7919 + rank)
+        self.broker = InMemoryBroker(num_partitions=16)
+        self.db = Database(uri="")
+        self.kafka = KafkaClient(broker=self.broker)
+        self.agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
+                              max_response_tokens=respond_tokens)
+        self.worker = ChatWorker(self.db, self.kafka, self.agent, max_concurrent_turns=4 * num_convs)
+        self.convs = []
+        for i in range(num_convs):
+            uid = user_name(self.rng.randrange(num_users))
+            doc = context_doc(rank * 100000 + i, uid, self.rng)
+            self.db.put_context(doc)
+            self.convs.append(doc)
+        self.ts = 1_700_000_000
+        self.wave_idx = 0
+
+    async def _send_wave(self) -> None:
+        for i, doc in enumerate(self.convs):
+            pool = SPEND_QUESTIONS if (i + self.wave_idx) % 2 == 0 else ADVICE_QUESTIONS
+            text = pool[(i // 2 + self.wave_idx) % len(pool)]
+            self.ts += 1
+            self.db.put_user_message(doc["conversation_id"], text, doc["user_id"], self.ts)
+            self.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key=doc["conversation_id"],
+                                        value=json.dumps({"message": text, "conversation_id": doc["conversation_id"],
+                                                          "user_id": doc["user_id"]}))
+        self.wave_idx += 1
+
+    async def run_wave(self) -> WaveResult:
+        n0 = len(self.worker.traces)
+        t0 = time.perf_counter()
+        await self._send_wave()
+        target = n0 + len(self.convs)
+        while len(self.worker.traces) < target:
+            await asyncio.sleep(0.002)
+        dt = time.perf_counter() - t0
+        traces = self.worker.traces[n0:target]
+        return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
+                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces))
+
+
+def decide_script(messages, tools) -> str:
+    """Scripted decision for random-weight benchmarking: the reference's few-shot rule set."""
+    call = scripted_decision(messages[-1].content) if messages else None
+    if call is None or not any(t.name == call.name for t in tools):
+        return "No tool call"
+    return format_tool_call(call)

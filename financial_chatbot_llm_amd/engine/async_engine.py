@@ -1,0 +1,138 @@
+"""Asyncio front-end for the engine: one background thread owns the GPU and steps continuously.
+
+Every concurrent chat turn (decide call, respond stream) is a request in the SAME continuous
+batch.  Submissions and aborts cross into the engine thread through a lock-protected queue; per
+request outputs come back to the event loop with ``call_soon_threadsafe``.  The event loop never
+blocks on the GPU, so ``/health`` and Kafka polling stay responsive while the engine runs
+(the reference blocks its loop on every LLM call).
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import threading
+import time
+from typing import AsyncIterator, Dict, List, Optional, Sequence as Seq, Tuple
+
+from ..config import EngineConfig
+from ..utils.logging import get_logger
+from ..utils.metrics import METRICS
+from .llm_engine import LLMEngine, StepOutput
+from .sequence import SamplingParams
+
+logger = get_logger(__name__)
+_rid = itertools.count()
+
+
+class AsyncEngine:
+    def __init__(self, cfg: Optional[EngineConfig] = None, engine: Optional[LLMEngine] = None, start: bool = True,
+                 warmup: bool = True):
+        self.engine = engine or LLMEngine(cfg or EngineConfig.from_env())
+        if warmup:
+            self.engine.warmup()
+        self.tokenizer = self.engine.tokenizer
+        self._lock = threading.Lock()
+        self._wake = threading.Event()
+        self._pending: List[Tuple[str, Seq[int], SamplingParams]] = []
+        self._aborts: List[str] = []
+        self._sinks: Dict[str, Tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
+        self._stop = False
+        self.error: Optional[BaseException] = None
+        self.step_times: List[float] = []
+        self._thread = threading.Thread(target=self._loop, name="penny-engine", daemon=True)
+        if start:
+            self._thread.start()
+
+    # -- engine thread ---------------------------------------------------------------------
+    def _loop(self) -> None:
+        eng = self.engine
+        if eng.device.type == "cuda":
+            import torch
+            torch.cuda.set_device(eng.device)
+        while not self._stop:
+            with self._lock:
+                pending, self._pending = self._pending, []
+                aborts, self._aborts = self._aborts, []
+            for rid in aborts:
+                eng.abort(rid)
+            for rid, ids, params in pending:
+                try:
+                    eng.add_request(rid, ids, params)
+                except Exception as e:  # noqa: BLE001
+                    self._emit(rid, e)
+            if not eng.has_work():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                t0 = time.perf_counter()
+                outs = eng.step()
+                self.step_times.append(time.perf_counter() - t0)
+                if len(self.step_times) > 4096:
+                    del self.step_times[:2048]
+            except BaseException as e:  # noqa: BLE001 - surface GPU errors to every waiter
+                logger.exception("engine step failed")
+                self.error = e
+                for rid in list(self._sinks):
+                    self._emit(rid, e)
+                    eng.abort(rid)
+                continue
+            for o in outs:
+                self._emit(o.request_id, o)
+        eng.stop_followers()
+
+    def _emit(self, rid: str, item) -> None:
+        sink = self._sinks.get(rid)
+        if sink is None:
+            return
+        loop, q = sink
+        try:
+            loop.call_soon_threadsafe(q.put_nowait, item)
+        except RuntimeError:  # loop closed
+            self._sinks.pop(rid, None)
+
+    # -- public API --------------------------------------------------------------------------
+    async def generate(self, prompt_ids: Seq[int], params: SamplingParams,
+                       request_id: Optional[str] = None) -> AsyncIterator[StepOutput]:
+        rid = request_id or f"req-{next(_rid)}"
+        q: asyncio.Queue = asyncio.Queue()
+        self._sinks[rid] = (asyncio.get_running_loop(), q)
+        with self._lock:
+            self._pending.append((rid, list(prompt_ids), params))
+        self._wake.set()
+        done = False
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    done = True
+                    raise item
+                done = item.finished
+                yield item
+                if done:
+                    return
+        finally:
+            self._sinks.pop(rid, None)
+            if not done:  # consumer went away mid-stream (timeout / disconnect): free the KV
+                with self._lock:
+                    self._aborts.append(rid)
+                self._wake.set()
+
+    async def generate_all(self, prompt_ids: Seq[int], params: SamplingParams) -> StepOutput:
+        last = None
+        async for o in self.generate(prompt_ids, params):
+            last = o
+        return last
+
+    def stats(self) -> Dict[str, float]:
+        s = self.engine.stats()
+        if self.step_times:
+            st = sorted(self.step_times[-512:])
+            s["step_p50_ms"] = 1e3 * st[len(st) // 2]
+        return s
+
+    def shutdown(self) -> None:
+        self._stop = True
+        self._wake.set()
+        if self._thread.is_alive():
+            self._thread.join(timeout=30)

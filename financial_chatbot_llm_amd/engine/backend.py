@@ -1,0 +1,74 @@
+"""Agent backend on the local engine (replaces ``ChatGoogleGenerativeAI`` chains, llm_agent.py:34-45).
+
+* decide (``agenerate``): chat-templated prompt with the tool declarations, full generation,
+  tool-call JSON parsed from the text (``agent.toolcall``).
+* respond (``astream``): incremental detokenisation of the token stream into text deltas.
+
+``decide_script`` (benchmarks / demos with random weights) supplies the decide step's text per
+turn; the engine still runs every forward pass and teacher-forces those tokens (forced decoding),
+so the compute matches a real model producing that output (SURVEY §6 'scripted tool decision').
+"""
+from __future__ import annotations
+
+from typing import AsyncIterator, Callable, Optional, Sequence
+
+from ..agent.llm import LLMBackend, LLMResult
+from ..agent.toolcall import parse_tool_calls
+from ..tools.base import Tool
+from ..wire import ChatMessage
+from .async_engine import AsyncEngine
+from .chat_template import encode_chat
+from .sequence import SamplingParams
+from .tokenizer import IncrementalDetokenizer
+
+
+class EngineLLM(LLMBackend):
+    def __init__(self, engine: AsyncEngine, max_model_len: int = 8192,
+                 decide_script: Optional[Callable[[Sequence[ChatMessage], Sequence[Tool]], str]] = None,
+                 respond_ignore_eos: bool = False, respond_tokens: Optional[int] = None,
+                 stream_chunk_tokens: int = 1):
+        self.engine = engine
+        self.tok = engine.tokenizer
+        self.max_model_len = max_model_len
+        self.decide_script = decide_script
+        self.respond_ignore_eos = respond_ignore_eos
+        self.respond_tokens = respond_tokens
+        self.stream_chunk_tokens = max(1, stream_chunk_tokens)
+        self.eot = self.tok.special.get("<|eot_id|>")
+        self.last_prompt_tokens = 0
+
+    def _encode(self, messages, tools, max_tokens) -> list:
+        ids = encode_chat(self.tok, messages, tools, max_prompt_tokens=self.max_model_len - max_tokens - 1)
+        self.last_prompt_tokens = len(ids)
+        return ids
+
+    async def agenerate(self, messages, tools=None, temperature=0.5, max_tokens=256, **kw) -> LLMResult:
+        tools = list(tools or [])
+        ids = self._encode(messages, tools, max_tokens)
+        forced = None
+        if self.decide_script is not None:
+            text = self.decide_script(messages, tools)
+            forced = self.tok.encode(text, allow_special=False)[: max_tokens - 1] + ([self.eot] if self.eot is not None else [])
+        params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced)
+        out = await self.engine.generate_all(ids, params)
+        text = self.tok.decode(out.seq.output_ids)
+        return LLMResult(text=text, tool_calls=parse_tool_calls(text, tools), prompt_tokens=len(ids),
+                         completion_tokens=len(out.seq.output_ids))
+
+    async def astream(self, messages, temperature=0.5, max_tokens=512, **kw) -> AsyncIterator[str]:
+        n = self.respond_tokens or max_tokens
+        ids = self._encode(messages, None, n)
+        params = SamplingParams(temperature=temperature, max_tokens=n, ignore_eos=self.respond_ignore_eos)
+        detok = IncrementalDetokenizer(self.tok)
+        buf, k = [], 0
+        async for o in self.engine.generate(ids, params):
+            buf.append(detok.push(o.new_token_ids))
+            k += 1
+            if k % self.stream_chunk_tokens == 0 or o.finished:
+                text = "".join(buf)
+                buf = []
+                if text:
+                    yield text
+        tail = detok.flush()
+        if tail:
+            yield tail

@@ -1,0 +1,167 @@
+"""Synchronous engine core: model + paged KV pool + scheduler + runner, stepped by the caller.
+
+One :class:`LLMEngine` serves one TP group (a DP replica).  On TP>1 only the group leader runs
+the scheduler; each step it broadcasts the packed :class:`StepInputs` (C4) and every rank runs
+the identical forward (``follower_loop`` on the other ranks).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence as Seq
+
+import torch
+
+from ..config import EngineConfig
+from ..models import build_model
+from ..models.common import KVCache
+from ..ops.attention import KV_BS
+from ..parallel import comm
+from ..parallel.dist import state as pstate
+from ..utils.logging import get_logger
+from .block_manager import make_block_manager
+from .model_runner import ModelRunner, build_step_inputs
+from .scheduler import Scheduler
+from .sequence import SamplingParams, Sequence
+from .tokenizer import BaseTokenizer, load_tokenizer
+
+logger = get_logger(__name__)
+
+
+@dataclass
+class StepOutput:
+    request_id: str
+    new_token_ids: List[int]
+    finished: bool
+    finish_reason: Optional[str]
+    seq: Sequence
+
+
+def plan_kv_blocks(cfg: EngineConfig, model, device) -> int:
+    if cfg.num_kv_blocks:
+        return cfg.num_kv_blocks
+    per_block = KVCache.bytes_per_block(model.cfg.num_layers, model.hkv, model.D)
+    if device.type != "cuda":
+        return max(64, (cfg.max_num_seqs * cfg.max_model_len // KV_BS) // 8)
+    free, _ = torch.cuda.mem_get_info(device)
+    reserve = 6 << 30  # activations, hipBLASLt workspaces, graph pools
+    n = int(max(free - reserve, 0) * cfg.kv_mem_fraction) // per_block
+    return max(n, 16)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model=None, tokenizer: Optional[BaseTokenizer] = None):
+        self.cfg = cfg
+        device = torch.device(cfg.device if (cfg.device != "cuda" or torch.cuda.is_available()) else "cpu")
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        t0 = time.perf_counter()
+        self.model = model if model is not None else build_model(cfg, device)
+        self.tokenizer = tokenizer or load_tokenizer(cfg.tokenizer, self.model.cfg.vocab_size)
+        self.eos_ids = set(self.tokenizer.eos_ids)
+        nblocks = plan_kv_blocks(cfg, self.model, device)
+        self.kv = KVCache(self.model.cfg.num_layers, nblocks, self.model.hkv, self.model.D, device=device)
+        self.bm = make_block_manager(nblocks, KV_BS, cfg.enable_prefix_caching)
+        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
+                                  use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes)
+        self.requests: Dict[str, Sequence] = {}
+        self.ps = pstate()
+        logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
+                    f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
+                    f"init={time.perf_counter() - t0:.1f}s")
+
+    # ------------------------------------------------------------------------------------
+    def add_request(self, request_id: str, prompt_ids: Seq[int], params: SamplingParams) -> Sequence:
+        if not prompt_ids:
+            raise ValueError("empty prompt")
+        max_prompt = self.cfg.max_model_len - 1
+        seq = Sequence(request_id, list(prompt_ids)[-max_prompt:], params)
+        self.requests[request_id] = seq
+        self.scheduler.add(seq)
+        return seq
+
+    def abort(self, request_id: str) -> None:
+        seq = self.requests.pop(request_id, None)
+        if seq is not None and not seq.finished:
+            self.scheduler.abort(seq)
+            seq.finish_reason = "abort"
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    def warmup(self) -> None:
+        """Capture decode graphs (all TP ranks must call this together)."""
+        if self.runner.use_graphs:
+            self.runner.capture_graphs()
+
+    def step(self) -> List[StepOutput]:
+        batch = self.scheduler.schedule()
+        if batch.empty():
+            return []
+        si = build_step_inputs(batch)
+        if self.ps.tp_size > 1:
+            comm.broadcast_object(si)
+        sampled = self.runner.execute(si)
+        now = time.perf_counter()
+        outs: List[StepOutput] = []
+        for seq, start, n in batch.prefill:
+            seq.num_computed = start + n
+        for seq in batch.decode:
+            seq.num_computed = seq.num_tokens
+        # sampled order: completed prefills (in batch order), then decodes
+        samplers = [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
+        for seq, tok in zip(samplers, sampled):
+            forced = seq.params.forced_output
+            k = len(seq.output_ids)
+            if forced is not None and k < len(forced):
+                tok = forced[k]
+            seq.output_ids.append(int(tok))
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            reason = None
+            if len(seq.output_ids) >= seq.params.max_tokens:
+                reason = "length"
+            elif forced is not None and len(seq.output_ids) >= len(forced) and not seq.params.ignore_eos:
+                reason = "stop"
+            elif not seq.params.ignore_eos and (tok in self.eos_ids or tok in seq.params.stop_token_ids):
+                reason = "stop"
+            elif seq.num_tokens >= self.cfg.max_model_len:
+                reason = "length"
+            if reason is None:
+                self.bm.commit(seq)
+            else:
+                self.bm.commit(seq)
+                self.scheduler.finish(seq, reason)
+                self.requests.pop(seq.request_id, None)
+            outs.append(StepOutput(seq.request_id, [int(tok)], reason is not None, reason, seq))
+        for seq, start, n in batch.prefill:
+            if start + n < seq.num_tokens:
+                self.bm.commit(seq)
+        return outs
+
+    def follower_loop(self) -> None:
+        """Non-leader TP ranks: replay the leader's steps until it broadcasts None."""
+        while True:
+            si = comm.broadcast_object(None)
+            if si is None:
+                return
+            self.runner.execute(si)
+
+    def stop_followers(self) -> None:
+        if self.ps.tp_size > 1 and self.ps.is_tp_leader:
+            comm.broadcast_object(None)
+
+    # -- convenience --------------------------------------------------------------------
+    def generate(self, prompts: Seq[Seq[int]], params: SamplingParams) -> List[List[int]]:
+        seqs = [self.add_request(f"gen-{i}-{id(p)}", p, params) for i, p in enumerate(prompts)]
+        while any(not s.finished for s in seqs):
+            self.step()
+        return [s.output_ids for s in seqs]
+
+    def stats(self) -> Dict[str, float]:
+        return {"running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
+                "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
+                "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
+                "tokens": self.runner.stats["tokens"]}

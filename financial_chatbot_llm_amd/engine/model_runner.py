@@ -1,0 +1,280 @@
+"""Executes scheduled batches on the GPU: input prep, forward, logits, sampling, hipGraph decode.
+
+Per step the host packs one int32 staging buffer (token ids, positions, KV slots, context
+lengths, block tables, sampling seeds) and ships it with ONE pinned H2D copy; the forward then
+runs without further host round-trips, and the only D2H sync is the sampled ids.
+
+Pure-decode steps (the hot loop: one token per running sequence) replay a hipGraph captured
+per batch-size bucket (``torch.cuda.graph`` records hipGraph on ROCm): the ~10 kernels x L
+layers of a decode step become one launch, removing ~1.5 us x 300+ launch gaps per token
+(SURVEY §7.4).  Padding rows of a bucket write no KV (slot -1) and their outputs are dropped.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.common import AttentionMetadata, KVCache
+from ..ops.attention import KV_BS, DecodeWorkspace
+from ..parallel import comm
+from ..utils.logging import get_logger
+from .scheduler import ScheduledBatch
+from .sequence import Sequence
+
+logger = get_logger(__name__)
+
+
+@dataclass
+class StepInputs:
+    """Host-side description of one forward (also what the TP leader broadcasts, C4)."""
+
+    ids: np.ndarray                 # [T]
+    positions: np.ndarray           # [T]
+    slots: np.ndarray               # [T]
+    cu_q: np.ndarray                # [Sp+1]
+    ctx_p: np.ndarray               # [Sp]
+    bt_p: np.ndarray                # [Sp, W]
+    max_q_len: int
+    ctx_d: np.ndarray               # [Bd]
+    bt_d: np.ndarray                # [Bd, W]
+    logits_idx: np.ndarray          # [S] rows whose next token is sampled
+    temps: np.ndarray               # [S] f32
+    seeds: np.ndarray               # [S] int64
+    top_k: np.ndarray               # [S]
+    top_p: np.ndarray               # [S]
+
+    @property
+    def num_prefill_tokens(self) -> int:
+        return int(self.cu_q[-1]) if len(self.cu_q) else 0
+
+    @property
+    def num_decode(self) -> int:
+        return len(self.ctx_d)
+
+
+def _slots(seq: Sequence, start: int, n: int) -> List[int]:
+    bt = seq.block_table
+    return [bt[p // KV_BS] * KV_BS + p % KV_BS for p in range(start, start + n)]
+
+
+def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
+    ids: List[int] = []
+    pos: List[int] = []
+    slots: List[int] = []
+    cu = [0]
+    ctx_p, tables_p = [], []
+    logits_idx, temps, seeds, tk, tp = [], [], [], [], []
+    max_q = 0
+    for seq, start, n in batch.prefill:
+        all_ids = seq.all_ids
+        ids.extend(all_ids[start:start + n])
+        pos.extend(range(start, start + n))
+        slots.extend(_slots(seq, start, n))
+        cu.append(cu[-1] + n)
+        ctx_p.append(start + n)
+        tables_p.append(seq.block_table)
+        max_q = max(max_q, n)
+        if start + n == seq.num_tokens:
+            logits_idx.append(cu[-1] - 1)
+            temps.append(seq.params.temperature)
+            seeds.append(seq.step_seed())
+            tk.append(seq.params.top_k)
+            tp.append(seq.params.top_p)
+    Tp = cu[-1]
+    ctx_d, tables_d = [], []
+    for j, seq in enumerate(batch.decode):
+        p = seq.num_tokens - 1
+        ids.append(seq.all_ids[-1])
+        pos.append(p)
+        slots.extend(_slots(seq, p, 1))
+        ctx_d.append(seq.num_tokens)
+        tables_d.append(seq.block_table)
+        logits_idx.append(Tp + j)
+        temps.append(seq.params.temperature)
+        seeds.append(seq.step_seed())
+        tk.append(seq.params.top_k)
+        tp.append(seq.params.top_p)
+
+    def table(rows):
+        w = max((len(r) for r in rows), default=1) or 1
+        out = np.zeros((len(rows), w), np.int32)
+        for i, r in enumerate(rows):
+            out[i, :len(r)] = r
+        return out
+
+    i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
+    return StepInputs(i32(ids), i32(pos), i32(slots), i32(cu), i32(ctx_p), table(tables_p), max_q, i32(ctx_d),
+                      table(tables_d), np.asarray(logits_idx, np.int64), np.asarray(temps, np.float32),
+                      np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32))
+
+
+class _DecodeGraph:
+    def __init__(self, graph, B: int, out: torch.Tensor):
+        self.graph, self.B, self.out = graph, B, out
+
+
+class ModelRunner:
+    def __init__(self, model, kv: KVCache, max_model_len: int, max_decode_batch: int = 256,
+                 use_graphs: bool = True, graph_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 32, 64, 128, 256)):
+        self.model = model
+        self.kv = kv
+        self.device = model.device
+        self.max_model_len = max_model_len
+        self.max_blocks = (max_model_len + KV_BS - 1) // KV_BS
+        self.on_gpu = self.device.type == "cuda"
+        self.use_graphs = use_graphs and self.on_gpu
+        self.graph_sizes = tuple(sorted(s for s in graph_sizes if s <= max_decode_batch))
+        self.max_decode_batch = max(self.graph_sizes) if self.graph_sizes else max_decode_batch
+        cfg = model.cfg
+        self.decode_ws = DecodeWorkspace.create(max(max_decode_batch, 1), model.hq, model.D, max_model_len,
+                                                self.device) if self.on_gpu else None
+        self.graphs: Dict[int, _DecodeGraph] = {}
+        self._static = None
+        self.graph_pool = None
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+
+    # ------------------------------------------------------------------------------------
+    # eager path
+    # ------------------------------------------------------------------------------------
+    def _to_dev(self, a: np.ndarray, dtype=None) -> torch.Tensor:
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if self.on_gpu:
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t if dtype is None else t.to(dtype)
+
+    def _meta(self, si: StepInputs, slots: torch.Tensor) -> AttentionMetadata:
+        m = AttentionMetadata(slots=slots, num_prefill_tokens=si.num_prefill_tokens, num_decode=si.num_decode,
+                              decode_ws=self.decode_ws)
+        if si.num_prefill_tokens:
+            m.cu_q = self._to_dev(si.cu_q)
+            m.ctx_lens_p = self._to_dev(si.ctx_p)
+            m.block_tables_p = self._to_dev(si.bt_p)
+            m.max_q_len = si.max_q_len
+        if si.num_decode:
+            m.ctx_lens_d = self._to_dev(si.ctx_d)
+            m.block_tables_d = self._to_dev(si.bt_d)
+        return m
+
+    def forward_logits(self, si: StepInputs) -> torch.Tensor:
+        ids = self._to_dev(si.ids)
+        pos = self._to_dev(si.positions)
+        slots = self._to_dev(si.slots)
+        meta = self._meta(si, slots)
+        h = self.model.forward(ids, pos, meta, self.kv)
+        idx = self._to_dev(si.logits_idx)
+        return self.model.logits(h.index_select(0, idx))
+
+    def sample(self, logits: torch.Tensor, si: StepInputs) -> torch.Tensor:
+        if (si.top_k > 0).any() or (si.top_p < 1).any():
+            logits = ops.apply_top_k_top_p(logits, torch.from_numpy(si.top_k).to(logits.device),
+                                           torch.from_numpy(si.top_p).to(logits.device))
+        temps = self._to_dev(si.temps)
+        seeds = self._to_dev(si.seeds)
+        return ops.sample(logits.contiguous(), temps, seeds)
+
+    def execute(self, si: StepInputs) -> List[int]:
+        """Run one step; returns the sampled token per entry of ``si.logits_idx``."""
+        self.stats["steps"] += 1
+        self.stats["tokens"] += len(si.ids)
+        if len(si.logits_idx) == 0:
+            self._forward_only(si)
+            return []
+        if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
+                and not (si.top_k > 0).any() and not (si.top_p < 1).any()):
+            return self._graph_decode(si)
+        logits = self.forward_logits(si)
+        out = self.sample(logits, si)
+        return out.cpu().tolist()
+
+    def _forward_only(self, si: StepInputs) -> None:
+        ids = self._to_dev(si.ids)
+        pos = self._to_dev(si.positions)
+        slots = self._to_dev(si.slots)
+        self.model.forward(ids, pos, self._meta(si, slots), self.kv)
+
+    # ------------------------------------------------------------------------------------
+    # hipGraph decode
+    # ------------------------------------------------------------------------------------
+    def _alloc_static(self) -> None:
+        B, W = self.max_decode_batch, self.max_blocks
+        # ids | pos | slots | ctx | block tables live in ONE device buffer fed by ONE pinned H2D copy
+        self._dev_i32 = torch.zeros(4 * B + B * W, dtype=torch.int32, device=self.device)
+        d = self._dev_i32
+        self._static = {
+            "ids": d[0:B], "pos": d[B:2 * B], "slots": d[2 * B:3 * B], "ctx": d[3 * B:4 * B],
+            "bt": d[4 * B:].view(B, W),
+            "temps": torch.zeros(B, dtype=torch.float32, device=self.device),
+            "seeds": torch.zeros(B, dtype=torch.int64, device=self.device),
+        }
+        self._static["slots"].fill_(-1)
+        self._static["ctx"].fill_(1)
+        self._pinned_i32 = torch.zeros(4 * B + B * W, dtype=torch.int32).pin_memory()
+        self._pinned_f = torch.zeros(B, dtype=torch.float32).pin_memory()
+        self._pinned_l = torch.zeros(B, dtype=torch.int64).pin_memory()
+
+    def _run_static(self, B: int) -> torch.Tensor:
+        s = self._static
+        meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
+                                 ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws)
+        h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
+        logits = self.model.logits(h)
+        return ops.sample(logits, s["temps"][:B], s["seeds"][:B])
+
+    def capture_graphs(self) -> None:
+        if not self.use_graphs:
+            return
+        if self._static is None:
+            self._alloc_static()
+        torch.cuda.synchronize()
+        for B in sorted(self.graph_sizes, reverse=True):
+            # warm up (allocator + hipBLASLt heuristics) outside the capture
+            for _ in range(2):
+                self._run_static(B)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                out = self._run_static(B)
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.graphs[B] = _DecodeGraph(g, B, out)
+        torch.cuda.synchronize()
+        logger.info(f"captured decode hipGraphs for batch sizes {sorted(self.graphs)}")
+
+    def _bucket(self, n: int) -> int:
+        for b in self.graph_sizes:
+            if b >= n:
+                return b
+        return self.graph_sizes[-1]
+
+    def _graph_decode(self, si: StepInputs) -> List[int]:
+        if not self.graphs:
+            self.capture_graphs()
+        n = si.num_decode
+        B = self._bucket(n)
+        G = self.graphs[B]
+        S, W = self.max_decode_batch, self.max_blocks
+        buf = self._pinned_i32.numpy()
+        # layout: ids | pos | slots | ctx | bt  (each section sized for the largest bucket)
+        buf[0:n] = si.ids
+        buf[S:S + n] = si.positions
+        buf[2 * S:2 * S + B] = -1
+        buf[2 * S:2 * S + n] = si.slots
+        buf[3 * S:3 * S + B] = 1
+        buf[3 * S:3 * S + n] = si.ctx_d
+        bt = buf[4 * S:4 * S + S * W].reshape(S, W)
+        bt[:B] = 0
+        bt[:n, :si.bt_d.shape[1]] = si.bt_d
+        self._pinned_f.numpy()[:n] = si.temps
+        self._pinned_l.numpy()[:n] = si.seeds
+        self._dev_i32.copy_(self._pinned_i32, non_blocking=True)
+        s = self._static
+        s["temps"].copy_(self._pinned_f, non_blocking=True)
+        s["seeds"].copy_(self._pinned_l, non_blocking=True)
+        G.graph.replay()
+        self.stats["graph_steps"] += 1
+        return G.out[:n].cpu().tolist()

@@ -1,0 +1,125 @@
+"""Continuous-batching scheduler with chunked prefill, prefix caching and preemption.
+
+Every step builds ONE flat batch: a decode token for every running sequence that has finished
+its prompt, plus prefill chunks (new or continuing prompts) filling the rest of the token
+budget.  The reference processes one chat turn per worker process at a time (``main.py:138``);
+here every in-flight turn of every conversation shares each forward pass.
+
+Memory: a sequence holds KV blocks for exactly its computed tokens (+ the step's new tokens).
+When the pool runs dry the youngest running sequence is preempted (blocks freed, re-queued at
+the front, recomputed later -- its full blocks usually come back from the prefix cache).
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Deque, List, Tuple
+
+from .sequence import Sequence, SeqStatus
+
+
+@dataclass
+class ScheduledBatch:
+    prefill: List[Tuple[Sequence, int, int]] = field(default_factory=list)  # (seq, start, n_tokens)
+    decode: List[Sequence] = field(default_factory=list)
+    preempted: List[Sequence] = field(default_factory=list)
+
+    @property
+    def num_prefill_tokens(self) -> int:
+        return sum(n for _, _, n in self.prefill)
+
+    @property
+    def num_tokens(self) -> int:
+        return self.num_prefill_tokens + len(self.decode)
+
+    def empty(self) -> bool:
+        return not self.prefill and not self.decode
+
+
+class Scheduler:
+    def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
+                 max_model_len: int = 8192, decode_first: bool = True):
+        self.bm = block_manager
+        self.max_num_seqs = max_num_seqs
+        self.max_num_batched_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.waiting: Deque[Sequence] = deque()
+        self.running: List[Sequence] = []
+
+    def add(self, seq: Sequence) -> None:
+        if seq.num_tokens >= self.max_model_len:
+            raise ValueError(f"prompt of {seq.num_tokens} tokens exceeds max_model_len {self.max_model_len}")
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def abort(self, seq: Sequence) -> None:
+        if seq in self.running:
+            self.running.remove(seq)
+            self.bm.free(seq)
+        elif seq in self.waiting:
+            self.waiting.remove(seq)
+            if seq.block_table:
+                self.bm.free(seq)
+        seq.status = SeqStatus.FINISHED
+
+    def _preempt(self, seq: Sequence, batch: ScheduledBatch) -> None:
+        self.running.remove(seq)
+        self.bm.free(seq)
+        seq.num_computed = 0
+        seq.status = SeqStatus.WAITING
+        seq.num_preemptions += 1
+        self.waiting.appendleft(seq)
+        batch.preempted.append(seq)
+
+    def schedule(self) -> ScheduledBatch:
+        batch = ScheduledBatch()
+        budget = self.max_num_batched_tokens
+        # 1) decodes (oldest first); preempt youngest when blocks run out
+        decodes = [s for s in self.running if s.remaining_prefill == 1]
+        for seq in sorted(decodes, key=lambda s: s.arrival):
+            if seq not in self.running:
+                continue
+            while not self.bm.can_grow(seq, seq.num_tokens):
+                victim = max(self.running, key=lambda s: s.arrival)
+                self._preempt(victim, batch)
+                if victim is seq:
+                    break
+            if seq not in self.running:
+                continue
+            self.bm.grow(seq, seq.num_tokens)
+            batch.decode.append(seq)
+            budget -= 1
+        # 2) continuing prefills
+        for seq in sorted((s for s in self.running if s.remaining_prefill > 1), key=lambda s: s.arrival):
+            if budget <= 0:
+                break
+            n = min(seq.remaining_prefill, budget)
+            if not self.bm.grow(seq, seq.num_computed + n):
+                continue
+            batch.prefill.append((seq, seq.num_computed, n))
+            budget -= n
+        # 3) admit waiting sequences
+        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+            seq = self.waiting[0]
+            if not seq.block_table:
+                self.bm.match_prefix(seq)
+            n = min(seq.remaining_prefill, budget)
+            if not self.bm.grow(seq, seq.num_computed + n):
+                if seq.block_table and not self.running:
+                    raise MemoryError("KV pool too small for a single prompt")
+                break
+            self.waiting.popleft()
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+            batch.prefill.append((seq, seq.num_computed, n))
+            budget -= n
+        return batch
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        if seq in self.running:
+            self.running.remove(seq)
+        self.bm.free(seq)

@@ -1,0 +1,74 @@
+"""Request / sequence state for the continuous-batching engine."""
+from __future__ import annotations
+
+import enum
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence as Seq
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.5            # reference: llm_agent.py:37,44
+    top_k: int = 0                      # 0 = disabled
+    top_p: float = 1.0
+    max_tokens: int = 256
+    ignore_eos: bool = False            # benchmarks force fixed decode lengths
+    stop_token_ids: Seq[int] = ()
+    seed: Optional[int] = None
+    forced_output: Optional[List[int]] = None   # teacher-forced continuation (scripted tool calls)
+
+
+class SeqStatus(enum.Enum):
+    WAITING = 0
+    RUNNING = 1
+    FINISHED = 2
+
+
+_ids = itertools.count()
+
+
+class Sequence:
+    def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams, arrival: Optional[float] = None):
+        self.seq_id = next(_ids)
+        self.request_id = request_id
+        self.prompt_ids = list(prompt_ids)
+        self.output_ids: List[int] = []
+        self.params = params
+        self.status = SeqStatus.WAITING
+        self.block_table: List[int] = []
+        self.num_computed = 0          # tokens whose KV is in the cache
+        self.num_cached_prompt = 0     # prefix-cache hit (tokens)
+        self.arrival = time.perf_counter() if arrival is None else arrival
+        self.first_token_time: Optional[float] = None
+        self.finish_reason: Optional[str] = None
+        self.seed = params.seed if params.seed is not None else (hash((request_id, self.seq_id)) & 0x7FFFFFFF)
+        self.num_preemptions = 0
+
+    @property
+    def all_ids(self) -> List[int]:
+        return self.prompt_ids + self.output_ids
+
+    def __len__(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self)
+
+    @property
+    def in_prefill(self) -> bool:
+        return self.num_computed < self.num_tokens - 1 or (self.num_computed == 0)
+
+    @property
+    def remaining_prefill(self) -> int:
+        return self.num_tokens - self.num_computed
+
+    @property
+    def finished(self) -> bool:
+        return self.status == SeqStatus.FINISHED
+
+    def step_seed(self) -> int:
+        """Per-token seed: depends only on the request and the position (batch-invariant)."""
+        return (self.seed * 0x9E3779B1 + len(self.output_ids) * 0x85EBCA77 + 1) & 0x7FFFFFFFFFFFFFFF

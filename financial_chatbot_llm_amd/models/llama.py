@@ -1,0 +1,169 @@
+"""Llama-3 decoder (8B / 70B) and the shared decoder skeleton used by Mixtral.
+
+Replaces the remote Gemini model of the reference (``llm_agent.py:34-45``) with a local
+decoder whose per-layer hot path is::
+
+    K2 add+RMSNorm -> K3 QKV GEMM (hipBLASLt) -> K4/K5 RoPE + paged KV write (HIP)
+    -> K6/K7 paged attention (HIP, MFMA) -> K8 O GEMM [-> C1 all-reduce]
+    -> K2 add+RMSNorm -> K9 gate|up GEMM -> SiLU*mul (HIP) -> K10 down GEMM [-> C1]
+
+Weights are plain bf16 tensors (``[out, in]``), sharded Megatron-style over the TP group:
+QKV/gate-up column-parallel (whole heads per rank), O/down row-parallel, embedding and LM head
+vocab-parallel.  The batch is flat: prefill tokens of several sequences followed by one token
+per decoding sequence (continuous batching); the attention split is described by
+:class:`~.common.AttentionMetadata`.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel import comm
+from ..parallel.dist import state as pstate
+from ..parallel.layers import shard_cols, shard_rows, shard_sections, vocab_range
+from .common import AttentionMetadata, KVCache, random_tensor
+from .configs import ModelConfig
+
+
+class DecoderModel:
+    """Llama-family decoder; subclasses override the MLP (Mixtral MoE)."""
+
+    def __init__(self, cfg: ModelConfig, device="cuda", tp_rank: Optional[int] = None,
+                 tp_size: Optional[int] = None, dtype=torch.bfloat16):
+        ps = pstate()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp_rank = ps.tp_rank if tp_rank is None else tp_rank
+        self.tp_size = ps.tp_size if tp_size is None else tp_size
+        if cfg.num_heads % self.tp_size or cfg.num_kv_heads % self.tp_size:
+            raise ValueError(f"heads {cfg.num_heads}/{cfg.num_kv_heads} not divisible by tp={self.tp_size}")
+        self.hq = cfg.num_heads // self.tp_size
+        self.hkv = cfg.num_kv_heads // self.tp_size
+        self.D = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.vocab_start, self.vocab_end = vocab_range(cfg.vocab_size, self.tp_rank, self.tp_size)
+        self.w: Dict[str, torch.Tensor] = {}
+        self.cos_sin = ops.rope_cos_sin(self.D, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
+                                        device=self.device)
+
+    # ------------------------------------------------------------------------------------
+    # weights
+    # ------------------------------------------------------------------------------------
+    def full_shapes(self) -> Dict[str, tuple]:
+        c = self.cfg
+        H, F_ = c.hidden_size, c.intermediate_size
+        shapes = {"embed": (c.vocab_size, H), "final_norm": (H,)}
+        if not c.tie_embeddings:
+            shapes["lm_head"] = (c.vocab_size, H)
+        for i in range(c.num_layers):
+            p = f"layers.{i}."
+            shapes[p + "in_norm"] = (H,)
+            shapes[p + "post_norm"] = (H,)
+            shapes[p + "qkv"] = (c.q_size + 2 * c.kv_size, H)
+            shapes[p + "o"] = (H, c.q_size)
+            shapes.update(self.mlp_shapes(p))
+        return shapes
+
+    def mlp_shapes(self, p: str) -> Dict[str, tuple]:
+        c = self.cfg
+        return {p + "gate_up": (2 * c.intermediate_size, c.hidden_size), p + "down": (c.hidden_size, c.intermediate_size)}
+
+    def shard(self, name: str, full: torch.Tensor) -> torch.Tensor:
+        """Full (unsharded) parameter -> this rank's shard."""
+        r, n, c = self.tp_rank, self.tp_size, self.cfg
+        leaf = name.rsplit(".", 1)[-1]
+        if n == 1:
+            return full
+        if leaf in ("embed", "lm_head"):
+            a, b = self.vocab_start, self.vocab_end
+            return full[a:b].contiguous()
+        if leaf == "qkv":
+            return shard_sections(full, [c.q_size, c.kv_size, c.kv_size], r, n)
+        if leaf in ("gate_up", "w13"):
+            half = full.shape[-2] // 2
+            if full.dim() == 3:  # [E, 2F, H]
+                return torch.cat([full[:, :half].chunk(n, 1)[r], full[:, half:].chunk(n, 1)[r]], 1).contiguous()
+            return shard_sections(full, [half, half], r, n)
+        if leaf in ("o", "down"):
+            return shard_cols(full, r, n)
+        if leaf == "w2":  # [E, H, F]
+            return full.chunk(n, 2)[r].contiguous()
+        return full
+
+    def init_random(self, seed: int = 0, std: float = 0.02) -> "DecoderModel":
+        for name, shape in self.full_shapes().items():
+            kind = "ones" if name.endswith("norm") else "normal"
+            full = random_tensor(name, shape, seed, self.device, self.dtype, std=std, kind=kind)
+            self.w[name] = self.shard(name, full)
+            del full
+        return self
+
+    def load_state(self, full_weights: Dict[str, torch.Tensor]) -> "DecoderModel":
+        for name, t in full_weights.items():
+            self.w[name] = self.shard(name, t.to(self.device, self.dtype)).contiguous()
+        missing = set(self.full_shapes()) - set(self.w)
+        if missing:
+            raise KeyError(f"missing weights: {sorted(missing)[:5]}...")
+        return self
+
+    def num_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.w.values())
+
+    # ------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------
+    def embed(self, ids: torch.Tensor) -> torch.Tensor:
+        x = ops.embedding(ids, self.w["embed"], self.vocab_start, self.vocab_end)
+        return comm.tp_all_reduce(x) if self.tp_size > 1 else x
+
+    def mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+        p = f"layers.{i}."
+        gu = F.linear(h, self.w[p + "gate_up"])
+        out = F.linear(ops.silu_mul(gu), self.w[p + "down"])
+        return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+
+    def attention(self, i: int, h: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata,
+                  kv: KVCache) -> torch.Tensor:
+        p = f"layers.{i}."
+        T = h.shape[0]
+        qkv = F.linear(h, self.w[p + "qkv"])
+        kc, vc = kv.k(i), kv.v(i)
+        q = ops.rope_kv_write(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv, self.D)
+        attn = torch.empty_like(q)
+        tp = meta.num_prefill_tokens
+        if tp > 0:
+            ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, self.scale,
+                        causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp])
+        if meta.num_decode > 0:
+            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
+                       workspace=meta.decode_ws, out=attn[tp:])
+        out = F.linear(attn.view(T, self.hq * self.D), self.w[p + "o"])
+        return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+
+    def forward(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata, kv: KVCache) -> torch.Tensor:
+        c = self.cfg
+        x = self.embed(ids)
+        residual = x
+        h = ops.rms_norm(x, self.w["layers.0.in_norm"], c.norm_eps)
+        for i in range(c.num_layers):
+            p = f"layers.{i}."
+            if i > 0:
+                h = ops.rms_norm(x, self.w[p + "in_norm"], c.norm_eps, residual=residual)
+            a = self.attention(i, h, positions, meta, kv)
+            h = ops.rms_norm(a, self.w[p + "post_norm"], c.norm_eps, residual=residual)
+            x = self.mlp(i, h)
+        return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
+
+    def logits(self, h: torch.Tensor) -> torch.Tensor:
+        w = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
+        out = F.linear(h, w)
+        return comm.tp_all_gather_last(out) if self.tp_size > 1 else out
+
+
+class LlamaModel(DecoderModel):
+    pass

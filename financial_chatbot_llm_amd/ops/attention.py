@@ -181,10 +181,10 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
     Hkv = k_cache.shape[1]
     if N.use_native(q):
         out = torch.empty_like(q) if out is None else out
-        if workspace is None:
+        if workspace is None or workspace.part_m.shape[0] < B or workspace.part_m.shape[1] < Hq:
             if max_ctx is None:
                 max_ctx = int(ctx_lens.max().item())
-            workspace = DecodeWorkspace.create(B, Hq, D, max_ctx, q.device)
+            workspace = DecodeWorkspace.create(B, Hq, D, max(max_ctx, 1), q.device)
         ws = workspace
         N.call("penny_attention_decode", N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache),
                N.ptr(v_cache), N.ptr(out), N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D,

@@ -1,0 +1,104 @@
+"""Process-group management: one process per GPU, torch.distributed over RCCL (backend "nccl").
+
+Topology: ``world = dp * tp``; ranks ``[d*tp, (d+1)*tp)`` form tensor-parallel group ``d``
+(consecutive ranks = directly xGMI-linked GPUs of one node), and ranks with equal TP rank form
+the data-parallel groups.  On CPU (tests) the same code runs on gloo.
+
+The reference has no distributed compute at all (its only parallelism is N
+gunicorn worker processes); DP replicas here are that same idea, one engine per GPU group.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    tp_group: Optional[object] = None
+    dp_group: Optional[object] = None
+    backend: str = "none"
+
+    @property
+    def is_tp_leader(self) -> bool:
+        return self.tp_rank == 0
+
+    @property
+    def tp_leader_rank(self) -> int:
+        return self.rank - self.tp_rank
+
+
+_STATE = ParallelState()
+
+
+def state() -> ParallelState:
+    return _STATE
+
+
+def set_state(s: ParallelState) -> None:
+    global _STATE
+    _STATE = s
+
+
+def init_distributed(tp_size: int = 1, backend: Optional[str] = None, device_type: Optional[str] = None,
+                     timeout_s: float = 600.0) -> ParallelState:
+    """Initialise from torchrun env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if backend is None:
+        backend = "nccl" if device_type == "cuda" else "gloo"   # "nccl" is RCCL on ROCm
+    if device_type == "cuda":
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=_dt.timedelta(seconds=timeout_s), **kw)
+    if world % tp_size:
+        raise ValueError(f"world size {world} not divisible by tp {tp_size}")
+    dp = world // tp_size
+    s = ParallelState(world, rank, local, tp_size, rank % tp_size, dp, rank // tp_size, backend=backend)
+    if world > 1:
+        for d in range(dp):
+            ranks = list(range(d * tp_size, (d + 1) * tp_size))
+            g = dist.new_group(ranks) if tp_size > 1 else None
+            if rank in ranks:
+                s.tp_group = g
+        for t in range(tp_size):
+            ranks = list(range(t, world, tp_size))
+            g = dist.new_group(ranks) if dp > 1 else None
+            if rank in ranks:
+                s.dp_group = g
+    set_state(s)
+    return s
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        if _STATE.backend == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    set_state(ParallelState())
