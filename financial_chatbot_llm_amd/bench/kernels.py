@@ -1,0 +1,173 @@
+"""Kernel microbenchmarks on the GPU (hipEvent timing, interleaved variants, median of rounds).
+
+    python -m financial_chatbot_llm_amd.bench.kernels [--only decode,prefill,...]
+
+Reports time and the roofline-relevant rate (GB/s for bandwidth-bound ops, TFLOP/s for MFMA
+ones) on shapes taken from the Llama-3-8B RAG workload (B=64 decode, ~2k contexts with a shared
+~1k-token system-prompt prefix).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import statistics
+from typing import Callable, Dict, List
+
+import torch
+
+from .. import ops
+from ..ops.attention import KV_BS
+
+
+def timeit(fn: Callable[[], None], iters: int = 20, rounds: int = 5) -> float:
+    """Median over rounds of mean-per-iteration microseconds."""
+    fn()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        b.synchronize()
+        res.append(a.elapsed_time(b) * 1e3 / iters)
+    return statistics.median(res)
+
+
+def _paged(B, ctx, shared, Hkv, D, dev, gen):
+    """Block tables where the first `shared` tokens of every sequence are the SAME physical blocks."""
+    nsh = shared // KV_BS
+    nb = (ctx + KV_BS - 1) // KV_BS
+    total = nsh + B * (nb - nsh) + 1
+    tables = torch.zeros((B, nb), dtype=torch.int32)
+    nxt = nsh
+    for b in range(B):
+        tables[b, :nsh] = torch.arange(nsh, dtype=torch.int32)
+        tables[b, nsh:] = torch.arange(nxt, nxt + nb - nsh, dtype=torch.int32)
+        nxt += nb - nsh
+    kc = torch.randn((total, Hkv, KV_BS * D), generator=gen, device=dev).to(torch.bfloat16)
+    vc = torch.randn((total, Hkv, KV_BS * D), generator=gen, device=dev).to(torch.bfloat16)
+    return tables.to(dev), kc, vc, total
+
+
+def bench_decode(dev) -> List[Dict]:
+    out = []
+    g = torch.Generator(device=dev).manual_seed(0)
+    Hq, Hkv, D = 32, 8, 128
+    for B, ctx, shared in [(64, 2048, 0), (64, 2048, 1024), (16, 2048, 1024), (64, 512, 0), (128, 4096, 1024)]:
+        tables, kc, vc, total = _paged(B, ctx, shared, Hkv, D, dev, g)
+        q = torch.randn((B, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        lens = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
+        o = torch.empty_like(q)
+        us = timeit(lambda: ops.decode(q, lens, tables, kc, vc, 0.088, workspace=ws, out=o))
+        uniq = (B * ctx - (B - 1) * shared) * Hkv * D * 2 * 2
+        logical = B * ctx * Hkv * D * 2 * 2
+        out.append({"op": "decode_attn", "B": B, "ctx": ctx, "shared": shared, "us": round(us, 1),
+                    "GBps_unique": round(uniq / us / 1e3, 1), "GBps_logical": round(logical / us / 1e3, 1)})
+    return out
+
+
+def bench_prefill(dev) -> List[Dict]:
+    out = []
+    g = torch.Generator(device=dev).manual_seed(1)
+    Hq, Hkv, D = 32, 8, 128
+    for S, qlen, ctx in [(16, 512, 1536), (4, 2048, 2048), (1, 8192, 8192), (32, 256, 2048)]:
+        tables, kc, vc, _ = _paged(S, ctx, 0, Hkv, D, dev, g)
+        T = S * qlen
+        q = torch.randn((T, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        cu = torch.arange(0, T + 1, qlen, dtype=torch.int32, device=dev)
+        lens = torch.full((S,), ctx, dtype=torch.int32, device=dev)
+        o = torch.empty_like(q)
+        us = timeit(lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, qlen, out=o), iters=5)
+        # causal FLOPs: each query i attends to (ctx - qlen + i + 1) keys
+        keys = S * (qlen * (ctx - qlen) + qlen * (qlen + 1) / 2)
+        flops = 4 * keys * Hq * D
+        out.append({"op": "prefill_attn", "S": S, "q_len": qlen, "ctx": ctx, "us": round(us, 1),
+                    "TFLOPs": round(flops / us / 1e6, 1)})
+    return out
+
+
+def bench_elementwise(dev) -> List[Dict]:
+    out = []
+    for T, H in [(64, 4096), (8192, 4096)]:
+        x = torch.randn((T, H), device=dev).to(torch.bfloat16)
+        r = torch.randn((T, H), device=dev).to(torch.bfloat16)
+        w = torch.ones(H, device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.rms_norm(x, w, 1e-5, residual=r))
+        out.append({"op": "add_rmsnorm", "T": T, "H": H, "us": round(us, 2), "GBps": round(4 * T * H * 2 / us / 1e3, 1)})
+        gu = torch.randn((T, 2 * 14336), device=dev).to(torch.bfloat16)
+        us = timeit(lambda: ops.silu_mul(gu))
+        out.append({"op": "silu_mul", "T": T, "F": 14336, "us": round(us, 2), "GBps": round(3 * T * 14336 * 2 / us / 1e3, 1)})
+        qkv = torch.randn((T, 48 * 128), device=dev).to(torch.bfloat16)
+        cs = ops.rope_cos_sin(128, 8192, 5e5, device=dev)
+        pos = torch.arange(T, dtype=torch.int32, device=dev)
+        kc = torch.zeros(((T + 63) // 64 + 1, 8, 64 * 128), device=dev, dtype=torch.bfloat16)
+        vc = torch.zeros(((T + 63) // 64 + 1, 8, 64 * 128), device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.rope_kv_write(qkv, pos, cs, pos, kc, vc, 32, 8, 128))
+        out.append({"op": "rope_kv_write", "T": T, "us": round(us, 2), "GBps": round(2 * T * 48 * 128 * 2 / us / 1e3, 1)})
+    V = 128256
+    for B in (64, 256):
+        lg = torch.randn((B, V), device=dev).to(torch.bfloat16)
+        t = torch.full((B,), 0.5, device=dev)
+        s = torch.arange(B, device=dev, dtype=torch.int64)
+        us = timeit(lambda: ops.sample(lg, t, s))
+        out.append({"op": "sample", "B": B, "V": V, "us": round(us, 2), "GBps": round(B * V * 2 / us / 1e3, 1)})
+    return out
+
+
+def bench_topk(dev) -> List[Dict]:
+    N, D = 1_000_000, 768
+    corpus = torch.nn.functional.normalize(torch.randn((N, D), device=dev), dim=-1).to(torch.bfloat16)
+    users = torch.randint(0, 10_000, (N,), device=dev, dtype=torch.int32)
+    dates = torch.randint(0, 1 << 30, (N,), device=dev, dtype=torch.int64)
+    out = []
+    for nq in (1, 32, 64):
+        q = torch.nn.functional.normalize(torch.randn((nq, D), device=dev), dim=-1).to(torch.bfloat16)
+        qu = torch.randint(0, 10_000, (nq,), device=dev, dtype=torch.int32)
+        qf = torch.zeros((nq,), device=dev, dtype=torch.int64)
+        ks = torch.full((nq,), 20, device=dev, dtype=torch.int32)
+        us = timeit(lambda: ops.filtered_topk(corpus, users, dates, q, qu, qf, ks, 20), iters=10)
+        out.append({"op": "filtered_topk", "N": N, "nq": nq, "us": round(us, 1)})
+    return out
+
+
+def bench_gemm(dev) -> List[Dict]:
+    """hipBLASLt (torch.nn.functional.linear) on the Llama-3-8B projection shapes."""
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    for M in (16, 64, 128, 4096):
+        for name, (N, K) in shapes.items():
+            w = torch.randn((N, K), device=dev).to(torch.bfloat16)
+            x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+            us = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
+            bytes_ = (N * K + M * K + M * N) * 2
+            out.append({"op": "gemm", "name": name, "M": M, "N": N, "K": K, "us": round(us, 1),
+                        "GBps": round(bytes_ / us / 1e3, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)})
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="decode,prefill,elementwise,topk")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args(argv)
+    dev = torch.device("cuda")
+    res = []
+    for name in args.only.split(","):
+        res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
+                "topk": bench_topk, "gemm": bench_gemm}[name](dev)
+    for r in res:
+        print(json.dumps(r), flush=True)
+    if args.out:
+        with open(args.out, "w") as fh:
+            for r in res:
+                fh.write(json.dumps(r) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -3,27 +3,34 @@
 //
 // Orientation (see kv_layout.h): scores are computed TRANSPOSED, S^T = K . Q^T, so a lane holds
 // one query column and 16 keys in registers; the P.V product is O^T = V^T . P^T and takes P
-// straight from those registers (no LDS round trip for P), with V stored dim-major in the cache.
+// straight from those registers (no LDS round trip for P).  The KV cache is stored in
+// MFMA-fragment-native order, so every K/V operand fragment is one contiguous 16-B piece at
+// (64*fragment + lane)*16 inside a block tile.
 //
 // GQA packing: the G = Hq/Hkv query heads that share a kv head are packed into the MFMA's 16
 // query columns (decode) or into the 128 "rows" of a prefill tile (rows = token*G + head), so
 // every K/V byte staged is used by all G heads.
 //
 // Prefill: one workgroup = 4 waves = 128 (token, head) rows of one sequence and one kv head.
-// K and V^T blocks (64 keys) are staged through XOR-swizzled LDS, double-buffered: the global
-// loads for block j+1 are issued before block j's MFMAs and written to LDS after them
-// (async-STAGE split, cdna_hip_programming.md T14), one barrier per block.  Swizzles make every
-// ds_read_b128 of the fragment reads conflict-free (K rows of 256 B: chunk ^= key&15; 128-B rows
-// (V^T, or K at D=64): chunk ^= (row>>1)&7).
+// K and V blocks (64 keys) are staged into LDS with lane-linear global_load_lds (the tile is
+// already in fragment order, so no swizzle and no staging registers), double-buffered: block
+// j+1 is requested before block j's MFMAs, one barrier per block.  Fragment reads are
+// consecutive-lane ds_read_b128 (conflict-free).  ~64 KiB LDS and <=256 VGPRs per wave let two
+// workgroups share a CU, so one workgroup's softmax VALU overlaps the other's MFMAs.
 //
 // Decode: one workgroup = 4 waves = one (sequence, kv head, partition of PB blocks).  Each wave
-// streams whole 64-key blocks straight into VGPRs (decode is HBM-bound; an LDS hop is pure
-// overhead: the 'GEMV / M <= 16' row of the guide), the 4 waves merge through LDS, and a second
-// kernel merges partitions (flash-decoding split-K) when a sequence spans several.
+// streams whole 64-key blocks straight into VGPRs with 1-KiB coalesced loads (decode is
+// HBM-bound; an LDS hop is pure overhead: the 'GEMV / M <= 16' row of the guide), the 4 waves
+// merge through LDS, and a second kernel merges partitions (flash-decoding split-K).  The grid
+// runs the sequence index fastest so the workgroups that read the SAME shared-prefix blocks
+// (every turn's system prompt is a prefix-cache hit) are in flight together and hit in L2/MALL.
 #include "common.h"
 #include "kv_layout.h"
 
 #define LOG2E 1.4426950408889634f
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
 
 union Frag {
   uint4 u;
@@ -34,33 +41,19 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// byte offset of 16-B chunk `c` of row `r` in a swizzled LDS tile with ROWB-byte rows
-template <int ROWB>
-__device__ __forceinline__ int swz(int r, int c) {
-  if constexpr (ROWB == 256) {
-    return r * 256 + ((c ^ (r & 15)) << 4);
-  } else {
-    static_assert(ROWB == 128, "row width");
-    return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // Prefill
 // ------------------------------------------------------------------------------------------
 template <int D>
-__global__ void __launch_bounds__(256) prefill_kernel(
+__global__ void __launch_bounds__(256, 2) prefill_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
-  constexpr int KC = D / 32;        // k-chunks of the QK^T product
-  constexpr int DT = D / 16;        // 16-row dim tiles of O^T
-  constexpr int KROWB = D * 2;      // K row bytes in LDS
-  constexpr int KBYTES = KV_BS * D * 2;
-  constexpr int VBYTES = D * KV_BS * 2;
-  constexpr int KCH = KBYTES / 16 / 256;  // staged 16-B chunks per thread
-  constexpr int VCH = VBYTES / 16 / 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
+  constexpr int KC = D / 32;                 // k-chunks of the QK^T product
+  constexpr int DT = D / 16;                 // 16-row dim tiles of O^T
+  constexpr int TILE = KV_BS * D * 2;        // bytes of one K (or V) block tile
+  constexpr int PIECES = TILE / 1024 / 4;    // 1-KiB glds pieces per wave per tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
 
   const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
   const int G = Hq / Hkv;
@@ -71,7 +64,6 @@ __global__ void __launch_bounds__(256) prefill_kernel(
   const int ctx = ctx_lens[s];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
 
-  // query rows owned by this lane (one per column tile)
   int tok[2], head[2], qpos[2];
   Frag qf[2][KC];
 #pragma unroll
@@ -83,9 +75,8 @@ __global__ void __launch_bounds__(256) prefill_kernel(
     qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
     const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
 #pragma unroll
-    for (int c = 0; c < KC; ++c) {
+    for (int c = 0; c < KC; ++c)
       qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
-    }
   }
 
   const int last_tok = min(tok0 + TQ, qlen) - 1;
@@ -103,44 +94,31 @@ __global__ void __launch_bounds__(256) prefill_kernel(
     for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  uint4 kst[KCH], vst[VCH];
-  auto stage_load = [&](int j) {
+  // lane-linear global -> LDS copy of block j's K and V tiles into buffer `buf`
+  auto stage = [&](int j, int buf) {
     const long phys = bt[j];
-    const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    char* kl = smem + buf * 2 * TILE;
+    char* vl = kl + TILE;
 #pragma unroll
-    for (int i = 0; i < KCH; ++i) kst[i] = kb[threadIdx.x + i * 256];
-#pragma unroll
-    for (int i = 0; i < VCH; ++i) vst[i] = vb[threadIdx.x + i * 256];
-  };
-  auto stage_write = [&](int buf) {
-    char* kl = smem + buf * (KBYTES + VBYTES);
-    char* vl = kl + KBYTES;
-#pragma unroll
-    for (int i = 0; i < KCH; ++i) {
-      const int id = threadIdx.x + i * 256;
-      const int r = id / (KROWB / 16), c = id % (KROWB / 16);
-      *reinterpret_cast<uint4*>(kl + swz<KROWB>(r, c)) = kst[i];
-    }
-#pragma unroll
-    for (int i = 0; i < VCH; ++i) {
-      const int id = threadIdx.x + i * 256;
-      const int r = id >> 3, c = id & 7;
-      *reinterpret_cast<uint4*>(vl + swz<128>(r, c)) = vst[i];
+    for (int i = 0; i < PIECES; ++i) {
+      const int piece = w * PIECES + i;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kl + piece * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vl + piece * 1024),
+                                       16, 0, 0);
     }
   };
 
-  if (nblk > 0) {
-    stage_load(0);
-    stage_write(0);
-  }
+  if (nblk > 0) stage(0, 0);
   __syncthreads();
 
   for (int j = 0; j < nblk; ++j) {
     const int buf = j & 1;
-    if (j + 1 < nblk) stage_load(j + 1);
-    const char* kl = smem + buf * (KBYTES + VBYTES);
-    const char* vl = kl + KBYTES;
+    if (j + 1 < nblk) stage(j + 1, buf ^ 1);
+    const uint4* kl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE);
+    const uint4* vl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE + TILE);
 
     // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
     f32x4 sc[2][4];
@@ -151,7 +129,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         Frag kf;
-        kf.u = *reinterpret_cast<const uint4*>(kl + swz<KROWB>(16 * t + col, 4 * c + g));
+        kf.u = kl[(t * KC + c) * 64 + lane];
         sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
         sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
       }
@@ -159,6 +137,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 
     // ---- online softmax (base-2) -------------------------------------------------------
     Frag pf[2][2];
+    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       float mt = -INFINITY;
@@ -167,7 +146,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = j * KV_BS + 16 * t + 4 * g + r;
-          const bool ok = key < ctx && (!causal || key <= qpos[ct]);
+          const bool ok = full || (key < ctx && (!causal || key <= qpos[ct]));
           const float v = ok ? sc[ct][t][r] * scale_log2 : -INFINITY;
           sc[ct][t][r] = v;
           mt = fmaxf(mt, v);
@@ -176,13 +155,14 @@ __global__ void __launch_bounds__(256) prefill_kernel(
       mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mn = fmaxf(m[ct], mt);
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[ct] - mn);
+      const float mref = (mn == -INFINITY) ? 0.f : mn;
+      const float alpha = exp2f(m[ct] - mref);
       float ls = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = (mn == -INFINITY) ? 0.f : exp2f(sc[ct][t][r] - mn);
+          const float p = exp2f(sc[ct][t][r] - mref);
           sc[ct][t][r] = p;
           ls += p;
         }
@@ -207,14 +187,12 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         Frag vf;
-        vf.u = *reinterpret_cast<const uint4*>(vl + swz<128>(16 * dt + col, 4 * st + g));
+        vf.u = vl[(dt * 2 + st) * 64 + lane];
         o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
         o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
       }
     }
-
-    if (j + 1 < nblk) stage_write(buf ^ 1);
-    __syncthreads();
+    __syncthreads();  // block j+1 landed (vmcnt drained) and everyone is done with buffer `buf`
   }
 
   // ---- epilogue: finish row sums across the 4 lane groups, normalise, store -----------
@@ -249,7 +227,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
   __shared__ float s_m[4][16], s_l[4][16];
   __shared__ float s_o[4][16][D + 4];
 
-  const int b = blockIdx.z, h = blockIdx.y, p = blockIdx.x;
+  const int b = blockIdx.x, p = blockIdx.y, h = blockIdx.z;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
   const int blk0 = p * pb;
@@ -275,19 +253,17 @@ __global__ void __launch_bounds__(256) decode_kernel(
 
   for (int j = blk0 + w; j < blk1; j += 4) {
     const long phys = bt[j];
-    const bf16* kb = k_cache + (phys * Hkv + h) * (long)(KV_BS * D);
-    const bf16* vb = v_cache + (phys * Hkv + h) * (long)(KV_BS * D);
+    const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     Frag kf[4][KC], vf[DT][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int c = 0; c < KC; ++c)
-        kf[t][c].u = *reinterpret_cast<const uint4*>(kb + (16 * t + col) * D + 32 * c + 8 * g);
+      for (int c = 0; c < KC; ++c) kf[t][c].u = kb[(t * KC + c) * 64 + lane];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
-        vf[dt][st].u = *reinterpret_cast<const uint4*>(vb + (16 * dt + col) * KV_BS + 32 * st + 8 * g);
+      for (int st = 0; st < 2; ++st) vf[dt][st].u = vb[(dt * 2 + st) * 64 + lane];
 
     f32x4 sc[4];
     float mt = -INFINITY;
@@ -416,7 +392,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0) return (int)hipErrorInvalidValue;
-  dim3 grid(nparts, Hkv, B);
+  dim3 grid(B, nparts, Hkv);  // sequence fastest: shared-prefix blocks are read concurrently
   const float sl2 = scale * LOG2E;
   if (D == 128) {
     hipLaunchKernelGGL(decode_kernel<128>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, block_tables,

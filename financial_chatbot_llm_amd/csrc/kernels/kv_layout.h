@@ -1,20 +1,31 @@
 // Paged KV-cache layout shared by the KV writer (rope_kv.hip) and the attention kernels.
 //
-// A block holds KV_BS = 64 tokens = exactly one 64-key attention tile.
-//   K: [block][kv_head][64 keys][D]      key-major
-//   V: [block][kv_head][D][64 keys]      dim-major, keys permuted inside each 32-key group
+// A block holds KV_BS = 64 tokens of one kv head = exactly one 64-key attention tile, and is
+// stored in **MFMA-fragment-native order**: the 16-byte operand fragment that lane l of a wave
+// feeds to v_mfma_f32_16x16x32_bf16 for fragment f lives at byte 16*(64*f + l).  Hence
+//   * decode streams a block with perfectly coalesced 1-KiB wave-instructions straight into
+//     VGPRs (no LDS hop, no over-fetch), and
+//   * prefill stages a block into LDS with lane-linear global_load_lds (no swizzle needed) and
+//     reads fragments back with conflict-free consecutive ds_read_b128.
 //
-// Why the permutation: S^T = K.Q^T on v_mfma_f32_16x16x32_bf16 leaves lane l holding, for query
-// column l&15, the scores of keys 16t + 4g + r (g = l>>4, r = 0..3) of each 16-key tile t.  The
-// P.V product O^T = V^T.P^T consumes P straight from those registers if, for k-step s, lane
-// group g's 8 K-elements are keys {32s+4g+0..3} (tile 2s) and {32s+16+4g+0..3} (tile 2s+1).
-// Storing key k of a 32-key group at  8*((k&15)>>2) + 4*(k>>4) + (k&3)  makes those 8 keys
-// physically contiguous, so each V^T A-fragment is a single 16-byte load.
+// K (A operand of S^T = K.Q^T): fragment f = t*(D/32) + c for key tile t (16 keys) and k-chunk c
+//   (32 dims); lane = 16*g + r holds key 16t+r, dims 32c + 8g + 0..7.
+// V (A operand of O^T = V^T.P^T): fragment f = 2*dt + s for dim tile dt (16 dims) and key step s
+//   (32 keys); lane = 16*g + row holds dim 16dt+row and the 8 keys whose scores lane group g
+//   already holds in registers after the S^T MFMA: 32s + 4g + 0..3 and 32s + 16 + 4g + 0..3.
 #pragma once
 
 #define KV_BS 64
 
-__host__ __device__ __forceinline__ int kv_perm(int key) {
-  const int grp = key >> 5, k = key & 31;
-  return grp * 32 + 8 * ((k & 15) >> 2) + 4 * (k >> 4) + (k & 3);
+// element index inside one (block, kv head) tile of K
+__host__ __device__ __forceinline__ int k_index(int key, int d, int D) {
+  const int t = key >> 4, r = key & 15, c = d >> 5, g = (d >> 3) & 3, j = d & 7;
+  return (((t * (D >> 5) + c) * 64 + g * 16 + r) << 3) + j;
+}
+
+// element index inside one (block, kv head) tile of V
+__host__ __device__ __forceinline__ int v_index(int key, int d, int D) {
+  const int dt = d >> 4, row = d & 15, s = key >> 5, k = key & 31;
+  const int g = (k & 15) >> 2, j = ((k >> 4) << 2) + (k & 3);
+  return (((dt * 2 + s) * 64 + g * 16 + row) << 3) + j;
 }

@@ -3,11 +3,11 @@
 //
 // qkv      [T, (Hq + 2*Hkv) * D] bf16  (q heads, then k heads, then v heads)
 // q_out    [T, Hq, D] bf16              (rotated q, consumed by the attention kernels)
-// k_cache  [num_blocks][Hkv][BS][D]      bf16, key-major rows (MFMA A operand for S^T = K Q^T)
-// v_cache  [num_blocks][Hkv][D][BS]      bf16, dim-major with the key order inside each 32-key
-//                                        group permuted so that the P.V MFMA A-fragment of a lane
-//                                        (8 keys of one dim) is one contiguous 16-B load
-//                                        (see kv_perm() and attention.hip).
+// k_cache  [num_blocks][Hkv][64*D]       bf16, MFMA-fragment-native tiles (kv_layout.h k_index)
+// v_cache  [num_blocks][Hkv][64*D]       bf16, MFMA-fragment-native tiles (kv_layout.h v_index)
+//                                        -- a K row's 8 consecutive dims are one 16-B store; V is
+//                                        scattered element-wise (transposed on write, so that every
+//                                        attention-side read is a contiguous fragment).
 // cos_sin  [max_pos, D] f32: cos(pos * inv_freq[i]) for i < D/2, then sin(...)  (host-precomputed,
 //          so the kernel stays bandwidth-bound: no on-device trig, Appendix B 'Element-wise')
 // Rotation is the HF/"neox" rotate-half form used by Llama-3 checkpoints.
@@ -55,18 +55,18 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
         *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
       } else if (slot >= 0) {
         const int kh = h - Hq;
-        bf16* dst = k_cache + ((blk * Hkv + kh) * KV_BS + off) * D;
-        *reinterpret_cast<uint4*>(dst + c * 8) = p1;
-        *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
+        bf16* dst = k_cache + (blk * Hkv + kh) * (long)(KV_BS * D);
+        *reinterpret_cast<uint4*>(dst + k_index(off, c * 8, D)) = p1;
+        *reinterpret_cast<uint4*>(dst + k_index(off, HALF + c * 8, D)) = p2;
       }
     } else if (slot >= 0) {
       const int v = u - n_rot;
       const int h = v / VU, c = v % VU;
       Pack8 p;
       p.u = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + h) * D + c * 8);
-      bf16* base = v_cache + (blk * Hkv + h) * (long)D * KV_BS + kv_perm(off);
+      bf16* base = v_cache + (blk * Hkv + h) * (long)(KV_BS * D);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) base[(long)(c * 8 + i) * KV_BS] = p.e[i];
+      for (int i = 0; i < 8; ++i) base[v_index(off, c * 8 + i, D)] = p.e[i];
     }
   }
 }

@@ -62,11 +62,9 @@ class BertEncoder:
 
     def _kv_scratch(self, nblocks: int):
         if self._scratch is None or self._scratch.shape[1] < nblocks:
-            self._scratch = torch.zeros((2, max(nblocks, 64), self.nh, KV_BS, self.D), dtype=self.dtype,
+            self._scratch = torch.zeros((2, max(nblocks, 64), self.nh, KV_BS * self.D), dtype=self.dtype,
                                         device=self.device)
-        k = self._scratch[0]
-        v = self._scratch[1].view(self._scratch.shape[1], self.nh, self.D, KV_BS)
-        return k, v
+        return self._scratch[0], self._scratch[1]
 
     @torch.no_grad()
     def forward(self, ids_list: Sequence[Sequence[int]]) -> torch.Tensor:

@@ -29,24 +29,24 @@ class AttentionMetadata:
 
 
 class KVCache:
-    """All layers' paged K/V in ONE HBM allocation: [L, 2, num_blocks, Hkv, 64, D] bf16.
+    """All layers' paged K/V in ONE HBM allocation: [L, 2, num_blocks, Hkv, 64*D] bf16.
 
-    ``k(l)`` is [num_blocks, Hkv, 64, D]; ``v(l)`` views the same bytes as [num_blocks, Hkv, D, 64]
-    (dim-major V, see csrc/kernels/kv_layout.h).
+    ``k(l)`` / ``v(l)`` are [num_blocks, Hkv, 64*D] tiles in MFMA-fragment-native order
+    (csrc/kernels/kv_layout.h).
     """
 
     def __init__(self, num_layers: int, num_blocks: int, num_kv_heads: int, head_dim: int,
                  dtype=torch.bfloat16, device="cuda"):
         self.num_layers, self.num_blocks = num_layers, num_blocks
         self.num_kv_heads, self.head_dim = num_kv_heads, head_dim
-        self.buf = torch.zeros((num_layers, 2, num_blocks, num_kv_heads, KV_BS, head_dim), dtype=dtype,
+        self.buf = torch.zeros((num_layers, 2, num_blocks, num_kv_heads, KV_BS * head_dim), dtype=dtype,
                                device=device)
 
     def k(self, layer: int) -> torch.Tensor:
         return self.buf[layer, 0]
 
     def v(self, layer: int) -> torch.Tensor:
-        return self.buf[layer, 1].view(self.num_blocks, self.num_kv_heads, self.head_dim, KV_BS)
+        return self.buf[layer, 1]
 
     @staticmethod
     def bytes_per_block(num_layers: int, num_kv_heads: int, head_dim: int, elt: int = 2) -> int:

@@ -1,9 +1,10 @@
 """K3-epilogue/K4/K5 (RoPE + paged KV write) and K6/K7 (paged prefill / decode attention).
 
-Paged KV layout (see ``csrc/kernels/kv_layout.h``), blocks of ``KV_BS = 64`` tokens::
+Paged KV layout (see ``csrc/kernels/kv_layout.h``): blocks of ``KV_BS = 64`` tokens, one tile
+of ``64*D`` elements per (block, kv head), stored in MFMA-fragment-native order::
 
-    k_cache[layer]: [num_blocks, Hkv, 64, D]   key-major
-    v_cache[layer]: [num_blocks, Hkv, D, 64]   dim-major, keys permuted by KV_PERM
+    k_cache[layer]: [num_blocks, Hkv, 64*D]   element (key, d) at K_INDEX[D][key, d]
+    v_cache[layer]: [num_blocks, Hkv, 64*D]   element (key, d) at V_INDEX[D][key, d]
 
 The torch reference implementations here are the numerics oracle for the HIP kernels (fp32
 math on the same bf16 inputs) and the CPU path used by the CI tests.
@@ -12,6 +13,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
+from functools import lru_cache
 from typing import Optional
 
 import torch
@@ -21,12 +23,23 @@ from . import _native as N
 KV_BS = 64
 
 
-def _kv_perm(key: int) -> int:
-    grp, k = key >> 5, key & 31
-    return grp * 32 + 8 * ((k & 15) >> 2) + 4 * (k >> 4) + (k & 3)
+def k_index(key: int, d: int, D: int) -> int:
+    t, r, c, g, j = key >> 4, key & 15, d >> 5, (d >> 3) & 3, d & 7
+    return (((t * (D >> 5) + c) * 64 + g * 16 + r) << 3) + j
 
 
-KV_PERM = torch.tensor([_kv_perm(k) for k in range(KV_BS)], dtype=torch.long)
+def v_index(key: int, d: int, D: int) -> int:
+    dt, row, s, k = d >> 4, d & 15, key >> 5, key & 31
+    g, j = (k & 15) >> 2, ((k >> 4) << 2) + (k & 3)
+    return (((dt * 2 + s) * 64 + g * 16 + row) << 3) + j
+
+
+@lru_cache(maxsize=None)
+def kv_index_tables(D: int):
+    """(K_INDEX, V_INDEX) [64, D] long tensors for head dim D."""
+    ki = torch.tensor([[k_index(k, d, D) for d in range(D)] for k in range(KV_BS)], dtype=torch.long)
+    vi = torch.tensor([[v_index(k, d, D) for d in range(D)] for k in range(KV_BS)], dtype=torch.long)
+    return ki, vi
 
 
 # --------------------------------------------------------------------------------------------
@@ -69,16 +82,18 @@ def _rope_ref(x: torch.Tensor, pos: torch.Tensor, cos_sin: torch.Tensor) -> torc
 # --------------------------------------------------------------------------------------------
 def write_kv_ref(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
                  v_cache: torch.Tensor) -> None:
-    """k, v [T, Hkv, D] -> paged caches (skips slots < 0)."""
+    """k, v [T, Hkv, D] -> paged fragment-native caches (skips slots < 0)."""
     sl = slots.long()
     keep = sl >= 0
     if not bool(keep.any()):
         return
     sl, k, v = sl[keep], k[keep], v[keep]
+    D = k.shape[-1]
+    ki, vi = kv_index_tables(D)
     blk, off = sl // KV_BS, sl % KV_BS
-    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
-    poff = KV_PERM.to(sl.device)[off]
-    v_cache[blk, :, :, poff] = v.to(v_cache.dtype)
+    kc, vc = k_cache.permute(0, 2, 1), v_cache.permute(0, 2, 1)   # [NB, 64*D, Hkv] views
+    kc[blk[:, None], ki.to(sl.device)[off]] = k.transpose(1, 2).to(k_cache.dtype)
+    vc[blk[:, None], vi.to(sl.device)[off]] = v.transpose(1, 2).to(v_cache.dtype)
 
 
 def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
@@ -104,11 +119,15 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[
 # --------------------------------------------------------------------------------------------
 def gather_kv_ref(k_cache: torch.Tensor, v_cache: torch.Tensor, blocks: torch.Tensor, n: int):
     """-> K, V [n, Hkv, D] for one sequence (inverse of the paged layout)."""
+    Hkv = k_cache.shape[1]
+    D = k_cache.shape[2] // KV_BS
+    ki, vi = kv_index_tables(D)
     nb = (n + KV_BS - 1) // KV_BS
     b = blocks[:nb].long()
-    k = k_cache[b].permute(0, 2, 1, 3).reshape(nb * KV_BS, k_cache.shape[1], k_cache.shape[3])
-    vv = v_cache[b][..., KV_PERM.to(b.device)]  # [nb, Hkv, D, 64] in logical key order
-    v = vv.permute(0, 3, 1, 2).reshape(nb * KV_BS, v_cache.shape[1], v_cache.shape[2])
+    kt = k_cache[b][..., ki.to(b.device).flatten()].view(nb, Hkv, KV_BS, D)
+    vt = v_cache[b][..., vi.to(b.device).flatten()].view(nb, Hkv, KV_BS, D)
+    k = kt.permute(0, 2, 1, 3).reshape(nb * KV_BS, Hkv, D)
+    v = vt.permute(0, 2, 1, 3).reshape(nb * KV_BS, Hkv, D)
     return k[:n], v[:n]
 
 
@@ -136,6 +155,7 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     S = block_tables.shape[0]
+    assert k_cache.shape[-1] == KV_BS * D
     if N.use_native(q):
         out = torch.empty_like(q) if out is None else out
         if max_q_len is None:

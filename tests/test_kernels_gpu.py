@@ -78,8 +78,8 @@ def _paged_setup(seq_lens, Hkv, D, num_blocks=None, gen=None):
     for i, n in enumerate(nb_each):
         tables[i, :n] = perm[k:k + n].to(torch.int32)
         k += n
-    kc = rnd(num_blocks, Hkv, KV_BS, D, gen=gen)
-    vc = rnd(num_blocks, Hkv, D, KV_BS, gen=gen)
+    kc = rnd(num_blocks, Hkv, KV_BS * D, gen=gen)
+    vc = rnd(num_blocks, Hkv, KV_BS * D, gen=gen)
     return tables, kc, vc
 
 
@@ -93,8 +93,8 @@ def test_rope_kv_write(Hq, Hkv, D):
     nblk = 4
     slots = torch.randperm(nblk * KV_BS, generator=g)[:T].to(torch.int32)
     slots[5] = -1
-    kc = torch.zeros(nblk, Hkv, KV_BS, D, dtype=torch.bfloat16)
-    vc = torch.zeros(nblk, Hkv, D, KV_BS, dtype=torch.bfloat16)
+    kc = torch.zeros(nblk, Hkv, KV_BS * D, dtype=torch.bfloat16)
+    vc = torch.zeros(nblk, Hkv, KV_BS * D, dtype=torch.bfloat16)
     kcd, vcd = kc.to(DEV), vc.to(DEV)
     apply = D == 128
     q = ops.rope_kv_write(qkv.to(DEV), pos.to(DEV), cs.to(DEV), slots.to(DEV), kcd, vcd, Hq, Hkv, D, apply)

@@ -24,7 +24,7 @@ from financial_chatbot_llm_amd.ops.attention import KV_BS
 def _hf_llama(moe=False, seed=0):
     torch.manual_seed(seed)
     kw = dict(vocab_size=512, hidden_size=64, intermediate_size=96, num_hidden_layers=2, num_attention_heads=4,
-              num_key_value_heads=2, head_dim=16, max_position_embeddings=512, rms_norm_eps=1e-5,
+              num_key_value_heads=2, head_dim=32, max_position_embeddings=512, rms_norm_eps=1e-5,
               rope_theta=500000.0, tie_word_embeddings=False)
     if moe:
         cfg = transformers.MixtralConfig(num_local_experts=4, num_experts_per_tok=2, **kw)

@@ -4,23 +4,28 @@ import math
 import torch
 
 from financial_chatbot_llm_amd import ops
-from financial_chatbot_llm_amd.ops.attention import KV_BS, KV_PERM, gather_kv_ref, write_kv_ref
+from financial_chatbot_llm_amd.ops.attention import KV_BS, gather_kv_ref, kv_index_tables, write_kv_ref
 
 
-def test_kv_perm_is_permutation_and_fragment_contiguous():
-    assert sorted(KV_PERM.tolist()) == list(range(KV_BS))
-    # lane group g of k-step s reads 8 contiguous physical keys = {32s+4g+0..3, 32s+16+4g+0..3}
-    inv = {p: k for k, p in enumerate(KV_PERM.tolist())}
-    for s in range(2):
+def test_kv_tiles_are_fragment_native_permutations():
+    for D in (64, 128):
+        ki, vi = kv_index_tables(D)
+        assert sorted(ki.flatten().tolist()) == list(range(KV_BS * D))
+        assert sorted(vi.flatten().tolist()) == list(range(KV_BS * D))
+        # a K row's 8 consecutive dims are one contiguous 16-byte piece
+        assert all(int(ki[k, 8 * c + 7] - ki[k, 8 * c]) == 7 for k in range(KV_BS) for c in range(D // 8))
+        # V fragment of (dim tile 0, key step 0, lane 16g+row) = keys {4g..4g+3, 16+4g..16+4g+3} of that dim
         for g in range(4):
-            keys = [inv[32 * s + 8 * g + j] for j in range(8)]
-            assert keys == [32 * s + 4 * g + j for j in range(4)] + [32 * s + 16 + 4 * g + j for j in range(4)]
+            for row in (0, 5):
+                base = (g * 16 + row) * 8
+                keys = sorted(k for k in range(32) if base <= int(vi[k, row]) < base + 8)
+                assert keys == [4 * g + j for j in range(4)] + [16 + 4 * g + j for j in range(4)]
 
 
 def test_paged_roundtrip():
-    Hkv, D, nb = 2, 16, 5
-    kc = torch.zeros(nb, Hkv, KV_BS, D)
-    vc = torch.zeros(nb, Hkv, D, KV_BS)
+    Hkv, D, nb = 2, 64, 5
+    kc = torch.zeros(nb, Hkv, KV_BS * D)
+    vc = torch.zeros(nb, Hkv, KV_BS * D)
     L = 150
     blocks = torch.tensor([3, 0, 4], dtype=torch.int32)
     slots = torch.tensor([int(blocks[i // KV_BS]) * KV_BS + i % KV_BS for i in range(L)], dtype=torch.int32)
@@ -33,8 +38,8 @@ def test_paged_roundtrip():
 def test_prefill_ref_chunked_equals_full():
     torch.manual_seed(0)
     Hq, Hkv, D, L = 4, 2, 32, 90
-    kc = torch.zeros(4, Hkv, KV_BS, D)
-    vc = torch.zeros(4, Hkv, D, KV_BS)
+    kc = torch.zeros(4, Hkv, KV_BS * D)
+    vc = torch.zeros(4, Hkv, KV_BS * D)
     blocks = torch.tensor([[2, 1]], dtype=torch.int32)
     slots = torch.tensor([int(blocks[0, i // KV_BS]) * KV_BS + i % KV_BS for i in range(L)], dtype=torch.int32)
     write_kv_ref(torch.randn(L, Hkv, D), torch.randn(L, Hkv, D), slots, kc, vc)
@@ -51,13 +56,13 @@ def test_prefill_ref_chunked_equals_full():
 
 
 def test_rope_matches_complex_rotation():
-    D, T = 8, 3
+    D, T = 64, 3
     cs = ops.rope_cos_sin(D, 16, 10000.0)
     Hq, Hkv = 1, 1
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D)
     pos = torch.tensor([0, 1, 5], dtype=torch.int32)
-    kc = torch.zeros(1, Hkv, KV_BS, D)
-    vc = torch.zeros(1, Hkv, D, KV_BS)
+    kc = torch.zeros(1, Hkv, KV_BS * D)
+    vc = torch.zeros(1, Hkv, KV_BS * D)
     q = ops.rope_kv_write(qkv, pos, cs, torch.tensor([0, 1, 2], dtype=torch.int32), kc, vc, Hq, Hkv, D)
     x = qkv[:, :D]
     inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2).double() / D))
