@@ -150,6 +150,43 @@ def bench_gemm(dev) -> List[Dict]:
     return out
 
 
+def bench_skinny(dev) -> List[Dict]:
+    """Hand-written MFMA skinny GEMM vs hipBLASLt at decode batch sizes, every launch config."""
+    from ..ops import gemm
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    for M in (16, 64):
+        for name, (N, K) in shapes.items():
+            w = torch.randn((N, K), device=dev).to(torch.bfloat16)
+            x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+            bytes_ = (N * K + M * K + M * N) * 2
+            base = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
+            row = {"op": "skinny", "name": name, "M": M, "hipblaslt_us": round(base, 1),
+                   "hipblaslt_GBps": round(bytes_ / base / 1e3, 1)}
+            best = None
+            saved = (gemm.TUNING.get((N, K)), gemm.SKINNY_MAX_M.get((N, K)))
+            gemm.SKINNY_MAX_M[(N, K)] = 64
+            wt = gemm.tile_weight(w)
+            for cfg in [(2, 4), (2, 8), (4, 4), (1, 8), (1, 4)]:
+                gemm.TUNING[(N, K)] = cfg
+                if not gemm.skinny_ok(x, w, wt=wt):
+                    continue
+                us = timeit(lambda: gemm.linear(x, w, wt=wt), iters=10)
+                row[f"cfg{cfg[0]}x{cfg[1]}_us"] = round(us, 1)
+                if best is None or us < best[1]:
+                    best = (cfg, us)
+            gemm.TUNING.pop((N, K), None)
+            gemm.SKINNY_MAX_M.pop((N, K), None)
+            if saved[0] is not None:
+                gemm.TUNING[(N, K)], gemm.SKINNY_MAX_M[(N, K)] = saved
+            if best:
+                row["best"] = list(best[0])
+                row["best_GBps"] = round(bytes_ / best[1] / 1e3, 1)
+            out.append(row)
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="decode,prefill,elementwise,topk")
@@ -159,7 +196,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm}[name](dev)
+                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

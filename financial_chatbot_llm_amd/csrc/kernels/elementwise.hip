@@ -4,8 +4,11 @@
 // 256 CUs x 8 workgroups (cdna_hip_programming.md Guideline 11).
 #include "common.h"
 
-// out[t, f] = silu(gu[t, f]) * gu[t, F + f]   (gate and up projections fused in one GEMM)
-__global__ void silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out, int T, int F) {
+// out[t, f] = silu(gate[t, f]) * up[t, f] from the fused gate|up GEMM output.  Column layout of gu:
+// interleave16 = 0: [gate 0..F-1 | up 0..F-1];  interleave16 = 1: 16-column groups alternate
+// gate/up (gate 16i..16i+15, up 16i..16i+15), the layout the decode skinny GEMM's fused SiLU
+// epilogue needs, so one weight tensor serves both paths.
+__global__ void silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out, int T, int F, int il16) {
   const int cpr = F >> 3;  // 16-byte chunks per output row
   const long total = (long)T * cpr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -13,8 +16,14 @@ __global__ void silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ 
     const int c = (int)(i - t * cpr);
     const uint4* row = reinterpret_cast<const uint4*>(gu + t * 2L * F);
     float g[8], u[8], o[8];
-    unpack8(row[c], g);
-    unpack8(row[cpr + c], u);
+    if (il16) {  // chunk c covers output cols 8c..8c+7 = pair (8c)/16, half (c & 1)
+      const int pair = c >> 1, half = c & 1;
+      unpack8(row[pair * 4 + half], g);
+      unpack8(row[pair * 4 + 2 + half], u);
+    } else {
+      unpack8(row[c], g);
+      unpack8(row[cpr + c], u);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       // HF SiLU is computed in the activation dtype: silu(bf16) -> bf16, then * up in bf16
@@ -56,11 +65,11 @@ static inline int grid_for(long work, int threads) {
   return (int)g;
 }
 
-PENNY_API int penny_silu_mul(const void* gu, void* out, int T, int F, hipStream_t stream) {
+PENNY_API int penny_silu_mul(const void* gu, void* out, int T, int F, int interleave16, hipStream_t stream) {
   if (T <= 0) return 0;
-  if (F % 8) return (int)hipErrorInvalidValue;
+  if (F % (interleave16 ? 16 : 8)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for((long)T * (F / 8), 256)), dim3(256), 0, stream,
-                     (const bf16*)gu, (bf16*)out, T, F);
+                     (const bf16*)gu, (bf16*)out, T, F, interleave16);
   PENNY_RETURN_LAUNCH();
 }
 

@@ -27,22 +27,31 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
   }
 }
 
+// Pass 1: grid (B, SPLITS); each 256-thread workgroup scans one vocab slice of one row and writes
+// its (best value, index).  Pass 2: one wave per row merges the SPLITS candidates.  Splitting the
+// row keeps the whole chip busy at decode batch sizes (B = 64 rows alone would occupy 64 CUs,
+// and the per-element noise generation makes this pass VALU-, not bandwidth-, bound).
+#define SAMPLE_SPLITS 16
+
 template <typename T>
-__global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logits, long row_stride,
-                                                      const float* __restrict__ temps,
-                                                      const unsigned long long* __restrict__ seeds,
-                                                      int* __restrict__ out, int V) {
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  const int row = blockIdx.x;
+__global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict__ logits, long row_stride,
+                                                             const float* __restrict__ temps,
+                                                             const unsigned long long* __restrict__ seeds,
+                                                             float* __restrict__ pv, int* __restrict__ pi, int V) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x, split = blockIdx.y;
   const T* lr = logits + row * row_stride;
   const float temp = temps[row];
   const bool greedy = !(temp > 0.f);
   const float inv_t = greedy ? 1.f : 1.f / temp;
   const unsigned long long seed = seeds[row];
+  const int nch = V >> 3;
+  const int per = (nch + SAMPLE_SPLITS - 1) / SAMPLE_SPLITS;
+  const int c0 = split * per, c1 = min(nch, c0 + per);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int c = threadIdx.x; c < (V >> 3); c += blockDim.x) {
+  for (int c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
     float f[8];
     load8<T>(lr + c * 8, f);
 #pragma unroll
@@ -51,20 +60,20 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
       float v = f[k];
       if (!greedy) {
         const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
-        const float u = u01_from_bits((uint32_t)r);
-        v = v * inv_t - __logf(-__logf(u));
+        v = v * inv_t - __logf(-__logf(u01_from_bits((uint32_t)r)));
       }
       better(bv, bi, v, idx);
     }
   }
-  // tail (V not a multiple of 8)
-  for (int idx = (V & ~7) + threadIdx.x; idx < V; idx += blockDim.x) {
-    float v = (float)lr[idx];
-    if (!greedy) {
-      const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
-      v = v * inv_t - __logf(-__logf(u01_from_bits((uint32_t)r)));
+  if (split == SAMPLE_SPLITS - 1) {  // tail (V not a multiple of 8)
+    for (int idx = (V & ~7) + threadIdx.x; idx < V; idx += blockDim.x) {
+      float v = (float)lr[idx];
+      if (!greedy) {
+        const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
+        v = v * inv_t - __logf(-__logf(u01_from_bits((uint32_t)r)));
+      }
+      better(bv, bi, v, idx);
     }
-    better(bv, bi, v, idx);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -79,20 +88,40 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) better(bv, bi, sv[w], si[w]);
-    out[row] = bi;
+    for (int w = 1; w < 4; ++w) better(bv, bi, sv[w], si[w]);
+    pv[row * SAMPLE_SPLITS + split] = bv;
+    pi[row * SAMPLE_SPLITS + split] = bi;
   }
 }
 
-PENNY_API int penny_sample(const void* logits, int is_fp32, long row_stride, const float* temps,
-                           const unsigned long long* seeds, int* out, int B, int V, hipStream_t stream) {
-  if (B <= 0) return 0;
-  if (is_fp32) {
-    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(1024), 0, stream, (const float*)logits, row_stride, temps,
-                       seeds, out, V);
-  } else {
-    hipLaunchKernelGGL(sample_kernel<bf16>, dim3(B), dim3(1024), 0, stream, (const bf16*)logits, row_stride, temps,
-                       seeds, out, V);
+__global__ void sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi, int* __restrict__ out) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  float bv = lane < SAMPLE_SPLITS ? pv[row * SAMPLE_SPLITS + lane] : -INFINITY;
+  int bi = lane < SAMPLE_SPLITS ? pi[row * SAMPLE_SPLITS + lane] : 0x7fffffff;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    better(bv, bi, ov, oi);
   }
+  if (lane == 0) out[row] = bi;
+}
+
+// workspace: B * SAMPLE_SPLITS floats + B * SAMPLE_SPLITS ints
+PENNY_API int penny_sample(const void* logits, int is_fp32, long row_stride, const float* temps,
+                           const unsigned long long* seeds, int* out, void* workspace, int B, int V,
+                           hipStream_t stream) {
+  if (B <= 0) return 0;
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + (long)B * SAMPLE_SPLITS);
+  dim3 grid(B, SAMPLE_SPLITS);
+  if (is_fp32) {
+    hipLaunchKernelGGL(sample_partial_kernel<float>, grid, dim3(256), 0, stream, (const float*)logits, row_stride,
+                       temps, seeds, pv, pi, V);
+  } else {
+    hipLaunchKernelGGL(sample_partial_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)logits, row_stride,
+                       temps, seeds, pv, pi, V);
+  }
+  hipLaunchKernelGGL(sample_final_kernel, dim3(B), dim3(64), 0, stream, pv, pi, out);
   PENNY_RETURN_LAUNCH();
 }

@@ -1,0 +1,91 @@
+"""Projection GEMMs: hand-written MFMA skinny GEMM for decode (M <= 64), hipBLASLt otherwise.
+
+``linear(x, w, epilogue=...)`` is the single entry point the models use:
+
+* M <= 64 on the GPU -> ``penny_skinny_gemm`` (weight-streaming MFMA kernel, fused epilogues:
+  ``"silu"`` for the 16-row-interleaved gate|up weight, ``"residual"`` add);
+* otherwise (prefill) -> hipBLASLt via ``torch.nn.functional.linear`` followed by the matching
+  HIP epilogue kernel (``silu_mul(interleave16=True)``) or a fused add.
+
+Per-shape launch configs (rows per workgroup, waves per workgroup) come from ``TUNING`` --
+measured on MI355X with ``bench/kernels.py --only skinny`` -- with a heuristic fallback.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from .activation import silu_mul
+
+EPI = {None: 0, "silu": 1, "residual": 2}
+MAX_SKINNY_M = 64
+# (N, K) -> (ntf, nw): 16*ntf weight rows per workgroup, nw waves splitting K.  Measured on MI355X
+# (profiles/r1_skinny_gemm.jsonl): the hand-written kernel beats hipBLASLt by 1.3-1.6x on the
+# small-N projections (QKV, O) at M <= 16 and ties at M = 64; hipBLASLt already streams the wide
+# gate|up / LM-head weights at ~6 TB/s, so those stay on the library.
+TUNING: Dict[Tuple[int, int], Tuple[int, int]] = {(6144, 4096): (2, 4), (4096, 4096): (1, 4)}
+SKINNY_MAX_M: Dict[Tuple[int, int], int] = {(6144, 4096): 16, (4096, 4096): 32}
+
+
+def _config(N_: int, K: int, epilogue: Optional[str]) -> Tuple[int, int]:
+    if (N_, K) in TUNING:
+        return TUNING[(N_, K)]
+    ntf = 2
+    wgs = N_ // (16 * ntf)
+    nw = 8 if wgs < 512 else 4
+    if K % (nw * 128):
+        nw = 4 if K % 512 == 0 else 1
+    return ntf, nw
+
+
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> MFMA-fragment-tiled [N/16, K/32, 64, 8] copy for the decode GEMM: fragment
+    (row group, k-step) is 1 KiB contiguous and a row group's k-steps are consecutive."""
+    N_, K = w.shape
+    assert N_ % 16 == 0 and K % 32 == 0
+    return w.view(N_ // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N_ // 16, K // 32, 64, 8).contiguous()
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
+              wt: Optional[torch.Tensor] = None) -> bool:
+    M, K = x.shape
+    N_ = w.shape[0]
+    if wt is None or not N.use_native(x) or M > MAX_SKINNY_M or os.environ.get("PENNY_SKINNY", "1") == "0":
+        return False
+    if M > SKINNY_MAX_M.get((N_, K), MAX_SKINNY_M if (N_, K) in TUNING else 0):
+        return False
+    ntf, nw = _config(N_, K, epilogue)
+    return N_ % (16 * ntf) == 0 and K % (nw * 128) == 0 and x.stride(1) == 1 and w.is_contiguous()
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
+           residual: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T with an optional fused epilogue ("silu": w is gate|up 16-interleaved).
+
+    ``wt`` is the fragment-tiled copy of ``w`` (``tile_weight``); when given, decode-sized
+    batches (M <= 64) run the hand-written MFMA kernel on it."""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if skinny_ok(x, w, epilogue, wt):
+        ntf, nw = _config(N_, K, epilogue)
+        out_n = N_ // 2 if epilogue == "silu" else N_
+        y = torch.empty((M, out_n), dtype=x.dtype, device=x.device)
+        N.call("penny_skinny_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), out_n, N.ptr(residual),
+               residual.stride(0) if residual is not None else 0, M, N_, EPI[epilogue], ntf, nw, N.stream())
+        return y
+    y = F.linear(x, w)
+    if epilogue == "silu":
+        return silu_mul(y, interleave16=True)
+    if epilogue == "residual":
+        return (y.float() + residual.float()).to(y.dtype) if not N.use_native(y) else y.add_(residual)
+    return y
+
+
+def interleave16(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """[F, H] gate and up -> [2F, H] with rows alternating in 16-row groups (skinny SiLU layout)."""
+    Fr, H = gate.shape
+    return torch.stack([gate.view(Fr // 16, 16, H), up.view(Fr // 16, 16, H)], dim=1).reshape(2 * Fr, H)

@@ -7,6 +7,8 @@ import torch
 
 from . import _native as N
 
+SPLITS = 16  # vocab slices per row in the HIP sampler (SAMPLE_SPLITS)
+
 
 def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -20,8 +22,9 @@ def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor
     if N.use_native(logits):
         out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
         assert logits.stride(1) == 1 and logits.stride(0) % 8 == 0
+        ws = torch.empty((B * SPLITS * 2,), dtype=torch.float32, device=logits.device)
         N.call("penny_sample", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
-               N.ptr(temperatures), N.ptr(seeds), N.ptr(out), B, V, N.stream())
+               N.ptr(temperatures), N.ptr(seeds), N.ptr(out), N.ptr(ws), B, V, N.stream())
         return out
     res = torch.empty((B,), dtype=torch.int32)
     lf = logits.float()

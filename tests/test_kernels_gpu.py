@@ -195,3 +195,35 @@ def test_filtered_topk():
         # ids may differ only where scores tie within rounding
         same = (ids[i, :c].cpu() == rids[i, :c]).float().mean().item() if c else 1.0
         assert same > 0.97
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("cfg", [(2, 4), (2, 8), (4, 4), (1, 8)])
+def test_skinny_gemm(M, cfg):
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(9)
+    N_, K = 512, 2048
+    x = rnd(M, K, gen=g)
+    w = rnd(N_, K, scale=0.05, gen=g)
+    gemm.TUNING[(N_, K)] = cfg
+    try:
+        y = gemm.linear(x.to(DEV), w.to(DEV), wt=gemm.tile_weight(w.to(DEV)))
+        ref = (x.float() @ w.float().t())
+        close(y, ref, atol=2e-2)
+        if cfg[0] % 2 == 0:
+            gate, up = w[:256], w[256:]
+            wi = gemm.interleave16(gate, up)
+            wid = wi.to(DEV).contiguous()
+            y2 = gemm.linear(x.to(DEV), wid, epilogue="silu", wt=gemm.tile_weight(wid))
+            ref2 = ops.silu_mul(torch.cat([(x.float() @ gate.float().t()), (x.float() @ up.float().t())], -1).to(torch.bfloat16))
+            close(y2, ref2, atol=3e-2)
+    finally:
+        gemm.TUNING.pop((N_, K), None)
+
+
+def test_silu_mul_interleaved():
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(10)
+    gate, up = rnd(13, 256, gen=g), rnd(13, 256, gen=g)
+    il = gemm.interleave16(gate.t().contiguous(), up.t().contiguous()).t().contiguous()
+    close(ops.silu_mul(il.to(DEV), interleave16=True), ops.silu_mul(torch.cat([gate, up], -1)), atol=2e-2)
