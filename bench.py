@@ -36,7 +36,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--convs", type=int, default=64, help="concurrent conversations per GPU")
+    ap.add_argument("--convs", type=int, default=128, help="concurrent conversations per GPU")
     ap.add_argument("--respond-tokens", type=int, default=128)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--embed-model", default="bge-base-en")
