@@ -61,7 +61,8 @@ class LLMEngine:
         self.tokenizer = tokenizer or load_tokenizer(cfg.tokenizer, self.model.cfg.vocab_size)
         self.eos_ids = set(self.tokenizer.eos_ids)
         nblocks = plan_kv_blocks(cfg, self.model, device)
-        self.kv = KVCache(self.model.cfg.num_layers, nblocks, self.model.hkv, self.model.D, device=device)
+        self.kv = KVCache(self.model.cfg.num_layers, nblocks, self.model.hkv, self.model.D,
+                          dtype=getattr(self.model, "dtype", torch.bfloat16), device=device)
         self.bm = make_block_manager(nblocks, KV_BS, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,

@@ -1,0 +1,134 @@
+"""Multi-GPU serving launcher: one process per GPU, DP replicas of TP groups (torchrun).
+
+    # 8 x Llama-3-8B replicas, each its own Kafka consumer in group "message_consumer"
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m financial_chatbot_llm_amd.serving.launch --tp 1
+    # one Llama-3-70B TP=8 group (north-star config 4)
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m financial_chatbot_llm_amd.serving.launch \\
+        --tp 8 --model llama3-70b --tool-steps 3
+
+The reference scales by running N gunicorn worker processes that each consume Kafka serially
+(``gunicorn.conf.py:8-9``, ``main.py:131-138``).  Here each TP-group LEADER owns one engine
+replica and one Kafka consumer in the same group (Kafka spreads partitions across replicas, per
+key ordering preserved); its event loop runs hundreds of concurrent turns that batch inside the
+engine.  Non-leader TP ranks replay the leader's steps (``LLMEngine.follower_loop``).  The global
+rank 0 additionally serves the FastAPI surface (``/health``, ``/metrics``, ...) on ``--port``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import sys
+
+from .. import config
+from ..utils.logging import get_logger
+
+logger = get_logger(__name__)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tp", type=int, default=int(os.environ.get("PENNY_TP", "1")))
+    ap.add_argument("--model", default=os.environ.get("PENNY_MODEL", "llama3-8b"))
+    ap.add_argument("--embed-model", default=os.environ.get("PENNY_EMBED_MODEL", "bge-base-en"))
+    ap.add_argument("--corpus", type=int, default=int(os.environ.get("PENNY_CORPUS_SIZE", "0")))
+    ap.add_argument("--users", type=int, default=int(os.environ.get("PENNY_CORPUS_USERS", "10000")))
+    ap.add_argument("--port", type=int, default=int(os.environ.get("PORT", "8000")))
+    ap.add_argument("--tool-steps", type=int, default=1, help=">1 enables the multi-step agent (retrieval + plot)")
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--no-http", action="store_true")
+    ap.add_argument("--smoke", action="store_true", help="serve one synthetic turn from the in-memory broker and exit")
+    return ap.parse_args(argv)
+
+
+def build_leader_services(args, engine, device):
+    from ..adapters import Database, InMemoryBroker, KafkaClient
+    from ..agent import LLMAgent
+    from ..engine.backend import EngineLLM
+    from ..retrieval import BgeEmbedder, DeviceVectorStore, HashEmbedder, NumpyVectorStore, RetrievalService
+    from ..tools import make_plot_tool, make_retrieval_tool
+    from .app import Services
+
+    if device.type == "cuda":
+        embedder = BgeEmbedder(args.embed_model, device=str(device))
+        store = DeviceVectorStore(embedder.dim, device=str(device))
+        if args.corpus:
+            store.load_synthetic(args.corpus, args.users)
+    else:
+        embedder = HashEmbedder(768)
+        store = NumpyVectorStore(768)
+    retrieval = RetrievalService(embedder, store)
+    llm = EngineLLM(engine, max_model_len=args.max_model_len)
+    serving = config.ServingConfig.from_env()
+    agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
+                     temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
+                     max_tool_steps=args.tool_steps)
+    broker = InMemoryBroker() if args.smoke else None
+    return Services(db=Database(uri="" if args.smoke else None), kafka=KafkaClient(broker=broker), agent=agent,
+                    engine=engine, retrieval=retrieval, serving=serving)
+
+
+async def _smoke_turn(services) -> dict:
+    import json
+
+    from ..serving.worker import ChatWorker
+    services.db.put_context({"conversation_id": "smoke", "user_id": "user-000001", "name": "Smoke", "income": 5000,
+                             "savings_goal": 500, "accounts": [], "additional_monthly_expenses": []})
+    services.db.put_user_message("smoke", "How should I budget?", "user-000001", 1)
+    services.kafka.setup_consumer()
+    w = ChatWorker(services.db, services.kafka, services.agent)
+    task = asyncio.create_task(w.consume_messages())
+    services.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key="smoke", value=json.dumps(
+        {"message": "How should I budget?", "conversation_id": "smoke", "user_id": "user-000001"}))
+    while not w.traces:
+        await asyncio.sleep(0.01)
+    w.stop()
+    await task
+    return services.kafka.broker.values(config.AI_RESPONSE_TOPIC)[-1]
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    import torch
+
+    from ..engine.async_engine import AsyncEngine
+    from ..engine.llm_engine import LLMEngine
+    from ..parallel.dist import init_distributed, shutdown
+
+    ps = init_distributed(tp_size=args.tp)
+    dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    device = torch.device(dev_type, torch.cuda.current_device()) if dev_type == "cuda" else torch.device("cpu")
+    ecfg = config.EngineConfig.from_env(model=args.model, tp_size=args.tp, max_model_len=args.max_model_len,
+                                        device=dev_type, use_cuda_graph=dev_type == "cuda")
+    engine = LLMEngine(ecfg)
+    engine.warmup()   # every TP rank captures the same decode graphs (collectives inside)
+    if not ps.is_tp_leader:
+        engine.follower_loop()
+        shutdown()
+        return 0
+    aengine = AsyncEngine(engine=engine, warmup=False)
+    services = build_leader_services(args, aengine, device)
+    if args.smoke:
+        last = asyncio.run(_smoke_turn(services))
+        print(f"[launch r{ps.rank}] smoke turn complete: type={last.get('type')} error={last.get('error')}", flush=True)
+        aengine.shutdown()
+        shutdown()
+        return 0 if last.get("type") == "complete" else 1
+    from .app import create_app
+    app = create_app(services)
+    if ps.rank == 0 and not args.no_http:
+        import uvicorn
+        uvicorn.run(app, host="0.0.0.0", port=args.port, log_level="warning")
+    else:  # other DP replicas: Kafka consumer only (lifespan without HTTP)
+        async def run_headless():
+            async with app.router.lifespan_context(app):
+                await asyncio.Event().wait()
+        asyncio.run(run_headless())
+    aengine.shutdown()
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
