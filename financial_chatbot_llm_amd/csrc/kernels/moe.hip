@@ -1,0 +1,277 @@
+// K13: Mixtral-style sparse MoE on CDNA4 fp8 MFMA (OCP e4m3; v_mfma_f32_16x16x32_fp8_fp8).
+//
+// Decode-step pipeline (every launch graph-capturable; buffers sized for the max batch):
+//   1. moe_route:   router logits [T, E] -> softmax (f32), top-K, renormalise (HF Mixtral),
+//                   counting sort of the T*K (token, expert) pairs by expert ->
+//                   sorted token ids / routing weights, expert offsets [E+1], inverse map.
+//   2. quant_rows:  dynamic per-row fp8 quantisation of the activations (scale = amax / 448).
+//   3. moe_gemm<SILU>: per (expert, 32-row weight slice) workgroup: gathered token rows x W13_e
+//                   (fp8 x fp8 MFMA, f32 acc), dequantised by row scales x weight scales, fused
+//                   SiLU(gate) * up (16-row interleaved W13) -> [P, F] bf16.
+//   4. quant_rows on [P, F], then moe_gemm<SCALE_W>: x W2_e, output scaled by the routing weight.
+//   5. moe_combine: out[t] = sum over its K pairs (inverse map, no atomics).
+// Weights are pre-tiled (ops/moe.py tile_fp8_weight): fragment pair (row group, 2 k-steps) is
+// 1 KiB contiguous -- lane l holds 8 bytes of k-step 2p then 8 bytes of k-step 2p+1 -- so each
+// weight load is one coalesced 16-byte-per-lane instruction; fp8 halves the bytes streamed per
+// decode step versus bf16 (the whole expert bank is touched at decode batch sizes).
+#include "common.h"
+
+#define FP8_MAX 448.0f
+
+// ---------------------------------------------------------------------------------------------
+// 1. routing (single workgroup; T*K <= MOE_ROUTE_CAP pairs, E <= 64: decode batches)
+// ---------------------------------------------------------------------------------------------
+#define MOE_ROUTE_CAP 4096
+
+__global__ void __launch_bounds__(1024) moe_route_kernel(const bf16* __restrict__ logits, int T, int E, int K,
+                                                         int* __restrict__ sorted_tok, float* __restrict__ sorted_w,
+                                                         int* __restrict__ offsets, int* __restrict__ inv) {
+  __shared__ int cnt[64], cur[64];
+  __shared__ int pe[MOE_ROUTE_CAP];    // expert of pair (t, j)
+  __shared__ float pw[MOE_ROUTE_CAP];  // renormalised routing weight of pair (t, j)
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  // pass 1: softmax (f32) + top-K + renormalise per token; count pairs per expert
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    float p[64];
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) {
+      p[e] = (float)logits[(long)t * E + e];
+      mx = fmaxf(mx, p[e]);
+    }
+    for (int e = 0; e < E; ++e) p[e] = __expf(p[e] - mx);
+    float ws = 0.f;
+    for (int j = 0; j < K; ++j) {
+      int best = 0;
+      for (int e = 1; e < E; ++e)
+        if (p[e] > p[best]) best = e;
+      atomicAdd(&cnt[best], 1);
+      pe[t * K + j] = best;
+      pw[t * K + j] = p[best];
+      ws += p[best];
+      p[best] = -1.f;
+    }
+    for (int j = 0; j < K; ++j) pw[t * K + j] /= ws;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      offsets[e] = acc;
+      cur[e] = acc;
+      acc += cnt[e];
+    }
+    offsets[E] = acc;
+  }
+  __syncthreads();
+  // pass 2: scatter pairs into their expert buckets (order inside a bucket is irrelevant: every
+  // pair's rows are computed independently)
+  for (int i = threadIdx.x; i < T * K; i += blockDim.x) {
+    const int pos = atomicAdd(&cur[pe[i]], 1);
+    inv[i] = pos;
+    sorted_tok[pos] = i / K;
+    sorted_w[pos] = pw[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2. dynamic per-row fp8 quantisation (one workgroup per row; row length multiple of 8)
+// ---------------------------------------------------------------------------------------------
+__global__ void quant_rows_kernel(const bf16* __restrict__ x, int ld, int n, unsigned char* __restrict__ q,
+                                  float* __restrict__ scale) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (long)row * ld);
+  float amax = 0.f;
+  for (int c = threadIdx.x; c < n / 8; c += blockDim.x) {
+    float f[8];
+    unpack8(xr[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(f[i]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) amax = fmaxf(amax, red[i]);
+  const float s = amax > 0.f ? amax / FP8_MAX : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[row] = s;
+  uint2* qr = reinterpret_cast<uint2*>(q + (long)row * n);
+  for (int c = threadIdx.x; c < n / 8; c += blockDim.x) {
+    float f[8];
+    unpack8(xr[c], f);
+    uint32_t w0 = 0, w1 = 0;
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[0] * inv, f[1] * inv, w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(f[2] * inv, f[3] * inv, w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[4] * inv, f[5] * inv, w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(f[6] * inv, f[7] * inv, w1, true);
+    qr[c] = make_uint2(w0, w1);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 3/4. grouped fp8 GEMM over expert buckets
+// ---------------------------------------------------------------------------------------------
+#define MOE_EPI_SILU 1
+#define MOE_EPI_ROUTEW 2
+
+template <int NTF, int NW, int EPI>
+__global__ void __launch_bounds__(NW * 64) moe_gemm_kernel(
+    const unsigned char* __restrict__ Xq, const float* __restrict__ xs, const int* __restrict__ rows,
+    const int* __restrict__ offsets, const unsigned char* __restrict__ Wt, const float* __restrict__ ws,
+    const float* __restrict__ route_w, bf16* __restrict__ Y, int N, int K) {
+  constexpr int NR = 16 * NTF;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [NW][NR][64]
+  const int e = blockIdx.y;
+  const int p0 = offsets[e], p1 = offsets[e + 1];
+  if (p1 <= p0) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+  const int n0 = blockIdx.x * NR;
+  const int kper = K / NW, kb = w * kper;
+  const long kpairs = K / 64;
+  const unsigned char* We = Wt + (long)e * N * K;
+  for (int c0 = p0; c0 < p1; c0 += 64) {  // token chunks of 64 pairs
+    const int nrow = min(64, p1 - c0);
+    f32x4 acc[NTF][4];
+#pragma unroll
+    for (int f = 0; f < NTF; ++f)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[f][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* xr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int pr = c0 + min(16 * m + col, nrow - 1);
+      const int src = rows ? rows[pr] : pr;
+      xr[m] = Xq + (long)src * K + kb + 8 * g;
+    }
+    for (int k = 0; k < kper; k += 64) {
+      uint4 wv[NTF];
+#pragma unroll
+      for (int f = 0; f < NTF; ++f)
+        wv[f] = *reinterpret_cast<const uint4*>(We + (((long)(n0 / 16 + f) * kpairs + (kb + k) / 64) * 64 + lane) * 16);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        long xv[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) xv[m] = *reinterpret_cast<const long*>(xr[m] + k + 32 * half);
+#pragma unroll
+        for (int f = 0; f < NTF; ++f) {
+          const long a = half ? ((long)wv[f].w << 32 | wv[f].z) : ((long)wv[f].y << 32 | wv[f].x);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, xv[m], acc[f][m], 0, 0, 0);
+        }
+      }
+    }
+    float* mine = red + w * NR * 64;
+#pragma unroll
+    for (int f = 0; f < NTF; ++f)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mine[(16 * f + 4 * g + r) * 64 + 16 * m + col] = acc[f][m][r];
+    __syncthreads();
+    constexpr int OUTN = (EPI == MOE_EPI_SILU) ? NR / 2 : NR;
+    const int ldy = (EPI == MOE_EPI_SILU) ? N / 2 : N;
+    for (int idx = threadIdx.x; idx < 64 * (OUTN / 8); idx += NW * 64) {
+      const int m = idx / (OUTN / 8), c8 = (idx % (OUTN / 8)) * 8;
+      if (m >= nrow) continue;
+      const int pr = c0 + m;
+      const float sx = xs[rows ? rows[pr] : pr];
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (EPI == MOE_EPI_SILU) {
+          const int c = c8 + j, pair = c >> 4, jj = c & 15;
+          const int rg = 32 * pair + jj, ru = rg + 16;
+          float gs = 0.f, us = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) {
+            gs += red[(ww * NR + rg) * 64 + m];
+            us += red[(ww * NR + ru) * 64 + m];
+          }
+          const float gv = (float)(bf16)(gs * sx * ws[(long)e * N + n0 + rg]);
+          const float uv = (float)(bf16)(us * sx * ws[(long)e * N + n0 + ru]);
+          o[j] = (float)(bf16)(gv / (1.f + __expf(-gv))) * uv;
+        } else {
+          float s = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) s += red[(ww * NR + c8 + j) * 64 + m];
+          o[j] = s * sx * ws[(long)e * N + n0 + c8 + j] * route_w[pr];
+        }
+      }
+      const int ncol = (EPI == MOE_EPI_SILU) ? (n0 / 2 + c8) : (n0 + c8);
+      *reinterpret_cast<uint4*>(Y + (long)pr * ldy + ncol) = pack8(o);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 5. combine the K expert outputs of each token
+// ---------------------------------------------------------------------------------------------
+__global__ void moe_combine_kernel(const bf16* __restrict__ Y2, const int* __restrict__ inv, int K, int H,
+                                   bf16* __restrict__ out) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < K; ++j) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(Y2 + (long)inv[t * K + j] * H)[c], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+    }
+    reinterpret_cast<uint4*>(out + (long)t * H)[c] = pack8(acc);
+  }
+}
+
+PENNY_API int penny_moe_route(const void* logits, int T, int E, int K, int* sorted_tok, float* sorted_w, int* offsets,
+                              int* inv, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (E > 64 || K > 8 || K > E || T * K > MOE_ROUTE_CAP) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(1024), 0, stream, (const bf16*)logits, T, E, K, sorted_tok,
+                     sorted_w, offsets, inv);
+  PENNY_RETURN_LAUNCH();
+}
+
+PENNY_API int penny_quant_rows_fp8(const void* x, int ld, int rows, int n, void* q, float* scale, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_rows_kernel, dim3(rows), dim3(256), 0, stream, (const bf16*)x, ld, n, (unsigned char*)q,
+                     scale);
+  PENNY_RETURN_LAUNCH();
+}
+
+// epi 1: SiLU-gated (W13 interleaved, Y [P, N/2]); epi 2: scale by routing weight (Y [P, N])
+PENNY_API int penny_moe_gemm_fp8(const void* Xq, const float* xs, const int* rows, const int* offsets, const void* Wt,
+                                 const float* ws, const float* route_w, void* Y, int E, int N, int K, int epi,
+                                 hipStream_t stream) {
+  constexpr int NTF = 2;
+  if (N % (16 * NTF) || K % 64) return (int)hipErrorInvalidValue;
+  dim3 grid(N / (16 * NTF), E);
+  // waves split K: as many as divide it into whole 64-wide k-pairs (4 for every real model)
+#define MOE_LAUNCH(NW_)                                                                                          \
+  {                                                                                                              \
+    const size_t lds = (size_t)NW_ * 16 * NTF * 64 * sizeof(float);                                             \
+    if (epi == MOE_EPI_SILU)                                                                                     \
+      hipLaunchKernelGGL((moe_gemm_kernel<NTF, NW_, MOE_EPI_SILU>), grid, dim3(NW_ * 64), lds, stream,          \
+                         (const unsigned char*)Xq, xs, rows, offsets, (const unsigned char*)Wt, ws, route_w,     \
+                         (bf16*)Y, N, K);                                                                        \
+    else                                                                                                         \
+      hipLaunchKernelGGL((moe_gemm_kernel<NTF, NW_, MOE_EPI_ROUTEW>), grid, dim3(NW_ * 64), lds, stream,        \
+                         (const unsigned char*)Xq, xs, rows, offsets, (const unsigned char*)Wt, ws, route_w,     \
+                         (bf16*)Y, N, K);                                                                        \
+  }
+  if (K % 256 == 0) MOE_LAUNCH(4)
+  else if (K % 128 == 0) MOE_LAUNCH(2)
+  else MOE_LAUNCH(1)
+#undef MOE_LAUNCH
+  PENNY_RETURN_LAUNCH();
+}
+
+PENNY_API int penny_moe_combine(const void* Y2, const int* inv, int T, int K, int H, void* out, hipStream_t stream) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, stream, (const bf16*)Y2, inv, K, H, (bf16*)out);
+  PENNY_RETURN_LAUNCH();
+}

@@ -7,18 +7,17 @@ top-2-of-8 mixture of SiLU-gated experts:
     expert  y_e = W2_e (silu(W1_e h) * W3_e h)
     combine out = sum_k p_k y_{e_k}
 
-Two execution forms, chosen per step:
-* grouped (prefill, large T): tokens are bucketed by expert (``ops.moe.route``) and each expert
-  runs ONE GEMM pair over its bucket -- 2/8 of the dense FLOPs.
-* dense-masked (decode, small T, hipGraph-capturable): every expert runs over the whole batch
-  and the routing weights (zero for unselected experts) scale the combine.  At decode batch
-  sizes every expert's weights are streamed anyway, so this costs no extra HBM traffic and has
-  no data-dependent shapes.
+Execution forms:
+* fp8 experts on the GPU, decode-sized steps (T*top_k <= 4096): the HIP pipeline of
+  ``csrc/kernels/moe.hip`` -- device routing + counting sort, dynamic per-token fp8
+  activations, grouped fp8 x fp8 MFMA GEMMs over expert buckets with fused SiLU / routing-weight
+  epilogues, atomics-free combine.  Weights are OCP e4m3 with per-output-row scales, stored in
+  MFMA-fragment tiles, halving the expert bytes streamed per decode step vs bf16.
+* otherwise (prefill, CPU, bf16 experts): tokens are bucketed by expert (``ops.moe.route``) and
+  each expert runs one GEMM pair over its bucket (hipBLASLt; fp8 experts dequantised per layer).
 
 TP shards every expert's intermediate dimension (column-parallel W1|W3, row-parallel W2); the
-partial sums join the O-projection's all-reduce pattern (C1).  Expert weights may be stored in
-OCP fp8-e4m3 with per-output-channel scales (``fp8=True``), halving the expert bytes streamed
-per decode step.
+partial sums are all-reduced like the dense MLP (C1).
 """
 from __future__ import annotations
 
@@ -29,16 +28,16 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import moe as moe_ops
+from ..ops.gemm import linear
 from ..parallel import comm
 from .llama import DecoderModel
 
 
 class MixtralModel(DecoderModel):
-    dense_threshold = 64   # tokens per step at or below which the dense-masked form is used
-
     def __init__(self, *a, fp8: bool = False, **kw):
         super().__init__(*a, **kw)
         self.fp8 = fp8
+        self._moe_ws = None
 
     def mlp_shapes(self, p: str) -> Dict[str, tuple]:
         c = self.cfg
@@ -52,43 +51,56 @@ class MixtralModel(DecoderModel):
         return self
 
     def quantize_experts(self) -> None:
+        """bf16 experts -> fp8 e4m3 (per-row scales), W1|W3 interleaved by 16 rows, fragment-tiled."""
         for i in range(self.cfg.num_layers):
             p = f"layers.{i}."
-            for k in ("w13", "w2"):
-                q, s = moe_ops.quantize_fp8_rowwise(self.w[p + k])
-                self.w[p + k] = q
-                self.w[p + k + "_scale"] = s
+            w13 = self.w.pop(p + "w13")
+            half = w13.shape[1] // 2
+            w13 = torch.stack([ops.gemm.interleave16(w13[e, :half], w13[e, half:]) for e in range(w13.shape[0])])
+            for k, w in ((p + "w13", w13), (p + "w2", self.w.pop(p + "w2"))):
+                q, s = moe_ops.quantize_fp8_rowwise(w)
+                self.w[k + "_t"] = moe_ops.tile_fp8_weight(q)
+                self.w[k + "_scale"] = s.float().contiguous()
+        self.fp8 = True
 
-    def _expert_weights(self, p: str, e: int):
-        w13, w2 = self.w[p + "w13"][e], self.w[p + "w2"][e]
-        if self.fp8:
-            w13 = moe_ops.dequant_fp8(w13, self.w[p + "w13_scale"][e])
-            w2 = moe_ops.dequant_fp8(w2, self.w[p + "w2_scale"][e])
-        return w13, w2
+    def _dequant(self, p: str, key: str) -> torch.Tensor:
+        q = moe_ops.untile_fp8_weight(self.w[p + key + "_t"])
+        return moe_ops.dequant_fp8(q, self.w[p + key + "_scale"], self.dtype)
+
+    def _moe_workspace(self, T: int):
+        c = self.cfg
+        if self._moe_ws is None or self._moe_ws.max_tokens < T:
+            f_local = self.w["layers.0.w13_scale"].shape[-1] // 2   # per-rank expert FFN width
+            self._moe_ws = moe_ops.MoEWorkspace(max(T, 256), c.top_k_experts, c.num_experts, c.hidden_size,
+                                                f_local, self.device)
+        return self._moe_ws
 
     def mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
         p = f"layers.{i}."
         c = self.cfg
         T = h.shape[0]
-        logits = F.linear(h, self.w[p + "router"])
+        logits = linear(h, self.w[p + "router"])
+        if self.fp8 and ops._native.use_native(h) and T * c.top_k_experts <= 4096:
+            out = moe_ops.moe_decode_fp8(h.contiguous(), logits.contiguous(), self.w[p + "w13_t"],
+                                         self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
+                                         c.top_k_experts, self._moe_workspace(T))
+            return comm.tp_all_reduce(out) if self.tp_size > 1 else out
         topw, topi = moe_ops.topk_softmax(logits, c.top_k_experts)
+        order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
+        offs = offsets.tolist()
+        xs = h.index_select(0, tok_idx)
+        ys = torch.zeros_like(xs)
+        w13_all = self._dequant(p, "w13") if self.fp8 else None
+        w2_all = self._dequant(p, "w2") if self.fp8 else None
+        for e in range(c.num_experts):
+            a, b = offs[e], offs[e + 1]
+            if b <= a:
+                continue
+            if self.fp8:
+                act = ops.silu_mul(F.linear(xs[a:b], w13_all[e]), interleave16=True)
+                ys[a:b] = F.linear(act, w2_all[e])
+            else:
+                ys[a:b] = F.linear(ops.silu_mul(F.linear(xs[a:b], self.w[p + "w13"][e])), self.w[p + "w2"][e])
         out = torch.zeros_like(h)
-        if T <= self.dense_threshold:
-            dense_w = torch.zeros((T, c.num_experts), dtype=torch.float32, device=h.device)
-            dense_w.scatter_(1, topi.long(), topw)
-            for e in range(c.num_experts):
-                w13, w2 = self._expert_weights(p, e)
-                y = F.linear(ops.silu_mul(F.linear(h, w13)), w2)
-                out += (y.float() * dense_w[:, e:e + 1]).to(h.dtype)
-        else:
-            order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
-            offs = offsets.tolist()
-            xs = h.index_select(0, tok_idx)
-            ys = torch.empty_like(xs)
-            for e in range(c.num_experts):
-                a, b = offs[e], offs[e + 1]
-                if b > a:
-                    w13, w2 = self._expert_weights(p, e)
-                    ys[a:b] = F.linear(ops.silu_mul(F.linear(xs[a:b], w13)), w2)
-            out.index_add_(0, tok_idx, (ys.float() * tok_w[:, None]).to(h.dtype))
+        out.index_add_(0, tok_idx, (ys.float() * tok_w[:, None]).to(h.dtype))
         return comm.tp_all_reduce(out) if self.tp_size > 1 else out

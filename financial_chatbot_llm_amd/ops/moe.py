@@ -46,3 +46,94 @@ def quantize_fp8_rowwise(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
 
 def dequant_fp8(q: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
     return (q.float() * scale[..., None]).to(dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# fp8 expert bank in MFMA-fragment tiles + the HIP decode pipeline (csrc/kernels/moe.hip)
+# ----------------------------------------------------------------------------------------------
+def tile_fp8_weight(q: torch.Tensor) -> torch.Tensor:
+    """fp8 [E, N, K] -> uint8 [E, N/16, K/64, 64, 16]: fragment pair (row group, 2 k-steps) is
+    1 KiB contiguous; lane 16g+r holds row r, k = 64p + 32s + 8g + j at byte 8s + j."""
+    E, N_, K = q.shape
+    assert N_ % 16 == 0 and K % 64 == 0
+    u = q.view(torch.uint8).view(E, N_ // 16, 16, K // 64, 2, 4, 8)      # e rg r kp s g j
+    return u.permute(0, 1, 3, 5, 2, 4, 6).reshape(E, N_ // 16, K // 64, 64, 16).contiguous()
+
+
+def untile_fp8_weight(t: torch.Tensor) -> torch.Tensor:
+    E, RG, KP, _, _ = t.shape
+    u = t.view(E, RG, KP, 4, 16, 2, 8).permute(0, 1, 4, 2, 5, 3, 6)       # e rg r kp s g j
+    return u.reshape(E, RG * 16, KP * 64).contiguous().view(FP8)
+
+
+def _fake_quant_rows(x: torch.Tensor) -> torch.Tensor:
+    """Round-trip rows through dynamic per-row fp8 e4m3 (what ``penny_quant_rows_fp8`` does)."""
+    q, s = quantize_fp8_rowwise(x)
+    return q.float() * s[..., None]
+
+
+def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act: bool = False):
+    """fp32 reference of the fp8 MoE MLP (weights dequantised).  ``quant_act`` additionally rounds
+    both GEMM inputs through dynamic per-row fp8, matching the HIP pipeline's arithmetic."""
+    topw, topi = topk_softmax(h.float() @ router_w.float().t(), top_k)
+    out = torch.zeros(h.shape, dtype=torch.float32, device=h.device)
+    from .activation import silu_mul
+    for e in range(w13q.shape[0]):
+        sel = (topi == e)
+        rows = sel.any(-1).nonzero().flatten()
+        if rows.numel() == 0:
+            continue
+        w13 = w13q[e].float() * s13[e][:, None]
+        w2 = w2q[e].float() * s2[e][:, None]
+        x = h[rows].float()
+        if quant_act:
+            x = _fake_quant_rows(x)
+        a = silu_mul((x @ w13.t()).to(torch.bfloat16), interleave16=True).float()
+        if quant_act:
+            a = _fake_quant_rows(a)
+        y = a @ w2.t()
+        wt = (topw * sel).sum(-1)[rows]
+        out[rows] += y * wt[:, None]
+    return out.to(h.dtype)
+
+
+class MoEWorkspace:
+    """Device buffers for one decode-sized MoE step (reused across layers; graph-capturable)."""
+
+    def __init__(self, max_tokens: int, top_k: int, num_experts: int, H: int, F: int, device):
+        P = max_tokens * top_k
+        self.max_tokens = max_tokens
+        i32 = dict(dtype=torch.int32, device=device)
+        self.sorted_tok = torch.zeros(P, **i32)
+        self.sorted_w = torch.zeros(P, dtype=torch.float32, device=device)
+        self.offsets = torch.zeros(num_experts + 1, **i32)
+        self.inv = torch.zeros(P, **i32)
+        self.xq = torch.zeros((max_tokens, H), dtype=torch.uint8, device=device)
+        self.xs = torch.zeros(max_tokens, dtype=torch.float32, device=device)
+        self.a = torch.zeros((P, F), dtype=torch.bfloat16, device=device)
+        self.aq = torch.zeros((P, F), dtype=torch.uint8, device=device)
+        self.as_ = torch.zeros(P, dtype=torch.float32, device=device)
+        self.y2 = torch.zeros((P, H), dtype=torch.bfloat16, device=device)
+
+
+def moe_decode_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Tensor, s13: torch.Tensor,
+                   w2t: torch.Tensor, s2: torch.Tensor, top_k: int, ws: "MoEWorkspace") -> torch.Tensor:
+    """HIP fp8 MoE for decode-sized batches: route -> quant -> grouped GEMM(SiLU) -> quant ->
+    grouped GEMM(x routing weight) -> combine.  Returns [T, H] bf16 (TP partial sum)."""
+    from . import _native as N
+    T, H = h.shape
+    E, F2 = s13.shape
+    F_ = F2 // 2
+    P = T * top_k
+    st = N.stream()
+    N.call("penny_moe_route", N.ptr(router_logits), T, E, top_k, N.ptr(ws.sorted_tok), N.ptr(ws.sorted_w),
+           N.ptr(ws.offsets), N.ptr(ws.inv), st)
+    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(ws.xq), N.ptr(ws.xs), st)
+    N.call("penny_moe_gemm_fp8", N.ptr(ws.xq), N.ptr(ws.xs), N.ptr(ws.sorted_tok), N.ptr(ws.offsets), N.ptr(w13t),
+           N.ptr(s13), None, N.ptr(ws.a), E, F2, H, 1, st)
+    N.call("penny_quant_rows_fp8", N.ptr(ws.a), F_, P, F_, N.ptr(ws.aq), N.ptr(ws.as_), st)
+    N.call("penny_moe_gemm_fp8", N.ptr(ws.aq), N.ptr(ws.as_), None, N.ptr(ws.offsets), N.ptr(w2t), N.ptr(s2),
+           N.ptr(ws.sorted_w), N.ptr(ws.y2), E, H, F_, 2, st)
+    out = torch.empty_like(h)
+    N.call("penny_moe_combine", N.ptr(ws.y2), N.ptr(ws.inv), T, top_k, H, N.ptr(out), st)
+    return out

@@ -227,3 +227,30 @@ def test_silu_mul_interleaved():
     gate, up = rnd(13, 256, gen=g), rnd(13, 256, gen=g)
     il = gemm.interleave16(gate.t().contiguous(), up.t().contiguous()).t().contiguous()
     close(ops.silu_mul(il.to(DEV), interleave16=True), ops.silu_mul(torch.cat([gate, up], -1)), atol=2e-2)
+
+
+@pytest.mark.parametrize("T", [1, 13, 64, 200])
+def test_moe_fp8_pipeline(T):
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    g = torch.Generator().manual_seed(11)
+    E, H, F_, K = 8, 512, 384, 2
+    h = rnd(T, H, gen=g)
+    router = rnd(E, H, scale=0.2, gen=g)
+    w13 = rnd(E, 2 * F_, H, scale=0.05, gen=g)
+    w2 = rnd(E, H, F_, scale=0.05, gen=g)
+    w13i = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13i)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    ref = moe.moe_fp8_reference(h.float(), router.float(), q13, s13, q2, s2, K)
+    ws = moe.MoEWorkspace(256, K, E, H, F_, DEV)
+    logits = (h.to(DEV) @ router.to(DEV).t()).contiguous()
+    out = moe.moe_decode_fp8(h.to(DEV), logits, moe.tile_fp8_weight(q13.to(DEV)), s13.to(DEV),
+                             moe.tile_fp8_weight(q2.to(DEV)), s2.to(DEV), K, ws)
+    # same arithmetic (fp8 activations, per-row scales) in fp32: only accumulation order/bf16 rounding differ
+    ref_q = moe.moe_fp8_reference(h.float(), router.float(), q13, s13, q2, s2, K, quant_act=True)
+    err_q = (out.float().cpu() - ref_q.float()).abs()
+    assert err_q.mean() < 0.01 * ref_q.float().abs().mean() + 1e-4, (err_q.mean(), ref_q.abs().mean())
+    # vs high-precision activations: two e4m3 roundings of the GEMM inputs cost ~5% relative
+    err = (out.float().cpu() - ref.float()).abs()
+    assert err.mean() < 0.08 * ref.float().abs().mean() + 1e-3, (err.mean(), ref.abs().mean())
+    assert int(ws.offsets[-1]) == T * K
