@@ -12,6 +12,7 @@ import argparse
 import json
 import math
 import statistics
+import time
 from typing import Callable, Dict, List
 
 import torch
@@ -56,7 +57,8 @@ def bench_decode(dev) -> List[Dict]:
     out = []
     g = torch.Generator(device=dev).manual_seed(0)
     Hq, Hkv, D = 32, 8, 128
-    for B, ctx, shared in [(64, 2048, 0), (64, 2048, 1024), (16, 2048, 1024), (64, 512, 0), (128, 4096, 1024)]:
+    for B, ctx, shared in [(64, 2048, 0), (64, 2048, 1024), (16, 2048, 1024), (64, 512, 0), (128, 4096, 1024),
+                           (128, 2304, 1984), (128, 1536, 768), (64, 2304, 1984)]:
         tables, kc, vc, total = _paged(B, ctx, shared, Hkv, D, dev, g)
         q = torch.randn((B, Hq, D), generator=g, device=dev).to(torch.bfloat16)
         lens = torch.full((B,), ctx, dtype=torch.int32, device=dev)
@@ -65,8 +67,19 @@ def bench_decode(dev) -> List[Dict]:
         us = timeit(lambda: ops.decode(q, lens, tables, kc, vc, 0.088, workspace=ws, out=o))
         uniq = (B * ctx - (B - 1) * shared) * Hkv * D * 2 * 2
         logical = B * ctx * Hkv * D * 2 * 2
-        out.append({"op": "decode_attn", "B": B, "ctx": ctx, "shared": shared, "us": round(us, 1),
-                    "GBps_unique": round(uniq / us / 1e3, 1), "GBps_logical": round(logical / us / 1e3, 1)})
+        row = {"op": "decode_attn", "B": B, "ctx": ctx, "shared": shared, "us": round(us, 1),
+               "GBps_unique": round(uniq / us / 1e3, 1), "GBps_logical": round(logical / us / 1e3, 1)}
+        if shared >= 2 * KV_BS:
+            lens_h, tables_h = lens.cpu().numpy(), tables.cpu().numpy()
+            t0 = time.perf_counter()
+            for _ in range(20):
+                plan = ops.plan_cascade(lens_h, tables_h, Hq // Hkv)
+            row["plan_host_us"] = round((time.perf_counter() - t0) / 20 * 1e6, 1)
+            ci = ops.CascadeInputs.from_plan(plan, dev)
+            usc = timeit(lambda: ops.decode(q, lens, tables, kc, vc, 0.088, workspace=ws, out=o, cascade=ci))
+            row["cascade_us"] = round(usc, 1)
+            row["cascade_GBps_unique"] = round(uniq / usc / 1e3, 1)
+        out.append(row)
     return out
 
 
@@ -187,6 +200,48 @@ def bench_skinny(dev) -> List[Dict]:
     return out
 
 
+def bench_moe(dev) -> List[Dict]:
+    """Mixtral-8x7B MoE layer (E=8, top-2, H=4096, F=14336): HIP fp8 pipeline vs bf16 per-expert
+    hipBLASLt GEMMs (the eager bucketed path)."""
+    from ..ops import activation, moe
+    out = []
+    E, H, F_, K = 8, 4096, 14336, 2
+    g = torch.Generator(device=dev).manual_seed(0)
+    w13 = (torch.randn((E, 2 * F_, H), device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    w2 = (torch.randn((E, H, F_), device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    t13, t2 = moe.tile_fp8_weight(q13), moe.tile_fp8_weight(q2)
+    del q13, q2
+    router = torch.randn((E, H), device=dev, generator=g).to(torch.bfloat16)
+    ws = moe.MoEWorkspace(512, K, E, H, F_, dev)
+    for T in (1, 16, 64, 256):
+        h = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
+        logits = (h @ router.t()).contiguous()
+        us = timeit(lambda: moe.moe_decode_fp8(h, logits, t13, s13, t2, s2, K, ws), iters=10)
+        active = int((ws.offsets[1:] > ws.offsets[:-1]).sum())
+        wbytes = active * 3 * H * F_   # fp8 weights of the experts this batch touches
+
+        def bf16_path():
+            topw, topi = moe.topk_softmax(logits, K)
+            _, offsets, tok_idx, tok_w = moe.route(topi, topw, E)
+            offs = offsets.tolist()
+            xs = h.index_select(0, tok_idx)
+            ys = torch.empty_like(xs)
+            for e in range(E):
+                a, b = offs[e], offs[e + 1]
+                if b > a:
+                    ys[a:b] = torch.nn.functional.linear(
+                        activation.silu_mul(torch.nn.functional.linear(xs[a:b], w13[e])), w2[e])
+            o = torch.zeros_like(h)
+            o.index_add_(0, tok_idx, (ys.float() * tok_w[:, None]).to(h.dtype))
+        base = timeit(bf16_path, iters=5)
+        out.append({"op": "moe", "T": T, "active_experts": active, "fp8_us": round(us, 1),
+                    "fp8_GBps": round(wbytes / us / 1e3, 1), "bf16_hipblaslt_us": round(base, 1),
+                    "bf16_GBps": round(2 * wbytes / base / 1e3, 1)})
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="decode,prefill,elementwise,topk")
@@ -196,7 +251,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny}[name](dev)
+                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "moe": bench_moe}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

@@ -113,6 +113,10 @@ class EngineConfig:
     max_num_batched_tokens: int = 16384     # per-step token budget (chunked prefill)
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
+    # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
+    # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
+    # extra launch + partials only pay at very high sharing (profiles/r1_decode_cascade.jsonl)
+    enable_cascade_attention: bool = False
     use_cuda_graph: bool = True             # hipGraph capture of decode steps
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256)
     seed: int = 0
@@ -132,6 +136,7 @@ class EngineConfig:
             max_num_batched_tokens=_env_int("PENNY_MAX_BATCHED_TOKENS", cls.max_num_batched_tokens),
             max_model_len=_env_int("PENNY_MAX_MODEL_LEN", cls.max_model_len),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
+            enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),
         )

@@ -44,18 +44,40 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 // ------------------------------------------------------------------------------------------
 // Prefill
 // ------------------------------------------------------------------------------------------
+// Shared-prefix ("cascade") decode: the decode queries of every sequence in a prefix group are
+// the rows of one prefill-style tile against the group's shared KV blocks, so each shared block
+// is staged ONCE per 32 sequences instead of streamed once per sequence.  Output is flash-decoding
+// partial state (m, l, unnormalised O) in extra partition slots that decode_reduce merges with the
+// per-sequence suffix partitions.
+struct CascadeArgs {
+  const int* members;  // [*]  batch row of each group member (groups contiguous, bounds in cu_q)
+  const int* work;     // [nwork, 3] (group, member tile, kv chunk)
+  const int* nwork;    // device scalar
+  float* part_m;
+  float* part_l;
+  float* part_o;
+  int part_stride;     // partition slots per (row, head)
+  int slot0;           // first cascade slot (= number of suffix partitions)
+  int chunk_blocks;    // KV blocks per chunk (one work item)
+};
+
 template <int D>
-__global__ void __launch_bounds__(256, 2) prefill_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+constexpr int prefill_smem_bytes() { return 4 * KV_BS * D * 2; }
+
+// One 128-row (token*G + head) tile of sequence/group `s`, kv head `h`, against KV blocks [jb, je).
+template <int D, bool CASCADE>
+__device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__ q, const int* __restrict__ cu_q,
+                                            const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
+                                            const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+                                            bf16* __restrict__ out, float scale_log2, int Hq, int Hkv,
+                                            int max_blocks, int causal_arg, int s, int h, int tile, int chunk,
+                                            const CascadeArgs& ca) {
   constexpr int KC = D / 32;                 // k-chunks of the QK^T product
   constexpr int DT = D / 16;                 // 16-row dim tiles of O^T
   constexpr int TILE = KV_BS * D * 2;        // bytes of one K (or V) block tile
   constexpr int PIECES = TILE / 1024 / 4;    // 1-KiB glds pieces per wave per tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K|V]
+  const bool causal = !CASCADE && causal_arg;
 
-  const int s = blockIdx.z, h = blockIdx.y, tile = blockIdx.x;
   const int G = Hq / Hkv;
   const int TQ = 128 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
@@ -73,7 +95,8 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
     head[ct] = h * G + r % G;
     const bool valid = tok[ct] < qlen;
     qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
-    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
+    const int qi = q0 + (valid ? tok[ct] : 0);
+    const bf16* qrow = q + ((long)(CASCADE ? ca.members[qi] : qi) * Hq + head[ct]) * D;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
       qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
@@ -82,6 +105,9 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
   const int last_tok = min(tok0 + TQ, qlen) - 1;
   const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
   const int nblk = (kv_end + KV_BS - 1) / KV_BS;
+  const int jb = CASCADE ? chunk * ca.chunk_blocks : 0;
+  const int je = CASCADE ? min(jb + ca.chunk_blocks, nblk) : nblk;
+  if (jb >= je && CASCADE) return;
   const int* bt = block_tables + (long)s * max_blocks;
 
   f32x4 o[2][DT];
@@ -111,12 +137,12 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
     }
   };
 
-  if (nblk > 0) stage(0, 0);
+  if (je > jb) stage(jb, 0);
   __syncthreads();
 
-  for (int j = 0; j < nblk; ++j) {
-    const int buf = j & 1;
-    if (j + 1 < nblk) stage(j + 1, buf ^ 1);
+  for (int j = jb; j < je; ++j) {
+    const int buf = (j - jb) & 1;
+    if (j + 1 < je) stage(j + 1, buf ^ 1);
     const uint4* kl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE + TILE);
 
@@ -137,7 +163,7 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
 
     // ---- online softmax (base-2) -------------------------------------------------------
     Frag pf[2][2];
-    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0);
+    const bool full = CASCADE || ((j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0));
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       float mt = -INFINITY;
@@ -202,6 +228,17 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
     if (tok[ct] >= qlen) continue;
+    if constexpr (CASCADE) {
+      const long pi = ((long)ca.members[q0 + tok[ct]] * Hq + head[ct]) * ca.part_stride + ca.slot0 + chunk;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        *reinterpret_cast<f32x4*>(ca.part_o + pi * D + 16 * dt + 4 * g) = o[ct][dt];
+      if (g == 0) {
+        ca.part_m[pi] = m[ct];
+        ca.part_l[pi] = lt;
+      }
+      continue;
+    }
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
 #pragma unroll
@@ -214,15 +251,40 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
   }
 }
 
+template <int D>
+__global__ void __launch_bounds__(256, 2) prefill_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[prefill_smem_bytes<D>()];  // [buf][K|V]
+  attend_tile<D, false>(smem, q, cu_q, ctx_lens, block_tables, k_cache, v_cache, out, scale_log2, Hq, Hkv,
+                        max_blocks, causal, blockIdx.z, blockIdx.y, blockIdx.x, 0, CascadeArgs{});
+}
+
+// grid (W, Hkv): a fixed-size grid (hipGraph-capturable) strides over the device-side work list
+template <int D>
+__global__ void __launch_bounds__(256, 2) cascade_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_g, const int* __restrict__ g_ctx,
+    const int* __restrict__ g_bt, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    float scale_log2, int Hq, int Hkv, int g_max_blocks, CascadeArgs ca) {
+  __shared__ __attribute__((aligned(16))) char smem[prefill_smem_bytes<D>()];
+  const int n = *ca.nwork;
+  for (int wi = blockIdx.x; wi < n; wi += gridDim.x) {
+    const int g = ca.work[3 * wi], tile = ca.work[3 * wi + 1], chunk = ca.work[3 * wi + 2];
+    attend_tile<D, true>(smem, q, cu_g, g_ctx, g_bt, k_cache, v_cache, nullptr, scale_log2, Hq, Hkv, g_max_blocks,
+                         0, g, blockIdx.y, tile, chunk, ca);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------------------------
 template <int D>
 __global__ void __launch_bounds__(256) decode_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
-    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
-    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, float scale_log2, int Hq,
-    int Hkv, int max_blocks, int pb, int nparts) {
+    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o,
+    float scale_log2, int Hq, int Hkv, int max_blocks, int pb, int nparts, int part_stride) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ float s_m[4][16], s_l[4][16];
   __shared__ float s_o[4][16][D + 4];
@@ -230,7 +292,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
   const int b = blockIdx.x, p = blockIdx.y, h = blockIdx.z;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
-  const int blk0 = p * pb;
+  const int blk0 = (kv_start ? kv_start[b] : 0) + p * pb;  // cascade: shared blocks are done elsewhere
   if (blk0 >= nblk) return;
   const int blk1 = min(blk0 + pb, nblk);
   const int G = Hq / Hkv;
@@ -331,10 +393,10 @@ __global__ void __launch_bounds__(256) decode_kernel(
       O += s_o[ww][qc][d] * f;
     }
     const int hq = h * G + qc;
-    if (nparts == 1) {
+    if (nparts == 1 && !kv_start) {
       out[((long)b * Hq + hq) * D + d] = (bf16)(O / L);
     } else {
-      const long pi = ((long)b * Hq + hq) * nparts + p;
+      const long pi = ((long)b * Hq + hq) * part_stride + p;
       part_o[pi * D + d] = O;
       if (d == 0) {
         part_m[pi] = M;
@@ -345,17 +407,26 @@ __global__ void __launch_bounds__(256) decode_kernel(
 }
 
 template <int D>
-__global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const float* __restrict__ part_m,
-                                     const float* __restrict__ part_l, const float* __restrict__ part_o,
-                                     bf16* __restrict__ out, int Hq, int pb, int nparts) {
+__global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
+                                     const float* __restrict__ part_m, const float* __restrict__ part_l,
+                                     const float* __restrict__ part_o, bf16* __restrict__ out, int Hq, int pb,
+                                     int nparts, int part_stride, int chunk_blocks) {
   const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
   const int nblk = (ctx_lens[b] + KV_BS - 1) / KV_BS;
-  const int np = min(nparts, (nblk + pb - 1) / pb);
-  const long base = ((long)b * Hq + hq) * nparts;
+  const int s0 = kv_start ? kv_start[b] : 0;
+  const int np = min(nparts, (nblk - s0 + pb - 1) / pb);            // suffix partitions
+  const int nc = s0 > 0 ? (s0 + chunk_blocks - 1) / chunk_blocks : 0;  // shared-prefix chunks
+  const long base = ((long)b * Hq + hq) * part_stride;
   float M = -INFINITY;
   for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
+  for (int i = 0; i < nc; ++i) M = fmaxf(M, part_m[base + nparts + i]);
   float L = 0.f, O = 0.f;
   for (int i = 0; i < np; ++i) {
+    const float f = exp2f(part_m[base + i] - M);
+    L += part_l[base + i] * f;
+    O += part_o[(base + i) * D + d] * f;
+  }
+  for (int i = nparts; i < nparts + nc; ++i) {
     const float f = exp2f(part_m[base + i] - M);
     L += part_l[base + i] * f;
     O += part_o[(base + i) * D + d] * f;
@@ -388,28 +459,37 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
 
 PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const int* block_tables, const void* k_cache,
                                      const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
-                                     int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts, float scale,
+                                     int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts,
+                                     int part_stride, float scale, const int* kv_start, const int* members,
+                                     const int* cu_g, const int* g_ctx, const int* g_bt, const int* work,
+                                     const int* nwork, int grid_work, int g_max_blocks, int chunk_blocks,
                                      hipStream_t stream) {
   if (B <= 0) return 0;
-  if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
+  const bool cascade = kv_start != nullptr;
+  if (cascade && (chunk_blocks <= 0 || grid_work <= 0 || 128 % (Hq / Hkv) ||
+                  part_stride < nparts + (g_max_blocks + chunk_blocks - 1) / chunk_blocks))
+    return (int)hipErrorInvalidValue;
   dim3 grid(B, nparts, Hkv);  // sequence fastest: shared-prefix blocks are read concurrently
   const float sl2 = scale * LOG2E;
+  const CascadeArgs ca{members, work, nwork, part_m, part_l, part_o, part_stride, nparts, chunk_blocks};
+#define DECODE_LAUNCH(DD)                                                                                         \
+  if (cascade)                                                                                                  \
+    hipLaunchKernelGGL(cascade_kernel<DD>, dim3(grid_work, Hkv), dim3(256), 0, stream, (const bf16*)q, cu_g, g_ctx,  \
+                       g_bt, (const bf16*)k_cache, (const bf16*)v_cache, sl2, Hq, Hkv, g_max_blocks, ca);         \
+  hipLaunchKernelGGL(decode_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start, block_tables, \
+                     (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,   \
+                     max_blocks, pb, nparts, part_stride);                                                        \
+  if (nparts > 1 || cascade)                                                                                    \
+    hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, ctx_lens, kv_start, part_m,     \
+                       part_l, part_o, (bf16*)out, Hq, pb, nparts, part_stride, chunk_blocks);
   if (D == 128) {
-    hipLaunchKernelGGL(decode_kernel<128>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, block_tables,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,
-                       max_blocks, pb, nparts);
-    if (nparts > 1)
-      hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, B), dim3(128), 0, stream, ctx_lens, part_m, part_l,
-                         part_o, (bf16*)out, Hq, pb, nparts);
+    DECODE_LAUNCH(128)
   } else if (D == 64) {
-    hipLaunchKernelGGL(decode_kernel<64>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, block_tables,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,
-                       max_blocks, pb, nparts);
-    if (nparts > 1)
-      hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, B), dim3(64), 0, stream, ctx_lens, part_m, part_l,
-                         part_o, (bf16*)out, Hq, pb, nparts);
+    DECODE_LAUNCH(64)
   } else {
     return (int)hipErrorInvalidValue;
   }
+#undef DECODE_LAUNCH
   PENNY_RETURN_LAUNCH();
 }

@@ -66,7 +66,8 @@ class LLMEngine:
         self.bm = make_block_manager(nblocks, KV_BS, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
-                                  use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes)
+                                  use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
+                                  cascade=cfg.enable_cascade_attention)
         self.requests: Dict[str, Sequence] = {}
         self.ps = pstate()
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
@@ -165,4 +166,5 @@ class LLMEngine:
         return {"running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
                 "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
-                "tokens": self.runner.stats["tokens"]}
+                "tokens": self.runner.stats["tokens"], "cascade_steps": self.runner.stats["cascade_steps"],
+                "cascade_rows": self.runner.stats["cascade_rows"]}

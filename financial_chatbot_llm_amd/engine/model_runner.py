@@ -20,7 +20,7 @@ import torch
 
 from .. import ops
 from ..models.common import AttentionMetadata, KVCache
-from ..ops.attention import KV_BS, DecodeWorkspace
+from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade
 from ..parallel import comm
 from ..utils.logging import get_logger
 from .scheduler import ScheduledBatch
@@ -120,7 +120,8 @@ class _DecodeGraph:
 
 class ModelRunner:
     def __init__(self, model, kv: KVCache, max_model_len: int, max_decode_batch: int = 256,
-                 use_graphs: bool = True, graph_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 32, 64, 128, 256)):
+                 use_graphs: bool = True, graph_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 32, 64, 128, 256),
+                 cascade: bool = True):
         self.model = model
         self.kv = kv
         self.device = model.device
@@ -128,6 +129,8 @@ class ModelRunner:
         self.max_blocks = (max_model_len + KV_BS - 1) // KV_BS
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
+        self.cascade = cascade and self.on_gpu and ops._native.use_native(torch.empty(0, device=self.device))
+        self.G = model.hq // model.hkv
         self.graph_sizes = tuple(sorted(s for s in graph_sizes if s <= max_decode_batch))
         self.max_decode_batch = max(self.graph_sizes) if self.graph_sizes else max_decode_batch
         cfg = model.cfg
@@ -136,7 +139,7 @@ class ModelRunner:
         self.graphs: Dict[int, _DecodeGraph] = {}
         self._static = None
         self.graph_pool = None
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0}
 
     # ------------------------------------------------------------------------------------
     # eager path
@@ -158,7 +161,19 @@ class ModelRunner:
         if si.num_decode:
             m.ctx_lens_d = self._to_dev(si.ctx_d)
             m.block_tables_d = self._to_dev(si.bt_d)
+            plan = self._plan(si)
+            if plan is not None:
+                m.cascade = CascadeInputs.from_plan(plan, self.device)
         return m
+
+    def _plan(self, si: StepInputs):
+        if not self.cascade or si.num_decode < 2:
+            return None
+        plan = plan_cascade(si.ctx_d, si.bt_d, self.G)
+        if plan is not None:
+            self.stats["cascade_steps"] += 1
+            self.stats["cascade_rows"] += len(plan.members)
+        return plan
 
     def forward_logits(self, si: StepInputs) -> torch.Tensor:
         ids = self._to_dev(si.ids)
@@ -202,25 +217,30 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------
     def _alloc_static(self) -> None:
         B, W = self.max_decode_batch, self.max_blocks
-        # ids | pos | slots | ctx | block tables live in ONE device buffer fed by ONE pinned H2D copy
-        self._dev_i32 = torch.zeros(4 * B + B * W, dtype=torch.int32, device=self.device)
+        # ids | pos | slots | ctx | block tables | cascade plan live in ONE device buffer fed by ONE
+        # pinned H2D copy
+        self._cas_off = 4 * B + B * W
+        n_cas = sum(n for _, n in CascadeInputs.section_sizes(B)) if self.cascade else 0
+        self._dev_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32, device=self.device)
         d = self._dev_i32
         self._static = {
             "ids": d[0:B], "pos": d[B:2 * B], "slots": d[2 * B:3 * B], "ctx": d[3 * B:4 * B],
-            "bt": d[4 * B:].view(B, W),
+            "bt": d[4 * B:self._cas_off].view(B, W),
+            "cascade": CascadeInputs.views(d[self._cas_off:], B) if self.cascade else None,
             "temps": torch.zeros(B, dtype=torch.float32, device=self.device),
             "seeds": torch.zeros(B, dtype=torch.int64, device=self.device),
         }
         self._static["slots"].fill_(-1)
         self._static["ctx"].fill_(1)
-        self._pinned_i32 = torch.zeros(4 * B + B * W, dtype=torch.int32).pin_memory()
+        self._pinned_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32).pin_memory()
         self._pinned_f = torch.zeros(B, dtype=torch.float32).pin_memory()
         self._pinned_l = torch.zeros(B, dtype=torch.int64).pin_memory()
 
     def _run_static(self, B: int) -> torch.Tensor:
         s = self._static
         meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
-                                 ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws)
+                                 ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
+                                 cascade=s["cascade"])
         h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
         logits = self.model.logits(h)
         return ops.sample(logits, s["temps"][:B], s["seeds"][:B])
@@ -269,6 +289,8 @@ class ModelRunner:
         bt = buf[4 * S:4 * S + S * W].reshape(S, W)
         bt[:B] = 0
         bt[:n, :si.bt_d.shape[1]] = si.bt_d
+        if self.cascade:
+            CascadeInputs.pack(self._plan(si), buf[self._cas_off:], S, n)
         self._pinned_f.numpy()[:n] = si.temps
         self._pinned_l.numpy()[:n] = si.seeds
         self._dev_i32.copy_(self._pinned_i32, non_blocking=True)

@@ -7,7 +7,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..ops.attention import KV_BS, DecodeWorkspace
+from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace
 
 
 @dataclass
@@ -25,6 +25,7 @@ class AttentionMetadata:
     ctx_lens_d: Optional[torch.Tensor] = None  # [Bd]
     block_tables_d: Optional[torch.Tensor] = None
     decode_ws: Optional[DecodeWorkspace] = None
+    cascade: Optional[CascadeInputs] = None     # shared-prefix groups of the decode rows
     causal: bool = True
 
 

@@ -161,7 +161,7 @@ class DecoderModel:
                         causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp])
         if meta.num_decode > 0:
             ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
-                       workspace=meta.decode_ws, out=attn[tp:])
+                       workspace=meta.decode_ws, out=attn[tp:], cascade=meta.cascade)
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"))
         return comm.tp_all_reduce(out) if self.tp_size > 1 else out
 
