@@ -27,6 +27,10 @@ import time
 METRIC = "chat turns/sec + p50 TTFT, Llama-3-8B RAG agent at 1/2/4/8 MI355X"
 
 
+MODEL_LABELS = {"llama3-8b": "Llama-3-8B", "llama3.1-8b": "Llama-3.1-8B", "llama3-70b": "Llama-3-70B",
+                "mixtral-8x7b": "Mixtral-8x7B"}
+
+
 def log(msg: str) -> None:
     print(f"[bench r{os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -39,6 +43,8 @@ def parse(argv=None):
     ap.add_argument("--convs", type=int, default=128, help="concurrent conversations per GPU")
     ap.add_argument("--respond-tokens", type=int, default=128)
     ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: Mixtral experts as e4m3 on the fp8 MFMA path (attention/dense stay bf16)")
     ap.add_argument("--embed-model", default="bge-base-en")
     ap.add_argument("--corpus", type=int, default=1_000_000)
     ap.add_argument("--users", type=int, default=10_000)
@@ -70,7 +76,7 @@ async def run(args, ps):
     sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
                         max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
-                        graph_batch_sizes=sizes, seed=0, device="cuda")
+                        graph_batch_sizes=sizes, seed=0, device="cuda", dtype=args.dtype)
     engine = AsyncEngine(ecfg)
     log(f"engine ready in {time.perf_counter() - t0:.1f}s")
     llm = EngineLLM(engine, max_model_len=args.max_model_len, decide_script=decide_script,
@@ -130,9 +136,10 @@ def main(argv=None) -> int:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "turns/s", "n_gpus": ps.world_size,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / max(args.steps, 1), 1),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.dtype == "bf16" else "bf16 (fp8 e4m3 MoE experts)",
             "data": "synthetic conversations + 1M-vector synthetic corpus; random-init weights of the real architectures",
-            "config": {"model": "Llama-3-8B", "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
+            "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},

@@ -24,6 +24,11 @@ logger = get_logger(__name__)
 _rid = itertools.count()
 
 
+def _deliver(items) -> None:
+    for q, o in items:
+        q.put_nowait(o)
+
+
 class AsyncEngine:
     def __init__(self, cfg: Optional[EngineConfig] = None, engine: Optional[LLMEngine] = None, start: bool = True,
                  warmup: bool = True):
@@ -77,11 +82,24 @@ class AsyncEngine:
                     self._emit(rid, e)
                     eng.abort(rid)
                 continue
-            for o in outs:
-                self._emit(o.request_id, o)
+            self._emit_batch(outs)
         eng.stop_followers()
 
-    def _emit(self, rid: str, item) -> None:
+    def _emit_batch(self, outs) -> None:
+        """One thread-safe wakeup per event loop per step (not per token): with hundreds of
+        streams, per-item call_soon_threadsafe self-pipe writes cost ~1 ms/step and GIL churn."""
+        by_loop: Dict = {}
+        for o in outs:
+            sink = self._sinks.get(o.request_id)
+            if sink is not None:
+                by_loop.setdefault(sink[0], []).append((sink[1], o))
+        for loop, items in by_loop.items():
+            try:
+                loop.call_soon_threadsafe(_deliver, items)
+            except RuntimeError:  # loop closed
+                pass
+
+    def _emit(self, rid: str, item) -> None:  # single item (errors, aborts)
         sink = self._sinks.get(rid)
         if sink is None:
             return

@@ -69,6 +69,7 @@ class LLMEngine:
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)
         self.requests: Dict[str, Sequence] = {}
+        self.timing = {"prepare_s": 0.0, "execute_s": 0.0, "post_s": 0.0}   # host-side step anatomy
         self.ps = pstate()
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
                     f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
@@ -99,14 +100,19 @@ class LLMEngine:
             self.runner.capture_graphs()
 
     def step(self) -> List[StepOutput]:
+        t0 = time.perf_counter()
         batch = self.scheduler.schedule()
         if batch.empty():
             return []
         si = build_step_inputs(batch)
         if self.ps.tp_size > 1:
             comm.broadcast_object(si)
+        t1 = time.perf_counter()
         sampled = self.runner.execute(si)
         now = time.perf_counter()
+        tm = self.timing
+        tm["prepare_s"] += t1 - t0
+        tm["execute_s"] += now - t1
         outs: List[StepOutput] = []
         for seq, start, n in batch.prefill:
             seq.num_computed = start + n
@@ -141,6 +147,7 @@ class LLMEngine:
         for seq, start, n in batch.prefill:
             if start + n < seq.num_tokens:
                 self.bm.commit(seq)
+        tm["post_s"] += time.perf_counter() - now
         return outs
 
     def follower_loop(self) -> None:
@@ -166,5 +173,6 @@ class LLMEngine:
         return {"running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
                 "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
-                "tokens": self.runner.stats["tokens"], "cascade_steps": self.runner.stats["cascade_steps"],
+                "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
+                "cascade_steps": self.runner.stats["cascade_steps"],
                 "cascade_rows": self.runner.stats["cascade_rows"]}

@@ -19,6 +19,8 @@ def build_model(engine_cfg, device, seed: int = 0):
     if engine_cfg.weights:
         from .weights import load_decoder_weights
         load_decoder_weights(model, engine_cfg.weights)
+        if cfg.arch == "mixtral" and model.fp8:
+            model.quantize_experts()          # checkpoint experts (bf16) -> tiled fp8 + row scales
     else:
         model.init_random(seed=engine_cfg.seed if hasattr(engine_cfg, "seed") else seed)
     return model

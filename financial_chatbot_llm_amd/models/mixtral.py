@@ -62,10 +62,13 @@ class MixtralModel(DecoderModel):
                 self.w[k + "_t"] = moe_ops.tile_fp8_weight(q)
                 self.w[k + "_scale"] = s.float().contiguous()
         self.fp8 = True
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()   # return the bf16 experts to the pool before KV planning
 
-    def _dequant(self, p: str, key: str) -> torch.Tensor:
-        q = moe_ops.untile_fp8_weight(self.w[p + key + "_t"])
-        return moe_ops.dequant_fp8(q, self.w[p + key + "_scale"], self.dtype)
+    def _dequant(self, p: str, key: str, e: int) -> torch.Tensor:
+        """One expert's fp8 tiles -> [rows, cols] in the compute dtype (prefill path)."""
+        q = moe_ops.untile_fp8_weight(self.w[p + key + "_t"][e:e + 1])[0]
+        return moe_ops.dequant_fp8(q, self.w[p + key + "_scale"][e], self.dtype)
 
     def _moe_workspace(self, T: int):
         c = self.cfg
@@ -90,15 +93,13 @@ class MixtralModel(DecoderModel):
         offs = offsets.tolist()
         xs = h.index_select(0, tok_idx)
         ys = torch.zeros_like(xs)
-        w13_all = self._dequant(p, "w13") if self.fp8 else None
-        w2_all = self._dequant(p, "w2") if self.fp8 else None
         for e in range(c.num_experts):
             a, b = offs[e], offs[e + 1]
             if b <= a:
                 continue
             if self.fp8:
-                act = ops.silu_mul(F.linear(xs[a:b], w13_all[e]), interleave16=True)
-                ys[a:b] = F.linear(act, w2_all[e])
+                act = ops.silu_mul(F.linear(xs[a:b], self._dequant(p, "w13", e)), interleave16=True)
+                ys[a:b] = F.linear(act, self._dequant(p, "w2", e))
             else:
                 ys[a:b] = F.linear(ops.silu_mul(F.linear(xs[a:b], self.w[p + "w13"][e])), self.w[p + "w2"][e])
         out = torch.zeros_like(h)

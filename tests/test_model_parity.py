@@ -14,7 +14,7 @@ transformers = pytest.importorskip("transformers")
 from financial_chatbot_llm_amd.config import EngineConfig
 from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
 from financial_chatbot_llm_amd.models.common import AttentionMetadata, KVCache
-from financial_chatbot_llm_amd.models.configs import ModelConfig
+from financial_chatbot_llm_amd.models.configs import ModelConfig, get_model_config
 from financial_chatbot_llm_amd.models.llama import LlamaModel
 from financial_chatbot_llm_amd.models.mixtral import MixtralModel
 from financial_chatbot_llm_amd.models.weights import hf_decoder_to_internal
@@ -121,3 +121,17 @@ def test_bert_cls_matches_hf():
         with torch.no_grad():
             ref = hf(torch.tensor([s])).last_hidden_state[0, 0]
         assert torch.allclose(got[i], torch.nn.functional.normalize(ref, dim=-1), atol=1e-4)
+
+
+def test_mixtral_fp8_expert_path_cpu():
+    """fp8 e4m3 experts (tiled + per-row scales), eager bucketed path: close to the bf16 experts."""
+    cfg = get_model_config("mixtral-tiny")
+    m = MixtralModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=3, std=0.05)
+    ids = list(range(20, 90))
+    ref = _prefill_logits(m, ids)
+    m.quantize_experts()
+    assert "layers.0.w13_t" in m.w and "layers.0.w13" not in m.w
+    got = _prefill_logits(m, ids)
+    # random tiny model: many near-tied logits, so bound the mean error (~3 %) and a loose argmax agreement
+    assert (got - ref).abs().mean() < 0.05 * ref.abs().mean()
+    assert (got.argmax(-1) == ref.argmax(-1)).float().mean() > 0.7
