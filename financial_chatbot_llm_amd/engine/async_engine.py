@@ -44,9 +44,15 @@ class AsyncEngine:
         self._stop = False
         self.error: Optional[BaseException] = None
         self.step_times: List[float] = []
+        self._step_started: Optional[float] = None   # perf_counter of the in-flight step
+        self.stalled = False
+        self.step_timeout_s = float(getattr(self.engine.cfg, "step_timeout_s", 0) or 0)
         self._thread = threading.Thread(target=self._loop, name="penny-engine", daemon=True)
+        self._watchdog = threading.Thread(target=self._watch, name="penny-watchdog", daemon=True)
         if start:
             self._thread.start()
+            if self.step_timeout_s > 0:
+                self._watchdog.start()
 
     # -- engine thread ---------------------------------------------------------------------
     def _loop(self) -> None:
@@ -71,11 +77,15 @@ class AsyncEngine:
                 continue
             try:
                 t0 = time.perf_counter()
+                self._step_started = t0
                 outs = eng.step()
+                self._step_started = None
+                self.stalled = False
                 self.step_times.append(time.perf_counter() - t0)
                 if len(self.step_times) > 4096:
                     del self.step_times[:2048]
             except BaseException as e:  # noqa: BLE001 - surface GPU errors to every waiter
+                self._step_started = None
                 logger.exception("engine step failed")
                 self.error = e
                 for rid in list(self._sinks):
@@ -84,6 +94,25 @@ class AsyncEngine:
                 continue
             self._emit_batch(outs)
         eng.stop_followers()
+
+    def _watch(self) -> None:
+        """GPU-step watchdog: a step running past ``step_timeout_s`` (a wedged kernel,
+        a dead TP peer inside a collective) fails every waiting request with TimeoutError so the
+        serving layer emits its error/timeout events instead of hanging, and flags the engine
+        unhealthy (``/health`` reports it).  A kernel cannot be cancelled from the host, so the
+        requests are failed, not the step; the flag clears if the step ever completes."""
+        period = min(1.0, self.step_timeout_s / 4)
+        while not self._stop:
+            time.sleep(period)
+            t0 = self._step_started
+            if t0 is None or self.stalled or time.perf_counter() - t0 < self.step_timeout_s:
+                continue
+            self.stalled = True
+            err = TimeoutError(f"engine step exceeded {self.step_timeout_s:.1f}s")
+            logger.error(f"watchdog: {err}; failing {len(self._sinks)} waiting request(s)")
+            METRICS.inc("engine_step_timeouts")
+            for rid in list(self._sinks):
+                self._emit(rid, err)
 
     def _emit_batch(self, outs) -> None:
         """One thread-safe wakeup per event loop per step (not per token): with hundreds of
@@ -147,6 +176,7 @@ class AsyncEngine:
         if self.step_times:
             st = sorted(self.step_times[-512:])
             s["step_p50_ms"] = 1e3 * st[len(st) // 2]
+        s["stalled"] = float(self.stalled)
         return s
 
     def shutdown(self) -> None:

@@ -45,6 +45,7 @@ class Scheduler:
         self.max_model_len = max_model_len
         self.waiting: Deque[Sequence] = deque()
         self.running: List[Sequence] = []
+        self.num_preemptions = 0
 
     def add(self, seq: Sequence) -> None:
         if seq.num_tokens >= self.max_model_len:
@@ -70,6 +71,7 @@ class Scheduler:
         seq.num_computed = 0
         seq.status = SeqStatus.WAITING
         seq.num_preemptions += 1
+        self.num_preemptions += 1
         self.waiting.appendleft(seq)
         batch.preempted.append(seq)
 

@@ -22,7 +22,7 @@ from dataclasses import dataclass
 from typing import Any, Optional
 
 from fastapi import FastAPI
-from fastapi.responses import PlainTextResponse, StreamingResponse
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel
 
 from .. import config
@@ -85,6 +85,10 @@ def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
 
     @app.get("/health")
     async def health_check():
+        # reference body when healthy; 503 once the engine watchdog saw a wedged GPU step, so the
+        # container HEALTHCHECK / orchestrator restarts the replica
+        if getattr(services.engine, "stalled", False):
+            return JSONResponse({"status": "unhealthy", "reason": "engine step stalled"}, status_code=503)
         return {"status": "healthy"}
 
     @app.get("/metrics", response_class=PlainTextResponse)

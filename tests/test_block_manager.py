@@ -86,6 +86,7 @@ def test_native_matches_python_on_random_workload():
             py.free(s1)
             nat.free(s2)
         assert py.num_free() == nat.num_free()
+        assert nat.core.check_invariants() == ""
     assert py.hits == nat.hits and py.queries == nat.queries
 
 
