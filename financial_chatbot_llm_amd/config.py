@@ -103,6 +103,7 @@ class EngineConfig:
 
     model: str = "llama3-8b"                # registry key in models.configs
     dtype: str = "bf16"
+    moe_parallel: str = "tp"                # Mixtral under TP: "tp" (FFN-sharded experts) | "ep" (all-to-all)
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
@@ -137,6 +138,7 @@ class EngineConfig:
             max_model_len=_env_int("PENNY_MAX_MODEL_LEN", cls.max_model_len),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
+            moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),
         )

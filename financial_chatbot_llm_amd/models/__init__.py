@@ -11,7 +11,8 @@ def build_model(engine_cfg, device, seed: int = 0):
     from .mixtral import MixtralModel
     cfg = get_model_config(engine_cfg.model)
     if cfg.arch == "mixtral":
-        model = MixtralModel(cfg, device=device, fp8=getattr(engine_cfg, "dtype", "bf16") == "fp8")
+        model = MixtralModel(cfg, device=device, fp8=getattr(engine_cfg, "dtype", "bf16") == "fp8",
+                             moe_parallel=getattr(engine_cfg, "moe_parallel", "tp"))
     elif cfg.arch == "llama":
         model = LlamaModel(cfg, device=device)
     else:

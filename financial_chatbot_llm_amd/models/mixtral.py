@@ -16,8 +16,11 @@ Execution forms:
 * otherwise (prefill, CPU, bf16 experts): tokens are bucketed by expert (``ops.moe.route``) and
   each expert runs one GEMM pair over its bucket (hipBLASLt; fp8 experts dequantised per layer).
 
-TP shards every expert's intermediate dimension (column-parallel W1|W3, row-parallel W2); the
-partial sums are all-reduced like the dense MLP (C1).
+Under TP the experts are parallelised one of two ways (``moe_parallel``):
+* ``"tp"`` (default, hipGraph decode path): every expert's intermediate dimension is sharded
+  (column-parallel W1|W3, row-parallel W2) and the partial sums are all-reduced (C1);
+* ``"ep"``: whole experts are partitioned over the TP group and routed rows travel by
+  all-to-all dispatch/combine (C3, ``parallel/ep.py``).
 """
 from __future__ import annotations
 
@@ -30,14 +33,26 @@ from .. import ops
 from ..ops import moe as moe_ops
 from ..ops.gemm import linear
 from ..parallel import comm
+from ..parallel.dist import state as pstate
+from ..parallel.ep import ep_moe, expert_range
 from .llama import DecoderModel
 
 
 class MixtralModel(DecoderModel):
-    def __init__(self, *a, fp8: bool = False, **kw):
+    def __init__(self, *a, fp8: bool = False, moe_parallel: str = "tp", **kw):
         super().__init__(*a, **kw)
+        if moe_parallel not in ("tp", "ep"):
+            raise ValueError(f"moe_parallel must be 'tp' or 'ep', got {moe_parallel!r}")
         self.fp8 = fp8
+        self.ep = moe_parallel == "ep" and self.tp_size > 1
+        if self.ep:
+            self.expert_lo, self.expert_hi = expert_range(self.cfg.num_experts, self.tp_rank, self.tp_size)
         self._moe_ws = None
+
+    def shard(self, name: str, full: torch.Tensor) -> torch.Tensor:
+        if self.ep and name.rsplit(".", 1)[-1] in ("w13", "w2"):
+            return full[self.expert_lo:self.expert_hi].contiguous()   # whole local experts
+        return super().shard(name, full)
 
     def mlp_shapes(self, p: str) -> Dict[str, tuple]:
         c = self.cfg
@@ -78,11 +93,21 @@ class MixtralModel(DecoderModel):
                                                 f_local, self.device)
         return self._moe_ws
 
+    def _expert(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
+        """One (local) expert on its routed rows (eager path)."""
+        if self.fp8:
+            act = ops.silu_mul(F.linear(rows, self._dequant(p, "w13", e)), interleave16=True)
+            return F.linear(act, self._dequant(p, "w2", e))
+        return F.linear(ops.silu_mul(F.linear(rows, self.w[p + "w13"][e])), self.w[p + "w2"][e])
+
     def mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
         p = f"layers.{i}."
         c = self.cfg
         T = h.shape[0]
         logits = linear(h, self.w[p + "router"])
+        if self.ep:
+            return ep_moe(h, logits, c.top_k_experts, c.num_experts, lambda rows, e: self._expert(p, rows, e),
+                          group=pstate().tp_group)
         if self.fp8 and ops._native.use_native(h) and T * c.top_k_experts <= 4096:
             out = moe_ops.moe_decode_fp8(h.contiguous(), logits.contiguous(), self.w[p + "w13_t"],
                                          self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
@@ -95,13 +120,8 @@ class MixtralModel(DecoderModel):
         ys = torch.zeros_like(xs)
         for e in range(c.num_experts):
             a, b = offs[e], offs[e + 1]
-            if b <= a:
-                continue
-            if self.fp8:
-                act = ops.silu_mul(F.linear(xs[a:b], self._dequant(p, "w13", e)), interleave16=True)
-                ys[a:b] = F.linear(act, self._dequant(p, "w2", e))
-            else:
-                ys[a:b] = F.linear(ops.silu_mul(F.linear(xs[a:b], self.w[p + "w13"][e])), self.w[p + "w2"][e])
+            if b > a:
+                ys[a:b] = self._expert(p, xs[a:b], e)
         out = torch.zeros_like(h)
         out.index_add_(0, tok_idx, (ys.float() * tok_w[:, None]).to(h.dtype))
         return comm.tp_all_reduce(out) if self.tp_size > 1 else out
