@@ -1,0 +1,127 @@
+// C1 (custom path): one-shot all-reduce over xGMI peer-to-peer for decode-size TP messages.
+//
+// RCCL's ring all-reduce moves a message through n-1 sequential hops, each bound by ONE xGMI link
+// (~153 GB/s) and each paying a hop latency; a decode step's all-reduce is only a few hundred KB,
+// so it is latency-bound.  One-shot instead: every rank copies its input into its own registered
+// (IPC-shared) buffer, raises a flag in every peer's signal area, waits for all peers' flags, then
+// reads the n buffers CONCURRENTLY over its n-1 direct links and sums them locally.  One
+// publish/wait round trip, all 7 links busy at once.
+//
+// Protocol per launch ("round" r = *counter + 1, bumped by ar_bump_kernel after the launch, so a
+// hipGraph replay advances it on the device without host involvement):
+//   * data buffers are double-buffered by round parity: round r+1 writes the other half, and a
+//     rank can only reach round r+2 (same half again) after every peer has signalled r+1, i.e.
+//     after every peer finished READING round r;
+//   * flags are monotone round numbers (no reset), one slot per (source rank, block), so each
+//     block synchronises only its own chunk;
+//   * writer: all threads drain their stores with a system-scope fence, barrier, then one lane
+//     per peer stores the flag with system-scope release; reader: one lane per peer polls with
+//     system-scope acquire, barrier, system-scope acquire fence, then reads;
+//   * buffers are allocated uncached (hipDeviceMallocUncached): remote reads never hit a stale
+//     L2 line of an earlier round;
+//   * every wait is bounded (wall clock, 5 s): a missing peer sets *err and the kernel exits, so
+//     a dead rank can never wedge the GPU -- the host raises on the error flag.
+#include <string.h>
+
+#include "common.h"
+
+#define AR_MAX_RANKS 8
+#define AR_MAX_BLOCKS 64
+#define AR_TIMEOUT_TICKS (5ull * 100000000ull)  // wall_clock64() runs at 100 MHz
+
+struct ArPeers {
+  bf16* data[AR_MAX_RANKS];  // each rank's registered data buffer (2 halves of half_elems)
+  int* sig[AR_MAX_RANKS];    // each rank's signal area: [AR_MAX_RANKS source][AR_MAX_BLOCKS]
+};
+
+__global__ void __launch_bounds__(256) ar_oneshot_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                         long n, ArPeers peers, const int* __restrict__ counter,
+                                                         int* __restrict__ err, int rank, int nranks,
+                                                         long half_elems) {
+  const int round = *counter + 1;
+  const long off = (round & 1) * half_elems;
+  const long per = ((n + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
+  const long lo = blockIdx.x * per, hi = min(n, lo + per);
+
+  bf16* mine = peers.data[rank] + off;
+  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+    *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
+  __threadfence_system();  // every thread's stores complete (system scope) before the flag
+  __syncthreads();
+  if (threadIdx.x < nranks)
+    __hip_atomic_store(peers.sig[threadIdx.x] + rank * AR_MAX_BLOCKS + blockIdx.x, round, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x < nranks) {
+    const int* slot = peers.sig[rank] + threadIdx.x * AR_MAX_BLOCKS + blockIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
+      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+
+  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < nranks; ++q) {
+      // fixed rank order on every rank -> bit-identical results across the group
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(peers.data[q] + off + i), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    *reinterpret_cast<uint4*>(out + i) = pack8(acc);
+  }
+}
+
+__global__ void ar_bump_kernel(int* counter) { *counter += 1; }
+
+PENNY_API int penny_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Uncached device allocation + its IPC handle (written to `handle`, penny_ar_handle_size() bytes).
+PENNY_API int penny_ar_alloc(size_t bytes, void** out_ptr, void* handle) {
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  memcpy(handle, &h, sizeof(h));
+  *out_ptr = p;
+  return 0;
+}
+
+PENNY_API int penny_ar_open(const void* handle, void** out_ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out_ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+PENNY_API int penny_ar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+PENNY_API int penny_ar_free(void* p) { return (int)hipFree(p); }
+
+// data_ptrs / sig_ptrs: host arrays of nranks device pointers (own buffers + opened peer buffers).
+PENNY_API int penny_allreduce_oneshot(const void* in, void* out, long n, void* const* data_ptrs,
+                                      void* const* sig_ptrs, int* counter, int* err, int rank, int nranks,
+                                      long half_elems, int nblocks, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (nranks < 1 || nranks > AR_MAX_RANKS || rank < 0 || rank >= nranks || n % 8 || n > half_elems ||
+      nblocks < 1 || nblocks > AR_MAX_BLOCKS)
+    return (int)hipErrorInvalidValue;
+  ArPeers peers;
+  for (int q = 0; q < AR_MAX_RANKS; ++q) {
+    peers.data[q] = q < nranks ? (bf16*)data_ptrs[q] : nullptr;
+    peers.sig[q] = q < nranks ? (int*)sig_ptrs[q] : nullptr;
+  }
+  hipLaunchKernelGGL(ar_oneshot_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
+                     (const int*)counter, err, rank, nranks, half_elems);
+  hipLaunchKernelGGL(ar_bump_kernel, dim3(1), dim3(1), 0, stream, counter);
+  PENNY_RETURN_LAUNCH();
+}

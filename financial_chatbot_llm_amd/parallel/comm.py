@@ -26,10 +26,26 @@ def tp_size() -> int:
     return state().tp_size
 
 
+_CUSTOM_AR = None   # CustomAllReduce for the TP group (enable_custom_all_reduce)
+
+
+def enable_custom_all_reduce(max_bytes: int = 4 << 20):
+    """Route small bf16 TP all-reduces (decode) through the one-shot xGMI P2P kernel
+    (``custom_ar.py``); RCCL keeps everything else.  Call on every TP rank after init."""
+    global _CUSTOM_AR
+    s = state()
+    if s.tp_size > 1 and _CUSTOM_AR is None:
+        from .custom_ar import CustomAllReduce
+        _CUSTOM_AR = CustomAllReduce(s.tp_group, max_bytes=max_bytes)
+    return _CUSTOM_AR
+
+
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     s = state()
     if s.tp_size == 1:
         return x
+    if _CUSTOM_AR is not None and _CUSTOM_AR.eligible(x):
+        return _CUSTOM_AR.all_reduce(x, out=x)   # reads peers' staged copies, so in-place is safe
     dist.all_reduce(x, group=s.tp_group)
     return x
 
