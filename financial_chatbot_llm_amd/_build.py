@@ -117,9 +117,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--runtime-only", action="store_true", help="host runtime only (machines without hipcc)")
     args = ap.parse_args(argv)
     if args.clean:
         clean()
+    if args.runtime_only:
+        print(f"built {build_runtime(verbose=True)}")
+        return 0
     build_all(jobs=args.j, verbose=True)
     print(f"built {KERNEL_LIB}")
     return 0
