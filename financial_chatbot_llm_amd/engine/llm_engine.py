@@ -58,6 +58,9 @@ class LLMEngine:
         self.device = device
         t0 = time.perf_counter()
         self.model = model if model is not None else build_model(cfg, device)
+        if device.type == "cuda":
+            from ..ops.gemm import load_gemm_tuning
+            self.gemm_tuning = load_gemm_tuning(cfg.model, cfg.tp_size)
         self.tokenizer = tokenizer or load_tokenizer(cfg.tokenizer, self.model.cfg.vocab_size)
         self.eos_ids = set(self.tokenizer.eos_ids)
         nblocks = plan_kv_blocks(cfg, self.model, device)
@@ -174,5 +177,6 @@ class LLMEngine:
                 "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
+                "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),
                 "cascade_steps": self.runner.stats["cascade_steps"],
                 "cascade_rows": self.runner.stats["cascade_rows"]}

@@ -89,3 +89,35 @@ def interleave16(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     """[F, H] gate and up -> [2F, H] with rows alternating in 16-row groups (skinny SiLU layout)."""
     Fr, H = gate.shape
     return torch.stack([gate.view(Fr // 16, 16, H), up.view(Fr // 16, 16, H)], dim=1).reshape(2 * Fr, H)
+
+
+# ----------------------------------------------------------------------------------------------
+# Curated hipBLASLt/rocBLAS solution table for the decode buckets (bench/tune_gemm.py)
+# ----------------------------------------------------------------------------------------------
+TUNING_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
+_LOADED_TUNING: Optional[str] = None
+
+
+def tuning_file(model: str, tp: int = 1) -> str:
+    suffix = "" if tp == 1 else f"_tp{tp}"
+    return os.path.join(TUNING_DIR, f"gemm_{model}{suffix}_mi355x.csv")
+
+
+def load_gemm_tuning(model: str, tp: int = 1) -> Optional[str]:
+    """Enable PyTorch TunableOp READ-ONLY with the curated per-shape solutions for ``model``
+    (shapes not in the table, e.g. prefill M, keep the default heuristic).  Never tunes online,
+    so hipGraph capture and serving latency are unaffected.  Returns the file used, if any."""
+    global _LOADED_TUNING
+    path = tuning_file(model, tp)
+    if os.environ.get("PENNY_GEMM_TUNING", "1") != "1" or not os.path.exists(path) or not torch.cuda.is_available():
+        return None
+    if _LOADED_TUNING == path:
+        return path
+    tun = torch.cuda.tunable
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    if not tun.read_file(path):
+        return None
+    tun.enable(True)
+    _LOADED_TUNING = path
+    return path
