@@ -105,9 +105,10 @@ async def run(args, ps):
     await consumer
     stats = engine.stats()
     engine.shutdown()
+    stages = {k: [v for r in results for v in r.stages.get(k, [])] for k in ("decide", "retrieval", "respond_first_token")}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
             "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
-            "engine": stats}
+            "stages": stages, "engine": stats}
 
 
 def main(argv=None) -> int:
@@ -147,6 +148,8 @@ def main(argv=None) -> int:
             "p99_ttft_ms": None if p99 is None else round(p99, 1),
             "turn_errors": sum(r["errors"] for r in allr),
             "retrieval_turns": sum(r["retrievals"] for r in allr),
+            "ttft_p50_breakdown_ms": {k: round(1e3 * statistics.median(v), 1) if v else None
+                                      for k, v in allr[0]["stages"].items()},
             "engine_rank0": allr[0]["engine"],
         }
         line = json.dumps(out)

@@ -71,6 +71,7 @@ class WaveResult:
     turns: int
     errors: int
     retrievals: int
+    stages: Dict[str, List[float]] = field(default_factory=dict)   # TTFT anatomy per turn (s)
 
 
 class RagWorkload:
@@ -115,7 +116,22 @@ class RagWorkload:
         dt = time.perf_counter() - t0
         traces = self.worker.traces[n0:target]
         return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
-                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces))
+                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces), ttft_stages(traces))
+
+
+def ttft_stages(traces) -> Dict[str, List[float]]:
+    """Split each turn's TTFT: receive -> decide done (context fetch + LLM call 1), decide done ->
+    respond start (retrieval, when taken), respond start -> first chunk (LLM call 2 prefill)."""
+    out: Dict[str, List[float]] = {"decide": [], "retrieval": [], "respond_first_token": []}
+    for t in traces:
+        st = t.stages
+        if "decide_done" in st:
+            out["decide"].append(st["decide_done"] - t.t_receive)
+            if "respond_start" in st:
+                out["retrieval"].append(st["respond_start"] - st["decide_done"])
+        if "respond_start" in st and t.t_first_chunk is not None:
+            out["respond_first_token"].append(t.t_first_chunk - st["respond_start"])
+    return out
 
 
 def decide_script(messages, tools) -> str:

@@ -48,6 +48,7 @@ class AsyncEngine:
         self.stalled = False
         self.step_timeout_s = float(getattr(self.engine.cfg, "step_timeout_s", 0) or 0)
         self._thread = threading.Thread(target=self._loop, name="penny-engine", daemon=True)
+        self._stop_evt = threading.Event()
         self._watchdog = threading.Thread(target=self._watch, name="penny-watchdog", daemon=True)
         if start:
             self._thread.start()
@@ -103,7 +104,8 @@ class AsyncEngine:
         requests are failed, not the step; the flag clears if the step ever completes."""
         period = min(1.0, self.step_timeout_s / 4)
         while not self._stop:
-            time.sleep(period)
+            if self._stop_evt.wait(period):
+                return
             t0 = self._step_started
             if t0 is None or self.stalled or time.perf_counter() - t0 < self.step_timeout_s:
                 continue
@@ -181,6 +183,9 @@ class AsyncEngine:
 
     def shutdown(self) -> None:
         self._stop = True
+        self._stop_evt.set()
         self._wake.set()
         if self._thread.is_alive():
             self._thread.join(timeout=30)
+        if self._watchdog.is_alive():
+            self._watchdog.join(timeout=5)

@@ -12,6 +12,7 @@ math on the same bf16 inputs) and the CPU path used by the CI tests.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from functools import lru_cache
 from typing import Optional
@@ -186,6 +187,17 @@ class DecodeWorkspace:
     nparts: int
     part_stride: int = 0    # partition slots per (row, head): nparts suffix + cascade chunk slots
 
+    def partitioning(self, B: int):
+        """(pb, nparts) for a decode batch of B rows.  Large batches already fill the chip with
+        (row, head) work, so they take longer partitions: fewer empty workgroups in the fixed
+        hipGraph grid and fewer partials to merge (B=128: pb 16 is 10-16 % faster than 8;
+        profiles/r1_decode_partition.jsonl).  Small batches keep pb=8 for parallelism."""
+        if os.environ.get("PENNY_DECODE_FIXED_PB") == "1":
+            return self.pb, self.nparts
+        pb = self.pb if B < 96 else (2 * self.pb if B < 192 else 4 * self.pb)
+        nblk = self.nparts * self.pb
+        return pb, (nblk + pb - 1) // pb
+
     @classmethod
     def create(cls, max_batch: int, Hq: int, D: int, max_ctx: int, device, pb: int = 8) -> "DecodeWorkspace":
         nblk = (max_ctx + KV_BS - 1) // KV_BS
@@ -358,9 +370,10 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         cas = ((N.ptr(c.kv_start), N.ptr(c.members), N.ptr(c.cu_g), N.ptr(c.g_ctx), N.ptr(c.g_bt), N.ptr(c.work),
                 N.ptr(c.nwork), c.grid, CASCADE_MAX_BLOCKS, CASCADE_CHUNK) if c is not None
                else (None, None, None, None, None, None, None, 0, 0, 0))
+        pb, nparts = ws.partitioning(B) if c is None else (ws.pb, ws.nparts)
         N.call("penny_attention_decode", N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache),
                N.ptr(v_cache), N.ptr(out), N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D,
-               block_tables.shape[1], ws.pb, ws.nparts, ws.part_stride, float(scale), *cas, N.stream())
+               block_tables.shape[1], pb, nparts, ws.part_stride, float(scale), *cas, N.stream())
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()

@@ -69,6 +69,15 @@ class ChatWorker:
                     logger.info(f"Complete message sent to Kafka for conversation {conversation_id}")
                 elif kind == "retrieval_complete":
                     trace.retrieved = int(update.get("count", 0))
+                    trace.mark("retrieval_done")
+                elif kind == "status":
+                    m = update.get("message", "")
+                    if m.startswith("Analyzing"):
+                        trace.mark("decide_start")
+                    elif m.startswith("Retrieving") or m.startswith("No transaction"):
+                        trace.mark("decide_done")
+                    elif m.startswith("Generating"):
+                        trace.mark("respond_start")
         except Exception as e:  # noqa: BLE001
             logger.error(f"Error streaming LLM response: {e}")
             trace.error = True

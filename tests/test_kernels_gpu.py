@@ -124,7 +124,10 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333])])
+@pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
+                                         # B >= 96 / >= 192: longer partitions (pb 16 / 32)
+                                         (32, 8, [(37 * i) % 3000 + 1 for i in range(100)]),
+                                         (8, 2, [(53 * i) % 4000 + 1 for i in range(200)])])
 def test_decode_attention(Hq, Hkv, ctxs):
     g = torch.Generator().manual_seed(5)
     D = 128
