@@ -51,6 +51,9 @@ def parse(argv=None):
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--arrival", default="closed", choices=["closed", "wave"],
+                    help="closed: each conversation sends its next turn when its last completes (default); "
+                         "wave: all conversations send in lock-step waves")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -85,19 +88,30 @@ async def run(args, ps):
     wl.kafka.setup_consumer()
     consumer = asyncio.create_task(wl.worker.consume_messages())
 
-    for w in range(args.warmup):
-        r = await wl.run_wave()
-        log(f"warmup wave {w}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals}")
+    # a "step" = every conversation completes one more turn (W untimed, then K timed)
+    if args.warmup:
+        if args.arrival == "closed":
+            r = await wl.run_closed_loop(args.warmup)
+        else:
+            for _ in range(args.warmup):
+                r = await wl.run_wave()
+        log(f"warmup ({args.warmup} turns/conv): {r.seconds:.2f}s turns={r.turns} errors={r.errors}")
 
     torch.cuda.synchronize()
     barrier()
     t_start = time.perf_counter()
     results = []
-    for k in range(args.steps):
-        r = await wl.run_wave()
+    if args.arrival == "closed":
+        r = await wl.run_closed_loop(args.steps)
         results.append(r)
-        log(f"wave {k}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals} "
-            f"ttft_p50={1e3 * statistics.median(r.ttfts) if r.ttfts else float('nan'):.0f}ms")
+        log(f"{args.steps} turns/conv closed-loop: {r.seconds:.2f}s turns={r.turns} errors={r.errors} "
+            f"retrievals={r.retrievals} ttft_p50={1e3 * statistics.median(r.ttfts) if r.ttfts else float('nan'):.0f}ms")
+    else:
+        for k in range(args.steps):
+            r = await wl.run_wave()
+            results.append(r)
+            log(f"wave {k}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals} "
+                f"ttft_p50={1e3 * statistics.median(r.ttfts) if r.ttfts else float('nan'):.0f}ms")
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -142,6 +156,7 @@ def main(argv=None) -> int:
             "data": "synthetic conversations + 1M-vector synthetic corpus; random-init weights of the real architectures",
             "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
+                       "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},
             "p50_ttft_ms": None if p50 is None else round(p50, 1),

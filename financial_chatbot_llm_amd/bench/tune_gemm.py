@@ -96,7 +96,7 @@ def main(argv=None) -> int:
                        "solution": sol, "kept": win})
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w", newline="") as fh:
-        w = csv.writer(fh)
+        w = csv.writer(fh, lineterminator="\n")     # TunableOp's reader does not strip "\r"
         for k, v in validators:
             w.writerow(["Validator", k, v])
         for row in keep:

@@ -93,18 +93,49 @@ class RagWorkload:
             self.db.put_context(doc)
             self.convs.append(doc)
         self.ts = 1_700_000_000
-        self.wave_idx = 0
+        self.turn_of = [0] * num_convs            # next turn index per conversation
+        self.conv_index = {d["conversation_id"]: i for i, d in enumerate(self.convs)}
+
+    def _send(self, i: int) -> None:
+        """Conversation i's next user message (spend / advice questions alternate per turn)."""
+        doc, k = self.convs[i], self.turn_of[i]
+        pool = SPEND_QUESTIONS if (i + k) % 2 == 0 else ADVICE_QUESTIONS
+        text = pool[(i // 2 + k) % len(pool)]
+        self.ts += 1
+        self.db.put_user_message(doc["conversation_id"], text, doc["user_id"], self.ts)
+        self.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key=doc["conversation_id"],
+                                    value=json.dumps({"message": text, "conversation_id": doc["conversation_id"],
+                                                      "user_id": doc["user_id"]}))
+        self.turn_of[i] += 1
 
     async def _send_wave(self) -> None:
-        for i, doc in enumerate(self.convs):
-            pool = SPEND_QUESTIONS if (i + self.wave_idx) % 2 == 0 else ADVICE_QUESTIONS
-            text = pool[(i // 2 + self.wave_idx) % len(pool)]
-            self.ts += 1
-            self.db.put_user_message(doc["conversation_id"], text, doc["user_id"], self.ts)
-            self.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key=doc["conversation_id"],
-                                        value=json.dumps({"message": text, "conversation_id": doc["conversation_id"],
-                                                          "user_id": doc["user_id"]}))
-        self.wave_idx += 1
+        for i in range(len(self.convs)):
+            self._send(i)
+
+    async def run_closed_loop(self, turns_per_conv: int) -> WaveResult:
+        """Closed-loop load: every conversation is an independent client that sends its next
+        message as soon as its previous turn completes (no cross-conversation lock-step, so no
+        synchronised arrival bursts and no end-of-wave tail per turn).  Returns after every
+        conversation completed ``turns_per_conv`` turns."""
+        n0 = len(self.worker.traces)
+        t0 = time.perf_counter()
+        left = [turns_per_conv - 1] * len(self.convs)
+        for i in range(len(self.convs)):
+            self._send(i)
+        seen, target = n0, n0 + turns_per_conv * len(self.convs)
+        while seen < target:
+            await asyncio.sleep(0.002)
+            new = self.worker.traces[seen:]
+            seen += len(new)
+            for tr in new:
+                i = self.conv_index[tr.conversation_id]
+                if left[i] > 0:
+                    left[i] -= 1
+                    self._send(i)
+        dt = time.perf_counter() - t0
+        traces = self.worker.traces[n0:target]
+        return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
+                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces), ttft_stages(traces))
 
     async def run_wave(self) -> WaveResult:
         n0 = len(self.worker.traces)

@@ -26,6 +26,9 @@ def test_rag_workload_cpu():
         task = asyncio.create_task(wl.worker.consume_messages())
         r1 = await wl.run_wave()
         r2 = await wl.run_wave()
+        r3 = await wl.run_closed_loop(2)          # independent per-conversation clients
+        assert r3.turns == 8 and r3.errors == 0 and wl.turn_of == [4, 4, 4, 4]
+        assert len(r3.stages["respond_first_token"]) == 8
         wl.worker.stop()
         await task
         return wl, r1, r2
@@ -38,8 +41,8 @@ def test_rag_workload_cpu():
     assert r1.retrievals == 2 and r2.retrievals == 2
     assert len(r1.ttfts) == 4
     out = wl.broker.values("ai_response")
-    assert sum(e.get("type") == "complete" for e in out) == 8
+    assert sum(e.get("type") == "complete" for e in out) == 16
     # prefix cache: wave 2 prompts extend wave 1's and share the system prompt
     assert eng.engine.bm.hits > 0
     saved = list(wl.db.messages_collection.find({"sender": "AIMessage"}))
-    assert len(saved) == 8 and all(isinstance(d["message"], str) for d in saved)
+    assert len(saved) == 16 and all(isinstance(d["message"], str) for d in saved)
