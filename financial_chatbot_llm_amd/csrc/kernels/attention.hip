@@ -37,6 +37,11 @@ union Frag {
   bf16x8 v;
 };
 
+// Raw v_exp_f32: exp2f() wraps it in a denormal-range fix-up (cmp, 2x cndmask, ldexp) -- 5 VALU
+// ops per score instead of 1.  Softmax terms below 2^-126 are irrelevant (they add to l and O
+// below f32 resolution of the running max term), so the flush is harmless.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -60,6 +65,95 @@ struct CascadeArgs {
   int slot0;           // first cascade slot (= number of suffix partitions)
   int chunk_blocks;    // KV blocks per chunk (one work item)
 };
+
+// One 64-key block for a wave's 32 query rows (2 column tiles of 16): S^T = K.Q^T on MFMA,
+// base-2 online softmax in registers, O^T += V^T.P^T with P straight from the S^T registers.
+// kl / vl: the block's K and V tiles in LDS (fragment-native).  `full`: no key of the block needs
+// masking (all < ctx and, if causal, <= every row's position).
+// MASK is a template parameter so the hot (unmasked) path is straight-line code: a per-element
+// `full || (...)` short-circuit compiles to 32 divergent branches per block on gfx950.
+template <int D, bool MASK>
+__device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
+                                             const Frag (&qf)[2][D / 32], f32x4 (&o)[2][D / 16], float (&m)[2],
+                                             float (&l)[2], bool causal, int j, int ctx,
+                                             const int (&qpos)[2], float scale_log2, int lane, int g) {
+  constexpr int KC = D / 32;
+  constexpr int DT = D / 16;
+  // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
+  f32x4 sc[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      Frag kf;
+      kf.u = kl[(t * KC + c) * 64 + lane];
+      sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
+      sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
+    }
+  }
+
+  // ---- online softmax (base-2) -------------------------------------------------------
+  Frag pf[2][2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = j * KV_BS + 16 * t + 4 * g + r;
+        float v = sc[ct][t][r] * scale_log2;
+        if constexpr (MASK) {
+          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));   // non-short-circuit: selects
+          v = ok ? v : -INFINITY;
+        }
+        sc[ct][t][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m[ct], mt);
+    const float mref = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = fast_exp2(m[ct] - mref);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = fast_exp2(sc[ct][t][r] - mref);
+        sc[ct][t][r] = p;
+        ls += p;
+      }
+    }
+    l[ct] = l[ct] * alpha + ls;
+    m[ct] = mn;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
+        pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
+      }
+    }
+  }
+
+  // ---- O^T += V^T . P^T ---------------------------------------------------------------
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      Frag vf;
+      vf.u = vl[(dt * 2 + st) * 64 + lane];
+      o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
+      o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
+    }
+  }
+}
 
 template <int D>
 constexpr int prefill_smem_bytes() { return 4 * KV_BS * D * 2; }
@@ -146,78 +240,9 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
     const uint4* kl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE + TILE);
 
-    // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
-    f32x4 sc[2][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        Frag kf;
-        kf.u = kl[(t * KC + c) * 64 + lane];
-        sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
-        sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
-      }
-    }
-
-    // ---- online softmax (base-2) -------------------------------------------------------
-    Frag pf[2][2];
     const bool full = CASCADE || ((j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0));
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      float mt = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = j * KV_BS + 16 * t + 4 * g + r;
-          const bool ok = full || (key < ctx && (!causal || key <= qpos[ct]));
-          const float v = ok ? sc[ct][t][r] * scale_log2 : -INFINITY;
-          sc[ct][t][r] = v;
-          mt = fmaxf(mt, v);
-        }
-      }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m[ct], mt);
-      const float mref = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = exp2f(m[ct] - mref);
-      float ls = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sc[ct][t][r] - mref);
-          sc[ct][t][r] = p;
-          ls += p;
-        }
-      }
-      l[ct] = l[ct] * alpha + ls;
-      m[ct] = mn;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
-          pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
-        }
-      }
-    }
-
-    // ---- O^T += V^T . P^T ---------------------------------------------------------------
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        Frag vf;
-        vf.u = vl[(dt * 2 + st) * 64 + lane];
-        o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
-        o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
-      }
-    }
+    if (full) attend_block<D, false>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
+    else attend_block<D, true>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
     __syncthreads();  // block j+1 landed (vmcnt drained) and everyone is done with buffer `buf`
   }
 
@@ -345,14 +370,14 @@ __global__ void __launch_bounds__(256) decode_kernel(
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
+    const float alpha = fast_exp2(m - mn);
     float ls = 0.f;
     Frag pf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(sc[t][r] - mn);
+        const float pv = fast_exp2(sc[t][r] - mn);
         ls += pv;
         pf[t >> 1].v[4 * (t & 1) + r] = (bf16)pv;
       }
@@ -434,6 +459,128 @@ __global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int
   if (d < D) out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 
+
+// Pipelined prefill (the production prefill path for tiles of > 128 rows).
+// One workgroup = NW waves x 32 rows = NW*32 (token*G + head) rows of one sequence and kv head:
+// every staged K/V block is shared by NW waves (half the LDS fill traffic per row of the 4-wave
+// tile) and the K/V ring is NBUF blocks deep, so block j+NBUF-1 streams in while block j is on
+// the MFMAs.  Synchronisation follows the counted-vmcnt recipe: each wave waits only for ITS
+// pieces of block j (`s_waitcnt vmcnt(LOADS)` while the next block's pieces stay in flight), one
+// raw s_barrier publishes block j to all waves and retires everyone's reads of the buffer about
+// to be refilled -- one barrier per block, never a vmcnt(0) drain in the steady state.  All LDS is
+// one __shared__ array (a second one makes hipcc drain vmcnt before every ds_read).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int D, int NW, int NBUF>
+__global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+  constexpr int KC = D / 32, DT = D / 16;
+  constexpr int TILE = KV_BS * D * 2;         // bytes of one K (or V) block tile
+  constexpr int PIECES = TILE / 1024 / NW;    // 1-KiB glds pieces per wave per tile
+  constexpr int LOADS = 2 * PIECES;           // glds per wave per staged block (K + V)
+  static_assert(PIECES >= 1 && TILE % (1024 * NW) == 0, "tile must split evenly over the waves");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][K|V]
+
+  // causal tiles grow with their index: dispatch the longest first so they do not form the tail
+  const int s = blockIdx.z, h = blockIdx.y, tile = gridDim.x - 1 - blockIdx.x;
+  const int G = Hq / Hkv;
+  const int TQ = NW * 32 / G;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  const int tok0 = tile * TQ;
+  if (tok0 >= qlen) return;
+  const int ctx = ctx_lens[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+
+  const int last_tok = min(tok0 + TQ, qlen) - 1;
+  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
+  const int nblk = (kv_end + KV_BS - 1) / KV_BS;
+  const int* bt = block_tables + (long)s * max_blocks;
+
+  auto stage = [&](int j) {
+    const long phys = bt[j];
+    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    char* kl = smem + (j % NBUF) * 2 * TILE;
+    char* vl = kl + TILE;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int piece = w * PIECES + i;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kl + piece * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vl + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+  // K/V prologue first: the Q loads below are younger, so the first counted wait covers them too
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < nblk) stage(j);
+
+  int tok[2], head[2], qpos[2];
+  Frag qf[2][KC];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int r = w * 32 + ct * 16 + col;
+    tok[ct] = tok0 + r / G;
+    head[ct] = h * G + r % G;
+    const bool valid = tok[ct] < qlen;
+    qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
+    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
+  }
+  // Retire the Q loads (and the prologue) with a wait the compiler's waitcnt pass can SEE: it
+  // then knows qf is resident and does not re-insert a vmcnt(0) at every loop iteration (an
+  // inline-asm wait is opaque to it).  vmcnt(0), expcnt/lgkmcnt untouched.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+
+  f32x4 o[2][DT];
+  float m[2], l[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    m[ct] = -INFINITY;
+    l[ct] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int j = 0; j < nblk; ++j) {
+    // my pieces of block j landed (younger blocks j+1.. may stay in flight), then publish
+    if (j + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
+    else wait_vmcnt_barrier<0>();
+    if (j + NBUF - 1 < nblk) stage(j + NBUF - 1);   // refills the buffer everyone finished at j-1
+    const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
+    const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
+    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0);
+    if (full) attend_block<D, false>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
+    else attend_block<D, true>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
+  }
+
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float lt = l[ct];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (tok[ct] >= qlen) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x4 v4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
+    }
+  }
+}
+
 PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                       const void* k_cache, const void* v_cache, void* out, int num_seqs,
                                       int max_q_len, int Hq, int Hkv, int D, int max_blocks, float scale, int causal,
@@ -442,18 +589,29 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv;
   if (G > 128 || (128 % G)) return (int)hipErrorInvalidValue;
-  const int TQ = 128 / G;
-  dim3 grid((max_q_len + TQ - 1) / TQ, Hkv, num_seqs);
   const float sl2 = scale * LOG2E;
+  // > 128 rows per (sequence, kv head): the 8-wave pipelined kernel; short chunks keep the
+  // 4-wave tile (a 256-row tile would be mostly padding)
+  const bool big = (long)max_q_len * G > 128;
+  const int TQ = (big ? 256 : 128) / G;
+  dim3 grid((max_q_len + TQ - 1) / TQ, Hkv, num_seqs);
+#define PREFILL_LAUNCH(DD)                                                                                       \
+  if (big)                                                                                                       \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens,  \
+                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \
+                       max_blocks, causal);                                                                        \
+  else                                                                                                           \
+    hipLaunchKernelGGL(prefill_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens,           \
+                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \
+                       max_blocks, causal);
   if (D == 128) {
-    hipLaunchKernelGGL(prefill_kernel<128>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens, block_tables,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);
+    PREFILL_LAUNCH(128)
   } else if (D == 64) {
-    hipLaunchKernelGGL(prefill_kernel<64>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens, block_tables,
-                       (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);
+    PREFILL_LAUNCH(64)
   } else {
     return (int)hipErrorInvalidValue;
   }
+#undef PREFILL_LAUNCH
   PENNY_RETURN_LAUNCH();
 }
 

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import asyncio
 import itertools
+import os
+import sys
 import threading
 import time
 from typing import AsyncIterator, Dict, List, Optional, Sequence as Seq, Tuple
@@ -47,6 +49,13 @@ class AsyncEngine:
         self._step_started: Optional[float] = None   # perf_counter of the in-flight step
         self.stalled = False
         self.step_timeout_s = float(getattr(self.engine.cfg, "step_timeout_s", 0) or 0)
+        # The engine thread shares the GIL with the serving event loop (hundreds of streams).
+        # CPython's default 5 ms switch interval lets a busy event loop hold the GIL for up to
+        # 5 ms while the engine thread waits to launch the next GPU step; a short interval keeps
+        # the GPU fed (PENNY_GIL_SWITCH_MS, 0 = leave the interpreter default).
+        sw = float(os.environ.get("PENNY_GIL_SWITCH_MS", "0.5"))
+        if sw > 0:
+            sys.setswitchinterval(sw / 1e3)
         self._thread = threading.Thread(target=self._loop, name="penny-engine", daemon=True)
         self._stop_evt = threading.Event()
         self._watchdog = threading.Thread(target=self._watch, name="penny-watchdog", daemon=True)
