@@ -104,7 +104,7 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = j * KV_BS + 16 * t + 4 * g + r;
-        float v = sc[ct][t][r] * scale_log2;
+        float v = sc[ct][t][r];
         if constexpr (MASK) {
           const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));   // non-short-circuit: selects
           v = ok ? v : -INFINITY;
@@ -115,23 +115,31 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
     }
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m[ct], mt);
-    const float mref = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = fast_exp2(m[ct] - mref);
+    mt *= scale_log2;   // max of the scaled scores (scale > 0) -- the 32 scores stay unscaled
+    // Deferred rescale: the running max m only moves when a block raises it by more than 8
+    // (log2 domain), so p <= 2^8 in between -- harmless for f32 l/O and bf16 P -- and the 64
+    // multiplies of O (plus l) run on the rare blocks that need them, behind a wave-uniform branch.
+    const bool grow = mt > m[ct] + 8.f;
+    if (__any(grow)) {
+      const float mn = grow ? mt : m[ct];
+      const float alpha = grow ? fast_exp2(m[ct] - mn) : 1.f;
+      l[ct] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+      m[ct] = mn;
+    }
+    const float mref = (m[ct] == -INFINITY) ? 0.f : m[ct];
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = fast_exp2(sc[ct][t][r] - mref);
+        const float p = fast_exp2(fmaf(sc[ct][t][r], scale_log2, -mref));
         sc[ct][t][r] = p;
         ls += p;
       }
     }
-    l[ct] = l[ct] * alpha + ls;
-    m[ct] = mn;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+    l[ct] += ls;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
 #pragma unroll

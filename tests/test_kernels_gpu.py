@@ -104,18 +104,21 @@ def test_rope_kv_write(Hq, Hkv, D):
     close(vcd, vc, atol=0)
 
 
-@pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
-    (32, 8, 128, True, [(130, 130), (1, 77), (64, 200), (300, 300)]),   # (q_len, ctx_len): prefix hits
-    (8, 1, 128, True, [(100, 100), (17, 600)]),                          # GQA 8 (70B TP=8 shard)
-    (12, 12, 64, False, [(9, 9), (64, 64), (200, 200)]),                 # BERT: bidirectional, D=64
+@pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
+    (32, 8, 128, True, [(130, 130), (1, 77), (64, 200), (300, 300)], 1.0),   # (q_len, ctx_len): prefix hits
+    (8, 1, 128, True, [(100, 100), (17, 600)], 1.0),                          # GQA 8 (70B TP=8 shard)
+    (12, 12, 64, False, [(9, 9), (64, 64), (200, 200)], 1.0),                 # BERT: bidirectional, D=64
+    # peaky scores (std ~12 in log2 units): exercises the deferred-max rescale path
+    (32, 8, 128, True, [(700, 900), (33, 33)], 12.0),
+    (32, 8, 128, False, [(257, 257)], 12.0),
 ])
-def test_prefill_attention(Hq, Hkv, D, causal, lens):
+def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     g = torch.Generator().manual_seed(4)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
     tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
     cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
-    q = rnd(int(cu[-1]), Hq, D, gen=g)
+    q = rnd(int(cu[-1]), Hq, D, scale=qscale, gen=g)
     ctx_t = torch.tensor(ctx, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
     out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, causal,
