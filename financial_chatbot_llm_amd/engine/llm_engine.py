@@ -22,7 +22,7 @@ from ..utils.logging import get_logger
 from .block_manager import make_block_manager
 from .model_runner import ModelRunner, build_step_inputs
 from .scheduler import Scheduler
-from .sequence import SamplingParams, Sequence
+from .sequence import PENDING, SamplingParams, Sequence
 from .tokenizer import BaseTokenizer, load_tokenizer
 
 logger = get_logger(__name__)
@@ -73,6 +73,8 @@ class LLMEngine:
                                   cascade=cfg.enable_cascade_attention)
         self.requests: Dict[str, Sequence] = {}
         self.timing = {"prepare_s": 0.0, "execute_s": 0.0, "post_s": 0.0}   # host-side step anatomy
+        self.async_scheduling = bool(getattr(cfg, "async_scheduling", True))
+        self._inflight = None      # (batch, samplers, PendingStep) of the step on the GPU
         self.ps = pstate()
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
                     f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
@@ -95,7 +97,7 @@ class LLMEngine:
             seq.finish_reason = "abort"
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     def warmup(self) -> None:
         """Capture decode graphs (all TP ranks must call this together)."""
@@ -103,6 +105,116 @@ class LLMEngine:
             self.runner.capture_graphs()
 
     def step(self) -> List[StepOutput]:
+        """One engine iteration.  Overlap mode (``async_scheduling``): schedule + launch step N+1
+        while step N is still on the GPU, then collect N -- the host's scheduling, input packing
+        and token bookkeeping hide behind the device instead of idling it between steps."""
+        return self._step_overlap() if self.async_scheduling else self._step_sync()
+
+    # -- overlap (one-step lookahead) ------------------------------------------------------------
+    def _samplers(self, batch) -> List[Sequence]:
+        """Rows of a batch that sample a token, in sampled-vector order."""
+        return [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
+
+    def _ends_after(self, seq: Sequence, tok: Optional[int]) -> bool:
+        """Will the token about to be sampled certainly finish ``seq``?  (tok: known forced token)"""
+        k = len(seq.output_ids) + 1
+        p = seq.params
+        if k >= p.max_tokens or seq.num_tokens + 1 >= self.cfg.max_model_len:
+            return True
+        if p.forced_output is not None and k >= len(p.forced_output) and not p.ignore_eos:
+            return True
+        return tok is not None and not p.ignore_eos and (tok in self.eos_ids or tok in p.stop_token_ids)
+
+    def _advance(self, batch, samplers: List[Sequence]) -> None:
+        """Host view of an in-flight step as if it had completed: KV written (num_computed), full
+        blocks committed, one placeholder token per sampler (device-gathered by the next step)."""
+        for seq, start, n in batch.prefill:
+            if not seq.finished:
+                seq.num_computed = start + n
+        for seq in batch.decode:
+            if not seq.finished:
+                seq.num_computed = seq.num_tokens
+        for i, seq in enumerate(samplers):
+            if seq.finished:
+                continue
+            forced = seq.params.forced_output
+            k = len(seq.output_ids)
+            tok = forced[k] if forced is not None and k < len(forced) else None
+            if self._ends_after(seq, tok):
+                seq.awaiting = True            # sits out the next step; resolved by _resolve
+            else:
+                seq.output_ids.append(PENDING if tok is None else tok)
+                seq.pending_src = i if tok is None else -1
+            self.bm.commit(seq)
+        for seq, start, n in batch.prefill:
+            if not seq.finished and start + n < seq.num_tokens:
+                self.bm.commit(seq)
+
+    def _resolve(self, samplers: List[Sequence], sampled: List[int]) -> List[StepOutput]:
+        now = time.perf_counter()
+        outs: List[StepOutput] = []
+        for seq, tok in zip(samplers, sampled):
+            if seq.finished:                   # aborted (or finished) while in flight
+                continue
+            forced = seq.params.forced_output
+            if seq.awaiting:
+                seq.awaiting = False
+                k = len(seq.output_ids)
+                tok = forced[k] if forced is not None and k < len(forced) else int(tok)
+                seq.output_ids.append(tok)
+            elif seq.pending_src >= 0:
+                tok = int(tok)
+                seq.output_ids[-1] = tok
+                seq.pending_src = -1
+            else:                              # forced token, appended at launch time
+                tok = seq.output_ids[-1]
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            reason = None
+            if len(seq.output_ids) >= seq.params.max_tokens:
+                reason = "length"
+            elif forced is not None and len(seq.output_ids) >= len(forced) and not seq.params.ignore_eos:
+                reason = "stop"
+            elif not seq.params.ignore_eos and (tok in self.eos_ids or tok in seq.params.stop_token_ids):
+                reason = "stop"
+            elif seq.num_tokens >= self.cfg.max_model_len:
+                reason = "length"
+            if reason is not None:
+                # its speculative row in the step now in flight writes into blocks freed here; any
+                # reuse is by a LATER step, ordered after it on the stream
+                self.scheduler.finish(seq, reason)
+                self.requests.pop(seq.request_id, None)
+            outs.append(StepOutput(seq.request_id, [tok], reason is not None, reason, seq))
+        return outs
+
+    def _step_overlap(self) -> List[StepOutput]:
+        t0 = time.perf_counter()
+        prev = self._inflight
+        if prev is not None:
+            self._advance(prev[0], prev[1])
+        batch = self.scheduler.schedule()
+        launched = None
+        t1 = t0
+        if not batch.empty():
+            si = build_step_inputs(batch)
+            if self.ps.tp_size > 1:
+                comm.broadcast_object(si)
+            t1 = time.perf_counter()
+            launched = (batch, self._samplers(batch), self.runner.launch(si))
+        t2 = time.perf_counter()
+        outs: List[StepOutput] = []
+        if prev is not None:
+            outs = self._resolve(prev[1], prev[2].result())
+        self._inflight = launched
+        t3 = time.perf_counter()
+        tm = self.timing
+        tm["prepare_s"] += t1 - t0
+        tm["execute_s"] += t2 - t1
+        tm["post_s"] += t3 - t2
+        return outs
+
+    # -- synchronous ------------------------------------------------------------------------------
+    def _step_sync(self) -> List[StepOutput]:
         t0 = time.perf_counter()
         batch = self.scheduler.schedule()
         if batch.empty():

@@ -47,6 +47,7 @@ class StepInputs:
     seeds: np.ndarray               # [S] int64
     top_k: np.ndarray               # [S]
     top_p: np.ndarray               # [S]
+    src: Optional[np.ndarray] = None  # [Bd] row of the previous step's sampled vector (-1: ids[] is real)
 
     @property
     def num_prefill_tokens(self) -> int:
@@ -86,10 +87,15 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
             tk.append(seq.params.top_k)
             tp.append(seq.params.top_p)
     Tp = cu[-1]
-    ctx_d, tables_d = [], []
+    ctx_d, tables_d, src = [], [], []
     for j, seq in enumerate(batch.decode):
         p = seq.num_tokens - 1
-        ids.append(seq.all_ids[-1])
+        if seq.pending_src >= 0:      # token sampled by the step still in flight: device gather
+            ids.append(0)
+            src.append(seq.pending_src)
+        else:
+            ids.append(seq.output_ids[-1] if seq.output_ids else seq.prompt_ids[-1])
+            src.append(-1)
         pos.append(p)
         slots.extend(_slots(seq, p, 1))
         ctx_d.append(seq.num_tokens)
@@ -108,9 +114,25 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
         return out
 
     i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
+    src_a = i32(src) if any(x >= 0 for x in src) else None
     return StepInputs(i32(ids), i32(pos), i32(slots), i32(cu), i32(ctx_p), table(tables_p), max_q, i32(ctx_d),
                       table(tables_d), np.asarray(logits_idx, np.int64), np.asarray(temps, np.float32),
-                      np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32))
+                      np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32), src_a)
+
+
+class PendingStep:
+    """Sampled ids of a launched step (host copy in flight)."""
+
+    def __init__(self, cpu_out: Optional[torch.Tensor], n: int, host: Optional[torch.Tensor], event):
+        self._cpu, self.n, self._host, self._event = cpu_out, n, host, event
+
+    def result(self) -> List[int]:
+        if self.n == 0:
+            return []
+        if self._cpu is not None:
+            return self._cpu.tolist()
+        self._event.synchronize()
+        return self._host[:self.n].tolist()
 
 
 class _DecodeGraph:
@@ -140,6 +162,13 @@ class ModelRunner:
         self._static = None
         self.graph_pool = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0}
+        # sampled ids of the latest step stay on the device: the next step gathers its decode ids
+        # from here when it was launched before this one's ids reached the host (overlap mode)
+        self.max_samplers = max(self.max_decode_batch, max_decode_batch) + 1024
+        self.last_sampled = torch.zeros(self.max_samplers, dtype=torch.int32, device=self.device)
+        self._pinned_out = ([torch.zeros(self.max_samplers, dtype=torch.int32).pin_memory() for _ in range(2)]
+                            if self.on_gpu else None)
+        self._out_flip = 0
 
     # ------------------------------------------------------------------------------------
     # eager path
@@ -175,8 +204,15 @@ class ModelRunner:
             self.stats["cascade_rows"] += len(plan.members)
         return plan
 
+    def _gather_pending(self, ids: torch.Tensor, src: torch.Tensor, offset: int) -> None:
+        """ids[offset + r] <- last_sampled[src[r]] where src[r] >= 0 (device-side, no host sync)."""
+        rows = ids[offset:offset + src.shape[0]]
+        rows.copy_(torch.where(src >= 0, self.last_sampled[src.clamp(min=0).long()], rows))
+
     def forward_logits(self, si: StepInputs) -> torch.Tensor:
         ids = self._to_dev(si.ids)
+        if si.src is not None:
+            self._gather_pending(ids, self._to_dev(si.src), si.num_prefill_tokens)
         pos = self._to_dev(si.positions)
         slots = self._to_dev(si.slots)
         meta = self._meta(si, slots)
@@ -194,17 +230,31 @@ class ModelRunner:
 
     def execute(self, si: StepInputs) -> List[int]:
         """Run one step; returns the sampled token per entry of ``si.logits_idx``."""
+        return self.launch(si).result()
+
+    def launch(self, si: StepInputs) -> "PendingStep":
+        """Enqueue one step on the current stream and return without waiting for the GPU; the
+        sampled ids reach the host through ``PendingStep.result()`` (pinned D2H + event)."""
         self.stats["steps"] += 1
         self.stats["tokens"] += len(si.ids)
         if len(si.logits_idx) == 0:
             self._forward_only(si)
-            return []
+            return PendingStep(None, 0, None, None)
         if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
                 and not (si.top_k > 0).any() and not (si.top_p < 1).any()):
-            return self._graph_decode(si)
-        logits = self.forward_logits(si)
-        out = self.sample(logits, si)
-        return out.cpu().tolist()
+            out = self._graph_decode(si)
+        else:
+            out = self.sample(self.forward_logits(si), si)
+        n = len(si.logits_idx)
+        self.last_sampled[:n].copy_(out[:n].to(torch.int32), non_blocking=True)
+        if not self.on_gpu:
+            return PendingStep(out[:n].clone(), n, None, None)
+        host = self._pinned_out[self._out_flip]
+        self._out_flip ^= 1
+        host[:n].copy_(out[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return PendingStep(None, n, host, ev)
 
     def _forward_only(self, si: StepInputs) -> None:
         ids = self._to_dev(si.ids)
@@ -219,25 +269,29 @@ class ModelRunner:
         B, W = self.max_decode_batch, self.max_blocks
         # ids | pos | slots | ctx | block tables | cascade plan live in ONE device buffer fed by ONE
         # pinned H2D copy
-        self._cas_off = 4 * B + B * W
+        self._src_off = 4 * B + B * W          # pending-token gather rows (-1: host id)
+        self._cas_off = self._src_off + B
         n_cas = sum(n for _, n in CascadeInputs.section_sizes(B)) if self.cascade else 0
         self._dev_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32, device=self.device)
         d = self._dev_i32
         self._static = {
             "ids": d[0:B], "pos": d[B:2 * B], "slots": d[2 * B:3 * B], "ctx": d[3 * B:4 * B],
-            "bt": d[4 * B:self._cas_off].view(B, W),
+            "bt": d[4 * B:self._src_off].view(B, W),
+            "src": d[self._src_off:self._cas_off],
             "cascade": CascadeInputs.views(d[self._cas_off:], B) if self.cascade else None,
             "temps": torch.zeros(B, dtype=torch.float32, device=self.device),
             "seeds": torch.zeros(B, dtype=torch.int64, device=self.device),
         }
         self._static["slots"].fill_(-1)
         self._static["ctx"].fill_(1)
+        self._static["src"].fill_(-1)
         self._pinned_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32).pin_memory()
         self._pinned_f = torch.zeros(B, dtype=torch.float32).pin_memory()
         self._pinned_l = torch.zeros(B, dtype=torch.int64).pin_memory()
 
     def _run_static(self, B: int) -> torch.Tensor:
         s = self._static
+        self._gather_pending(s["ids"], s["src"][:B], 0)
         meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
                                  ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
                                  cascade=s["cascade"])
@@ -289,6 +343,10 @@ class ModelRunner:
         bt = buf[4 * S:4 * S + S * W].reshape(S, W)
         bt[:B] = 0
         bt[:n, :si.bt_d.shape[1]] = si.bt_d
+        src = buf[self._src_off:self._src_off + S]
+        src[:B] = -1
+        if si.src is not None:
+            src[:n] = si.src
         if self.cascade:
             CascadeInputs.pack(self._plan(si), buf[self._cas_off:], S, n)
         self._pinned_f.numpy()[:n] = si.temps
@@ -299,4 +357,4 @@ class ModelRunner:
         s["seeds"].copy_(self._pinned_l, non_blocking=True)
         G.graph.replay()
         self.stats["graph_steps"] += 1
-        return G.out[:n].cpu().tolist()
+        return G.out[:n]

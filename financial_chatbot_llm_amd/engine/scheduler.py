@@ -79,7 +79,7 @@ class Scheduler:
         batch = ScheduledBatch()
         budget = self.max_num_batched_tokens
         # 1) decodes (oldest first); preempt youngest when blocks run out
-        decodes = [s for s in self.running if s.remaining_prefill == 1]
+        decodes = [s for s in self.running if s.remaining_prefill == 1 and not s.awaiting]
         for seq in sorted(decodes, key=lambda s: s.arrival):
             if seq not in self.running:
                 continue
@@ -94,7 +94,8 @@ class Scheduler:
             batch.decode.append(seq)
             budget -= 1
         # 2) continuing prefills
-        for seq in sorted((s for s in self.running if s.remaining_prefill > 1), key=lambda s: s.arrival):
+        for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting),
+                          key=lambda s: s.arrival):
             if budget <= 0:
                 break
             n = min(seq.remaining_prefill, budget)
@@ -105,6 +106,8 @@ class Scheduler:
         # 3) admit waiting sequences
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
+            if seq.pending_src >= 0 or seq.awaiting:
+                break   # preempted with an in-flight token: re-admit once it is known
             if not seq.block_table:
                 self.bm.match_prefix(seq)
             n = min(seq.remaining_prefill, budget)
@@ -124,4 +127,6 @@ class Scheduler:
         seq.finish_reason = reason
         if seq in self.running:
             self.running.remove(seq)
+        elif seq in self.waiting:          # preempted while its last token was in flight
+            self.waiting.remove(seq)
         self.bm.free(seq)

@@ -29,6 +29,9 @@ class SeqStatus(enum.Enum):
 _ids = itertools.count()
 
 
+PENDING = -1   # placeholder token id (never fed to the model: gathered on the device instead)
+
+
 class Sequence:
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams, arrival: Optional[float] = None):
         self.seq_id = next(_ids)
@@ -45,6 +48,12 @@ class Sequence:
         self.finish_reason: Optional[str] = None
         self.seed = params.seed if params.seed is not None else (hash((request_id, self.seq_id)) & 0x7FFFFFFF)
         self.num_preemptions = 0
+        # overlap scheduling (LLMEngine, async_scheduling): while step N runs, the sequence carries
+        # a placeholder for N's sampled token (output_ids[-1] == PENDING); pending_src is its row in
+        # N's sampled vector, gathered on the device by step N+1.  awaiting: N's token certainly
+        # ends the sequence (length / forced end), so it sits out N+1.
+        self.pending_src = -1
+        self.awaiting = False
 
     @property
     def all_ids(self) -> List[int]:
