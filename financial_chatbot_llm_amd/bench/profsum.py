@@ -15,7 +15,7 @@ from collections import defaultdict
 
 CLASSES = [
     ("attention-decode", r"decode_kernel|decode_reduce"),
-    ("attention-prefill", r"prefill_kernel"),
+    ("attention-prefill", r"prefill_kernel|prefill2_kernel|cascade_kernel"),
     ("gemm-skinny (HIP)", r"skinny"),
     ("moe (HIP)", r"moe_|quant_rows"),
     ("gemm (hipBLASLt)", r"^Cijk|^Custom_Cijk|gemm"),
@@ -60,13 +60,37 @@ def summarise(path: str, title: str, top: int) -> str:
     return "\n".join(out) + "\n"
 
 
+def utilisation(trace_csv: str) -> str:
+    """GPU busy time (union of kernel intervals) over the traced span -- what the host leaves idle."""
+    iv = []
+    with open(trace_csv) as fh:
+        for r in csv.DictReader(fh):
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    iv.sort()
+    busy, (cs, ce) = 0, iv[0]
+    for s_, e_ in iv[1:]:
+        if s_ > ce:
+            busy += ce - cs
+            cs, ce = s_, e_
+        else:
+            ce = max(ce, e_)
+    busy += ce - cs
+    span = iv[-1][1] - iv[0][0]
+    return f"GPU busy {busy / 1e9:.2f} s of a {span / 1e9:.2f} s traced span ({100 * busy / span:.1f} %).\n"
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--title", default="")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--trace", default="", help="kernel_trace.csv: also report GPU busy fraction")
     a = ap.parse_args(argv)
-    print(summarise(a.csv, a.title, a.top), end="")
+    text = summarise(a.csv, a.title, a.top)
+    if a.trace:
+        head, rest = text.split("\n\n", 1)
+        text = head + "\n\n" + utilisation(a.trace) + "\n" + rest
+    print(text, end="")
     return 0
 
 
