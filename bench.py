@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tool-steps", type=int, default=1,
+                    help=">1: multi-step agent with the plot tool bound (north-star config 4)")
     ap.add_argument("--arrival", default="closed", choices=["closed", "wave"],
                     help="closed: each conversation sends its next turn when its last completes (default); "
                          "wave: all conversations send in lock-step waves")
@@ -84,7 +86,8 @@ async def run(args, ps):
     log(f"engine ready in {time.perf_counter() - t0:.1f}s")
     llm = EngineLLM(engine, max_model_len=args.max_model_len, decide_script=decide_script,
                     respond_ignore_eos=True, respond_tokens=args.respond_tokens)
-    wl = RagWorkload(llm, retrieval, args.convs, args.users, args.respond_tokens, rank=ps.rank)
+    wl = RagWorkload(llm, retrieval, args.convs, args.users, args.respond_tokens, rank=ps.rank,
+                     max_tool_steps=args.tool_steps)
     wl.kafka.setup_consumer()
     consumer = asyncio.create_task(wl.worker.consume_messages())
 
@@ -157,6 +160,7 @@ def main(argv=None) -> int:
             "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
+                       "tool_steps": args.tool_steps,
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},
             "p50_ttft_ms": None if p50 is None else round(p50, 1),

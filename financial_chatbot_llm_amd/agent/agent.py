@@ -54,7 +54,7 @@ def initial_state(user_query: str, user_id: str, user_context: str, chat_history
 class LLMAgent:
     def __init__(self, llm: LLMBackend, retrieval_tool: Tool, extra_tools: Sequence[Tool] = (),
                  temperature: float = config.DEFAULT_TEMPERATURE, max_response_tokens: int = 512,
-                 max_decide_tokens: int = 96, max_tool_steps: int = 1,
+                 max_decide_tokens: int = 160, max_tool_steps: int = 1,
                  today_fn: Callable[[], _dt.date] = _dt.date.today,
                  system_prompt: Optional[str] = None, tool_prompt: Optional[str] = None):
         self.llm = llm

@@ -32,6 +32,7 @@ from ..retrieval import RetrievalService
 from ..retrieval.store import MERCHANTS, user_name
 from ..serving.worker import ChatWorker
 from ..tools import make_plot_tool, make_retrieval_tool
+from ..tools.base import ToolCall
 
 ADVICE_QUESTIONS = [
     "How should I invest for retirement given my income?",
@@ -78,13 +79,13 @@ class RagWorkload:
     """Owns the fakes, the worker and the synthetic conversations for one GPU replica."""
 
     def __init__(self, llm, retrieval: RetrievalService, num_convs: int, num_users: int,
-                 respond_tokens: int, seed: int = 0, rank: int = 0):
+                 respond_tokens: int, seed: int = 0, rank: int = 0, max_tool_steps: int = 1):
         self.rng = random.Random(seed * 7919 + rank)
         self.broker = InMemoryBroker(num_partitions=16)
         self.db = Database(uri="")
         self.kafka = KafkaClient(broker=self.broker)
         self.agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
-                              max_response_tokens=respond_tokens)
+                              max_response_tokens=respond_tokens, max_tool_steps=max_tool_steps)
         self.worker = ChatWorker(self.db, self.kafka, self.agent, max_concurrent_turns=4 * num_convs)
         self.convs = []
         for i in range(num_convs):
@@ -165,8 +166,21 @@ def ttft_stages(traces) -> Dict[str, List[float]]:
     return out
 
 
+PLOT_CALL = ToolCall("create_financial_plot", {"plot_config": {"plot_type": "bar", "x_axis": "date",
+                                                                "title": "Spending"}})
+
+
 def decide_script(messages, tools) -> str:
-    """Scripted decision for random-weight benchmarking: the reference's few-shot rule set."""
+    """Scripted decision for random-weight benchmarking: the reference's few-shot rule set.
+
+    Multi-step agent (plot tool bound, north-star config 4): once transactions were retrieved the
+    next decision plots them, after the plot it answers."""
+    names = {t.name for t in tools}
+    system = messages[0].content if messages else ""
+    if "[retrieve_transactions]" in system:
+        if PLOT_CALL.name in names and f"[{PLOT_CALL.name}]" not in system:
+            return format_tool_call(PLOT_CALL)
+        return "No tool call"
     call = scripted_decision(messages[-1].content) if messages else None
     if call is None or not any(t.name == call.name for t in tools):
         return "No tool call"

@@ -46,3 +46,38 @@ def test_rag_workload_cpu():
     assert eng.engine.bm.hits > 0
     saved = list(wl.db.messages_collection.find({"sender": "AIMessage"}))
     assert len(saved) == 16 and all(isinstance(d["message"], str) for d in saved)
+
+
+def test_multistep_agent_workload_cpu():
+    """North-star config 4's agent loop on the bench workload: retrieve, then plot, then answer."""
+    emb = BgeEmbedder("bert-tiny", device="cpu")
+    store = DeviceVectorStore(emb.dim, device="cpu")
+    store.load_synthetic(5000, 50, seed=0)
+    ret = RetrievalService(emb, store)
+    ecfg = EngineConfig(model="llama-tiny", device="cpu", num_kv_blocks=256, max_model_len=4096,
+                        max_num_batched_tokens=4096, use_cuda_graph=False, max_num_seqs=16)
+    eng = AsyncEngine(ecfg)
+    llm = EngineLLM(eng, max_model_len=4096, decide_script=decide_script, respond_ignore_eos=True, respond_tokens=6)
+
+    async def main():
+        wl = RagWorkload(llm, ret, num_convs=4, num_users=50, respond_tokens=6, max_tool_steps=3)
+        plot = wl.agent.tools["create_financial_plot"]
+        real = plot.ainvoke
+
+        async def counted(args):
+            calls.append(args)
+            return await real(args)
+        plot.ainvoke = counted
+        wl.kafka.setup_consumer()
+        task = asyncio.create_task(wl.worker.consume_messages())
+        r = await wl.run_closed_loop(1)
+        wl.worker.stop()
+        await task
+        return r
+    calls = []
+    try:
+        r = asyncio.run(main())
+    finally:
+        eng.shutdown()
+    assert r.turns == 4 and r.errors == 0 and r.retrievals == 2
+    assert len(calls) == 2 and all(c["plot_config"]["plot_type"] == "bar" for c in calls)

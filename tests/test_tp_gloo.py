@@ -1,4 +1,4 @@
-"""Tensor parallelism on CPU with gloo, world_size 2 (SURVEY §4 'Distributed').
+"""Tensor parallelism on CPU with gloo, world_size 2 and 4 (SURVEY §4 'Distributed').
 
 Each rank owns half the heads / half the MLP columns / half the vocabulary; row-parallel outputs
 are all-reduced (C1), vocab-parallel logits all-gathered (C2), and the engine leader broadcasts
@@ -53,7 +53,8 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_tp2_matches_tp1():
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_matches_tp1(world):
     from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
     from financial_chatbot_llm_amd.engine.tokenizer import SyntheticLlamaTokenizer
     from financial_chatbot_llm_amd.models.llama import LlamaModel
@@ -62,11 +63,11 @@ def test_tp2_matches_tp1():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         r, a, b = q.get(timeout=240)
         res[r] = (a, b)
     for p in procs:
@@ -77,8 +78,8 @@ def test_tp2_matches_tp1():
     cfg = get_model_config("llama-tiny-tp")
     ref = LlamaModel(cfg, device="cpu", tp_rank=0, tp_size=1, dtype=torch.float32).init_random(seed=7, std=0.05)
     ref_logits = _prefill_logits(ref, list(range(3, 140)))
-    assert torch.allclose(res[0][0], ref_logits, atol=1e-4, rtol=1e-4)
-    assert torch.allclose(res[1][0], ref_logits, atol=1e-4, rtol=1e-4)
+    for r in range(world):
+        assert torch.allclose(res[r][0], ref_logits, atol=1e-4, rtol=1e-4)
     ecfg = EngineConfig(model="unused", device="cpu", num_kv_blocks=32, max_model_len=1024,
                         max_num_batched_tokens=64, use_cuda_graph=False)
     eng = LLMEngine(ecfg, model=ref, tokenizer=SyntheticLlamaTokenizer(cfg.vocab_size))
