@@ -8,12 +8,11 @@
 // interleave16 = 0: [gate 0..F-1 | up 0..F-1];  interleave16 = 1: 16-column groups alternate
 // gate/up (gate 16i..16i+15, up 16i..16i+15), the layout the decode skinny GEMM's fused SiLU
 // epilogue needs, so one weight tensor serves both paths.
+// grid (chunks/256, rows): no 64-bit index division on the hot path (it dominated at decode sizes)
 __global__ void silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out, int T, int F, int il16) {
   const int cpr = F >> 3;  // 16-byte chunks per output row
-  const long total = (long)T * cpr;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long t = i / cpr;
-    const int c = (int)(i - t * cpr);
+  const long t = blockIdx.y;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cpr; c += gridDim.x * blockDim.x) {
     const uint4* row = reinterpret_cast<const uint4*>(gu + t * 2L * F);
     float g[8], u[8], o[8];
     if (il16) {  // chunk c covers output cols 8c..8c+7 = pair (8c)/16, half (c & 1)
@@ -68,8 +67,9 @@ static inline int grid_for(long work, int threads) {
 PENNY_API int penny_silu_mul(const void* gu, void* out, int T, int F, int interleave16, hipStream_t stream) {
   if (T <= 0) return 0;
   if (F % (interleave16 ? 16 : 8)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for((long)T * (F / 8), 256)), dim3(256), 0, stream,
-                     (const bf16*)gu, (bf16*)out, T, F, interleave16);
+  if (T > 65535) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, stream, (const bf16*)gu,
+                     (bf16*)out, T, F, interleave16);
   PENNY_RETURN_LAUNCH();
 }
 

@@ -53,6 +53,55 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16* __restrict__ 
   }
 }
 
+
+// One wave64 per row (rows of H = 512*CPW elements): every lane holds CPW 16-byte chunks, the
+// weight is fetched together with x/residual (one memory round trip instead of three), and the
+// sum of squares is a pure register/DPP reduction -- no LDS, no barrier.  Decode-size batches
+// (T = 1..256 rows) are latency-bound, so this is what keeps a B=128 norm at a few us.
+template <int CPW, bool ADD_RES>
+__global__ void __launch_bounds__(256) rmsnorm_wave_kernel(const bf16* __restrict__ x, bf16* __restrict__ res,
+                                                           const bf16* __restrict__ w, bf16* __restrict__ y,
+                                                           int T, int H, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * H);
+  uint4* rr = reinterpret_cast<uint4*>(res + (size_t)row * H);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4 xv[CPW], rv[CPW], wv[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    xv[c] = xr[lane + 64 * c];
+    if (ADD_RES) rv[c] = rr[lane + 64 * c];
+    wv[c] = wr[lane + 64 * c];
+  }
+  float v[CPW][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    unpack8(xv[c], v[c]);
+    if (ADD_RES) {
+      float r[8];
+      unpack8(rv[c], r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = (float)(bf16)(v[c][i] + r[i]);  // residual kept in bf16
+      rr[lane + 64 * c] = pack8(v[c]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+  }
+  const float inv = rsqrtf(wave_sum(ss) / (float)H + eps);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * H);
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    float g[8], o[8];
+    unpack8(wv[c], g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(v[c][i] * inv) * g[i];
+    yr[lane + 64 * c] = pack8(o);
+  }
+}
+
 template <int CPT, bool ADD_RES>
 __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                          const bf16* __restrict__ g, const bf16* __restrict__ b,
@@ -136,6 +185,22 @@ PENNY_API int penny_rmsnorm(const void* x, void* res, const void* w, void* y, in
                             int add_residual, hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8) return (int)hipErrorInvalidValue;
+  if (H % 512 == 0 && H <= 4096 && T <= 4096) {   // wave-per-row path (decode + short prefill)
+    const int cpw = H / 512;
+    dim3 grid((T + 3) / 4);
+#define WAVE_NORM(CPW_)                                                                                        \
+  if (cpw == CPW_) {                                                                                           \
+    if (add_residual)                                                                                          \
+      hipLaunchKernelGGL((rmsnorm_wave_kernel<CPW_, true>), grid, dim3(256), 0, stream, (const bf16*)x,        \
+                         (bf16*)res, (const bf16*)w, (bf16*)y, T, H, eps);                                     \
+    else                                                                                                       \
+      hipLaunchKernelGGL((rmsnorm_wave_kernel<CPW_, false>), grid, dim3(256), 0, stream, (const bf16*)x,       \
+                         (bf16*)res, (const bf16*)w, (bf16*)y, T, H, eps);                                     \
+    PENNY_RETURN_LAUNCH();                                                                                     \
+  }
+    WAVE_NORM(1) WAVE_NORM(2) WAVE_NORM(4) WAVE_NORM(8)
+#undef WAVE_NORM
+  }
   int threads, cpt;
   pick_geometry(H, &threads, &cpt);
   if (add_residual) {

@@ -40,12 +40,16 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
       unpack8(*reinterpret_cast<const uint4*>(src + c * 8), x1);
       unpack8(*reinterpret_cast<const uint4*>(src + HALF + c * 8), x2);
       if (apply_rope) {
+        float co[8], si[8];   // 4 x 16-B loads instead of 16 scalar loads
+        *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
+        *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+        *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
+        *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float co = cs[c * 8 + i], si = cs[HALF + c * 8 + i];
           const float a = x1[i], b = x2[i];
-          x1[i] = a * co - b * si;
-          x2[i] = b * co + a * si;
+          x1[i] = a * co[i] - b * si[i];
+          x2[i] = b * co[i] + a * si[i];
         }
       }
       const uint4 p1 = pack8(x1), p2 = pack8(x2);

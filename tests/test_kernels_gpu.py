@@ -34,7 +34,7 @@ def test_native_library_loaded():
     assert "libpenny_kernels.so" in maps
 
 
-@pytest.mark.parametrize("T,H", [(1, 4096), (37, 4096), (64, 8192), (5, 768)])
+@pytest.mark.parametrize("T,H", [(1, 4096), (37, 4096), (64, 8192), (5, 768), (130, 2048), (5000, 4096), (3, 512)])
 def test_rmsnorm(T, H):
     torch.manual_seed(0)
     x, res, w = rnd(T, H), rnd(T, H), rnd(H, scale=0.1) + 1
