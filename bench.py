@@ -156,7 +156,8 @@ def main(argv=None) -> int:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * tmax / max(args.steps, 1), 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if args.dtype == "bf16" else "bf16 (fp8 e4m3 MoE experts)",
-            "data": "synthetic conversations + 1M-vector synthetic corpus; random-init weights of the real architectures",
+            "data": f"synthetic conversations + {args.corpus:,}-vector synthetic corpus per GPU; "
+                    "random-init weights of the real architectures",
             "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",

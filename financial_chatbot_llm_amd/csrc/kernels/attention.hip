@@ -629,7 +629,9 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      int part_stride, float scale, const int* kv_start, const int* members,
                                      const int* cu_g, const int* g_ctx, const int* g_bt, const int* work,
                                      const int* nwork, int grid_work, int g_max_blocks, int chunk_blocks,
-                                     hipStream_t stream) {
+                                     int phases, hipStream_t stream) {
+  // phases: 1 cascade (shared-prefix tiles), 2 split-K decode, 4 merge -- the caller may run
+  // phase 1 on a side stream concurrently with phase 2 (ops/attention.py), joining before 4
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
   const bool cascade = kv_start != nullptr;
@@ -640,13 +642,14 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   const float sl2 = scale * LOG2E;
   const CascadeArgs ca{members, work, nwork, part_m, part_l, part_o, part_stride, nparts, chunk_blocks};
 #define DECODE_LAUNCH(DD)                                                                                         \
-  if (cascade)                                                                                                  \
+  if (cascade && (phases & 1))                                                                                  \
     hipLaunchKernelGGL(cascade_kernel<DD>, dim3(grid_work, Hkv), dim3(256), 0, stream, (const bf16*)q, cu_g, g_ctx,  \
                        g_bt, (const bf16*)k_cache, (const bf16*)v_cache, sl2, Hq, Hkv, g_max_blocks, ca);         \
-  hipLaunchKernelGGL(decode_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start, block_tables, \
-                     (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l, part_o, sl2, Hq, Hkv,   \
-                     max_blocks, pb, nparts, part_stride);                                                        \
-  if (nparts > 1 || cascade)                                                                                    \
+  if (phases & 2)                                                                                               \
+    hipLaunchKernelGGL(decode_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start,          \
+                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
+                       part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
+  if ((phases & 4) && (nparts > 1 || cascade))                                                                  \
     hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, ctx_lens, kv_start, part_m,     \
                        part_l, part_o, (bf16*)out, Hq, pb, nparts, part_stride, chunk_blocks);
   if (D == 128) {

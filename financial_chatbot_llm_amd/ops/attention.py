@@ -349,6 +349,16 @@ class CascadeInputs:
         return cls.views(buf, B)
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
 def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, k_cache: torch.Tensor,
            v_cache: torch.Tensor, scale: float, workspace: Optional[DecodeWorkspace] = None,
            max_ctx: Optional[int] = None, out: Optional[torch.Tensor] = None,
@@ -371,9 +381,22 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
                 N.ptr(c.nwork), c.grid, CASCADE_MAX_BLOCKS, CASCADE_CHUNK) if c is not None
                else (None, None, None, None, None, None, None, 0, 0, 0))
         pb, nparts = ws.partitioning(B) if c is None else (ws.pb, ws.nparts)
-        N.call("penny_attention_decode", N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache),
-               N.ptr(v_cache), N.ptr(out), N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D,
-               block_tables.shape[1], pb, nparts, ws.part_stride, float(scale), *cas, N.stream())
+        args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
+                N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
+                nparts, ws.part_stride, float(scale), *cas]
+        if c is None:
+            N.call("penny_attention_decode", *args, 7, N.stream())
+        else:
+            # shared-prefix tiles on a side stream, concurrent with the per-row suffix partitions;
+            # join before the merge (fork/join via events: hipGraph-capturable)
+            main = torch.cuda.current_stream()
+            side = _side_stream(q.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                N.call("penny_attention_decode", *args, 1, side.cuda_stream)
+            N.call("penny_attention_decode", *args, 2, main.cuda_stream)
+            main.wait_stream(side)
+            N.call("penny_attention_decode", *args, 4, main.cuda_stream)
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()

@@ -61,7 +61,8 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None, device_typ
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if backend is None:
-        backend = "nccl" if device_type == "cuda" else "gloo"   # "nccl" is RCCL on ROCm
+        # "nccl" is RCCL on ROCm; PENNY_DIST_BACKEND=gloo rehearses multi-rank paths on one GPU
+        backend = os.environ.get("PENNY_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if device_type == "cuda":
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
     if world > 1 and not dist.is_initialized():
