@@ -97,15 +97,17 @@ class MetricsRegistry:
         ttfts = [t.ttft for t in traces if t.ttft is not None]
         lats = [t.latency for t in traces if t.latency is not None]
         itl = [x for t in traces for x in t.itls()]
-        ret = [t.stages["search_done"] - t.stages["search_start"] for t in traces
-               if "search_done" in t.stages and "search_start" in t.stages]
+        # decide_done -> retrieval_done: embed + filtered top-k (+ tool execution), marked by the worker
+        ret = [t.stages["retrieval_done"] - t.stages["decide_done"] for t in traces
+               if "retrieval_done" in t.stages and "decide_done" in t.stages]
+        decide = [t.stages["decide_done"] - t.t_receive for t in traces if "decide_done" in t.stages]
         done = [t.t_complete for t in traces if t.t_complete is not None]
         span = (max(done) - min(t.t_receive for t in traces)) if done else 0.0
         out: Dict[str, Optional[float]] = {
             "turns_per_s": (len(done) / span) if span > 0 else None,
             "ttft_p50_s": percentile(ttfts, 50), "ttft_p99_s": percentile(ttfts, 99),
             "latency_p50_s": percentile(lats, 50), "itl_p50_s": percentile(itl, 50),
-            "retrieval_p50_s": percentile(ret, 50),
+            "retrieval_p50_s": percentile(ret, 50), "decide_p50_s": percentile(decide, 50),
         }
         out.update(counters)
         out.update(gauges)

@@ -118,3 +118,110 @@ def test_http_surface():
                 r = await cl.get("/metrics")
                 assert r.status_code == 200
     asyncio.run(main())
+
+
+# ---- fault injection in the fakes (drop, delay, raise) ------------------------------
+def test_fault_poll_errors_back_off_and_recover(monkeypatch):
+    """Consumer-loop errors are logged and retried after the backoff (main.py:157-159); the turn
+    is processed once polling recovers."""
+    monkeypatch.setattr(config, "LOOP_ERROR_BACKOFF_S", 0.01)
+    svc = services(StubLLM(responses=["ok"]))
+    svc.kafka.broker.faults.raise_on_poll = True
+
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent)
+        task = asyncio.create_task(w.consume_messages())
+        send(svc, "c1", "hello")
+        await asyncio.sleep(0.1)
+        assert not w.traces                     # nothing consumed while polling fails
+        svc.kafka.broker.faults.raise_on_poll = False
+        for _ in range(300):
+            await asyncio.sleep(0.01)
+            if w.traces:
+                break
+        w.stop()
+        await task
+        return w
+    w = asyncio.run(main())
+    assert len(w.traces) == 1 and not w.traces[0].error
+    assert out(svc, "c1")[-1]["type"] == "complete"
+
+
+def test_fault_dropped_chunks_still_save_the_reply():
+    """A lossy producer (dropped records) does not break the turn: the reply is still saved."""
+    svc = services(StubLLM(responses=["all the tokens"]))
+
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent)
+        send(svc, "c1", "q")                       # the request itself is delivered ...
+        svc.kafka.broker.faults.drop_produce = 1.0  # ... every reply record is lost
+        task = asyncio.create_task(w.consume_messages())
+        for _ in range(300):
+            await asyncio.sleep(0.01)
+            if w.traces and not w._tasks:
+                break
+        w.stop()
+        await task
+        return w
+    w = asyncio.run(main())
+    assert len(w.traces) == 1 and not w.traces[0].error
+    assert out(svc, "c1") == []
+    saved = [d for d in svc.db.messages_collection.find({"conversation_id": "c1", "sender": "AIMessage"})]
+    assert len(saved) == 1 and saved[0]["message"] == "all the tokens"
+
+
+def test_fault_produce_raises_marks_turn_failed():
+    """A producer that raises mid-stream: the worker reports the turn as failed, tries the
+    error event (which also fails) and keeps consuming (next turn succeeds)."""
+    svc = services(StubLLM(responses=["first", "second"]), convs=(("c1", "u1"), ("c2", "u1")))
+
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent)
+        send(svc, "c1", "q1")
+        svc.kafka.broker.faults.raise_on_produce = True
+        task = asyncio.create_task(w.consume_messages())
+        for _ in range(300):
+            await asyncio.sleep(0.01)
+            if w.traces:
+                break
+        svc.kafka.broker.faults.raise_on_produce = False
+        send(svc, "c2", "q2")
+        for _ in range(300):
+            await asyncio.sleep(0.01)
+            if len(w.traces) >= 2:
+                break
+        w.stop()
+        await task
+        return w
+    w = asyncio.run(main())
+    assert len(w.traces) == 2 and w.traces[0].error and not w.traces[1].error
+    assert out(svc, "c2")[-1]["type"] == "complete"
+
+
+def test_fault_slow_producer_delays_but_delivers():
+    """A slow (blocking) producer, like a congested librdkafka queue: every record is still
+    delivered in order and the turn's latency absorbs the delay."""
+    svc = services(StubLLM(responses=["slow answer here"]))
+
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent)
+        send(svc, "c1", "q")
+        svc.kafka.broker.faults.delay_produce_s = 0.05
+        task = asyncio.create_task(w.consume_messages())
+        for _ in range(300):
+            await asyncio.sleep(0.01)
+            if w.traces and not w._tasks:
+                break
+        w.stop()
+        await task
+        return w
+    w = asyncio.run(main())
+    svc.kafka.broker.faults.delay_produce_s = 0.0
+    tr = w.traces[0]
+    assert not tr.error and tr.t_complete - tr.t_receive >= 0.1   # >= 2 delayed records
+    ev = out(svc, "c1")
+    assert [e.get("type") for e in ev] == ["response_chunk", "complete"]
