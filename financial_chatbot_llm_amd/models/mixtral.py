@@ -39,8 +39,9 @@ from .llama import DecoderModel
 
 
 class MixtralModel(DecoderModel):
-    def __init__(self, *a, fp8: bool = False, moe_parallel: str = "tp", **kw):
+    def __init__(self, *a, fp8: bool = False, moe_parallel: str = "tp", prefill_dequant_cache: bool = True, **kw):
         super().__init__(*a, **kw)
+        self.prefill_dequant_cache = prefill_dequant_cache
         if moe_parallel not in ("tp", "ep"):
             raise ValueError(f"moe_parallel must be 'tp' or 'ep', got {moe_parallel!r}")
         self.fp8 = fp8
@@ -76,12 +77,20 @@ class MixtralModel(DecoderModel):
                 q, s = moe_ops.quantize_fp8_rowwise(w)
                 self.w[k + "_t"] = moe_ops.tile_fp8_weight(q)
                 self.w[k + "_scale"] = s.float().contiguous()
+                if self.prefill_dequant_cache:
+                    # the SAME quantized values in bf16 for the prefill GEMMs (hipBLASLt): ~90 GB for
+                    # 8x7B -- HBM3E has it, and prefill stops re-dequantizing 2.8 GB per layer per step
+                    self.w[k + "_deq"] = moe_ops.dequant_fp8(q, s, self.dtype)
+                del q, w
         self.fp8 = True
         if self.device.type == "cuda":
             torch.cuda.empty_cache()   # return the bf16 experts to the pool before KV planning
 
     def _dequant(self, p: str, key: str, e: int) -> torch.Tensor:
-        """One expert's fp8 tiles -> [rows, cols] in the compute dtype (prefill path)."""
+        """One expert's fp8 weights -> [rows, cols] in the compute dtype (prefill path)."""
+        cached = self.w.get(p + key + "_deq")
+        if cached is not None:
+            return cached[e]
         q = moe_ops.untile_fp8_weight(self.w[p + key + "_t"][e:e + 1])[0]
         return moe_ops.dequant_fp8(q, self.w[p + key + "_scale"][e], self.dtype)
 
@@ -108,7 +117,10 @@ class MixtralModel(DecoderModel):
         if self.ep:
             return ep_moe(h, logits, c.top_k_experts, c.num_experts, lambda rows, e: self._expert(p, rows, e),
                           group=pstate().tp_group)
-        if self.fp8 and ops._native.use_native(h) and T * c.top_k_experts <= 4096:
+        # fp8 MFMA pipeline while the step is weight-bandwidth-bound; bigger prefill chunks go to
+        # hipBLASLt on the cached bf16 copy of the same quantized experts (compute-bound regime)
+        fp8_limit = 1024 if self.prefill_dequant_cache else 4096
+        if self.fp8 and ops._native.use_native(h) and T * c.top_k_experts <= fp8_limit:
             out = moe_ops.moe_decode_fp8(h.contiguous(), logits.contiguous(), self.w[p + "w13_t"],
                                          self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
                                          c.top_k_experts, self._moe_workspace(T))
