@@ -200,6 +200,54 @@ def bench_skinny(dev) -> List[Dict]:
     return out
 
 
+def bench_splitk(dev) -> List[Dict]:
+    """Mid-batch split-K GEMM (+ slab reduce) vs hipBLASLt on the Llama-3-8B decode projections.
+
+    Weights rotate over enough copies (>= 768 MB) that every call streams W from HBM, not from
+    the 256 MB Infinity Cache -- the situation of a 32-layer decode step."""
+    from ..ops import gemm
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
+    for name, (N, K) in shapes.items():
+        copies = max(2, (768 << 20) // (N * K * 2))
+        ws = [torch.randn((N, K), device=dev).to(torch.bfloat16) for _ in range(copies)]
+        wts = [gemm.tile_weight(w) for w in ws]
+        it = [0]
+
+        def nxt():
+            it[0] = (it[0] + 1) % copies
+            return it[0]
+
+        for M in (16, 32, 48, 64, 96, 128, 192, 256):
+            x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+            wbytes = N * K * 2
+            base = timeit(lambda: torch.nn.functional.linear(x, ws[nxt()]), iters=copies * 2)
+            row = {"op": "splitk", "name": name, "M": M, "hipblaslt_us": round(base, 1),
+                   "hipblaslt_GBps": round(wbytes / base / 1e3, 1)}
+            best = None
+            for S in (1, 2, 4, 7, 8):
+                for nf in (2, 4, 8):
+                    if K % (64 * S) or N % (16 * nf):
+                        continue
+                    P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                    us = timeit(lambda: gemm.splitk_partials(x, wts[nxt()], N, S, nf, out=P), iters=copies * 2)
+                    y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+                    red = timeit(lambda: gemm.splitk_reduce(P, out=y), iters=20)
+                    row[f"s{S}nf{nf}_us"] = round(us, 1)
+                    row[f"s{S}nf{nf}_red_us"] = round(red, 1)
+                    if best is None or us + red < best[1]:
+                        best = ((S, nf), us + red, us)
+            row["best"] = list(best[0])
+            row["best_gemm_us"] = round(best[2], 1)
+            row["best_total_us"] = round(best[1], 1)
+            row["best_gemm_GBps"] = round(wbytes / best[2] / 1e3, 1)
+            row["speedup_total"] = round(base / best[1], 2)
+            out.append(row)
+        del ws, wts
+        torch.cuda.empty_cache()
+    return out
+
+
 def bench_moe(dev) -> List[Dict]:
     """Mixtral-8x7B MoE layer (E=8, top-2, H=4096, F=14336): HIP fp8 pipeline vs bf16 per-expert
     hipBLASLt GEMMs (the eager bucketed path)."""
@@ -251,7 +299,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "moe": bench_moe}[name](dev)
+                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk, "moe": bench_moe}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

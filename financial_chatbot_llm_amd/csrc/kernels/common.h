@@ -45,6 +45,22 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return p.u;
 }
 
+// 8 consecutive outputs of a split-K GEMM (gemm_splitk.hip): the sum of its S f32 slabs (slab
+// stride `ss` floats), rounded to bf16 exactly where the unsplit GEMM would round its output.
+__device__ __forceinline__ void load8_slabs(const float* __restrict__ p, int S, long ss, float* o) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll 4
+  for (int s = 1; s < S; ++s) {
+    a += *reinterpret_cast<const f32x4*>(p + s * ss);
+    b += *reinterpret_cast<const f32x4*>(p + s * ss + 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (float)(bf16)a[j];
+    o[4 + j] = (float)(bf16)b[j];
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

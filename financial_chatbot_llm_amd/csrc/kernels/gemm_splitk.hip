@@ -1,0 +1,256 @@
+// Mid-batch decode projection GEMM (K3/K8/K10 at 32 < M <= 256 tokens): f32 split-K slabs
+//   P[s, m, n] = sum_{k in slice s} X[m, k] * W[n, k]        (Y = sum_s P[s] is reduced by the consumer)
+//
+// Why not hipBLASLt here: at M = 64..256 the QKV / O / down projections are still weight streams
+// (33-117 MB of W against <= 7 MB of X) but the library runs them at 1.7-2.6 TB/s -- its tiles
+// leave most CUs idle at N = 4096-6144 or re-read X per narrow tile.  This kernel is shaped for
+// the stream instead:
+//   * one workgroup = 4 waves owns BN = 16*NF rows of W and one K slice (split-K over the grid, S
+//     slices) so N = 4096 still launches >= 256 workgroups; slice s = blockIdx.x % S keeps each
+//     XCD on 8/S K slices, so X's L2 footprint per XCD is X/S (down-proj X is 7 MB at M = 256);
+//   * BOTH operands stream into LDS with global_load_lds (16 B per lane, 1-KiB lane-linear pieces):
+//     W from its MFMA-fragment-tiled copy (ops/gemm.py tile_weight -- each piece IS one A
+//     fragment), X in full 128-B lines (8 token rows x 64 k per piece) with an XOR-swizzled image
+//     chosen on the SOURCE address so the 16-lane phases of the fragment reads are conflict-free;
+//     X is fetched once per workgroup and shared by its 4 waves (X/W on-chip traffic = M/BN);
+//   * NBUF-deep ring (3-8, what fits in LDS) of BK = 64 stages, counted `s_waitcnt vmcnt` + one raw s_barrier per stage (no
+//     vmcnt(0) drain in the steady state, no VGPR-destination loads in the loop at all);
+//   * waves split the (W rows x tokens) tile WA x WB; v_mfma_f32_16x16x32_bf16, f32 accumulate;
+//   * the epilogue writes the f32 partial tile (16-B stores); no in-launch reduction -- the next
+//     kernel that reads Y anyway (residual-add+RMSNorm, RoPE/KV-write, or penny_splitk_reduce)
+//     sums the S slabs, which costs S*4 B per output instead of a 1.5-2 us kernel boundary.
+#include "common.h"
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void vmcnt_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+union Frag {
+  uint4 u;
+  bf16x8 v;
+};
+
+// X image: token row r of a stage lives at byte r*128; its logical 16-B chunk c (k = 8c..8c+7) at
+// physical chunk c ^ (r & 7) ^ ((r >> 3) & 1).  A fragment read (16 consecutive rows, one logical
+// chunk) then touches 16 distinct (row parity, chunk) bank groups per 16-lane phase.
+__device__ __forceinline__ int xswz(int r, int c) { return c ^ (r & 7) ^ ((r >> 3) & 1); }
+
+// stage ring depth: as many BK=64 stages as fit in ~150 KB of LDS (one workgroup per CU), capped
+// at 8 -- a CU must keep ~50-70 KB of W in flight to stream its 1/256 share of HBM bandwidth
+template <int NF, int MT>
+struct Ring {
+  static constexpr int SBYTES = (NF + MT) * 2 * 1024;
+  static constexpr int NBUF = (150 * 1024 / SBYTES) < 8 ? (150 * 1024 / SBYTES) : 8;
+};
+
+// wait until at most `younger` stages of this wave's glds are still in flight, then barrier
+template <int LOADS, int MAXY>
+__device__ __forceinline__ void wait_stage(int younger) {
+  if constexpr (MAXY <= 0) {
+    vmcnt_barrier<0>();
+  } else {
+    if (younger >= MAXY) vmcnt_barrier<MAXY * LOADS>();
+    else wait_stage<LOADS, MAXY - 1>(younger);
+  }
+}
+
+// MFMAs of one BK=64 stage.  `base` is __restrict__ ON PURPOSE: inlined, it gives the ds_reads
+// alias-scope metadata, which is what lets hipcc's waitcnt pass leave the younger stages' LDS-DMA
+// in flight -- without it the pass cannot tell them apart from this stage and drains vmcnt(0)
+// before the first ds_read of every stage (measured: the ring then degenerates to one stage).
+template <int FW, int TW, int WBYTES>
+__device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (&acc)[FW][TW], int wa, int wb,
+                                          int lane, int g, int col) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    Frag wf[FW], xf[TW];
+#pragma unroll
+    for (int f = 0; f < FW; ++f)
+      wf[f].u = *reinterpret_cast<const uint4*>(base + ((wa * FW + f) * 2 + kk) * 1024 + lane * 16);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int r = (wb * TW + t) * 16 + col;
+      xf[t].u = *reinterpret_cast<const uint4*>(base + WBYTES + r * 128 + xswz(r, 4 * kk + g) * 16);
+    }
+#pragma unroll
+    for (int f = 0; f < FW; ++f)
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+        acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f].v, xf[t].v, acc[f][t], 0, 0, 0);
+  }
+}
+
+template <int NF, int MT, int WA>
+__global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restrict__ X, int ldx,
+                                                             const bf16* __restrict__ Wt, int K,
+                                                             float* __restrict__ P, int M, int N, int S) {
+  constexpr int WB = 4 / WA;
+  constexpr int FW = NF / WA;   // W row groups per wave
+  constexpr int TW = MT / WB;   // token tiles per wave
+  static_assert(NF % WA == 0 && MT % WB == 0, "wave split");
+  constexpr int NBUF = Ring<NF, MT>::NBUF;
+  static_assert(NBUF >= 3, "ring too shallow");
+  constexpr int WBYTES = NF * 2 * 1024;        // W pieces of one BK=64 stage
+  constexpr int XBYTES = MT * 2 * 1024;        // X pieces (16*MT rows x 128 B)
+  constexpr int SBYTES = WBYTES + XBYTES;
+  constexpr int PIECES = (2 * NF + 2 * MT);     // 1-KiB pieces per stage
+  static_assert(PIECES % 4 == 0, "pieces must split evenly over 4 waves");
+  constexpr int LOADS = PIECES / 4;             // glds per wave per stage
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * SBYTES];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
+  const int s = blockIdx.x % S, tile = blockIdx.x / S;
+  const int n0 = tile * 16 * NF;
+  const int kc = K / S, k0 = s * kc;
+  const int nst = kc / 64;
+  const int ksteps = K / 32;
+  const int wa = w / WB, wb = w % WB;
+
+  // per-lane glds source for each of this wave's pieces (fixed per kernel; advanced by k per stage)
+  // piece id q = w*LOADS + i:  q < 2*NF -> W (row group q/2, k-step q%2), else X rows 8*(q-2NF)..
+  const char* src[LOADS];
+  int dst[LOADS];
+  long step[LOADS];
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int q = w * LOADS + i;
+    if (q < 2 * NF) {
+      const int f = q >> 1, kk = q & 1;
+      src[i] = reinterpret_cast<const char*>(Wt) +
+               (((long)(n0 / 16 + f) * ksteps + k0 / 32 + kk) * 64 + lane) * 16;
+      step[i] = 2 * 1024;  // two k-steps of one row group per stage
+      dst[i] = (f * 2 + kk) * 1024;
+    } else {
+      const int xp = q - 2 * NF;
+      const int r = xp * 8 + (lane >> 3);                 // token row within the tile
+      const int c = xswz(r, lane & 7);                    // logical chunk this lane's slot holds
+      const int row = min(r, M - 1);
+      src[i] = reinterpret_cast<const char*>(X + (long)row * ldx + k0 + 8 * c);
+      step[i] = 128;  // 64 bf16 per stage
+      dst[i] = WBYTES + xp * 1024;
+    }
+  }
+  auto stage = [&](int j) {
+    char* base = smem + (j % NBUF) * SBYTES;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      if (w * LOADS + i < 2 * NF)  // weights are read once per decode step: non-temporal (aux = nt)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 2);
+      else
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[FW][TW];
+#pragma unroll
+  for (int f = 0; f < FW; ++f)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < nst) stage(j);
+
+  for (int j = 0; j < nst; ++j) {
+    // stages j+1 .. min(j+NBUF-2, nst-1) may stay in flight
+    wait_stage<LOADS, NBUF - 2>(min(NBUF - 2, nst - 1 - j));
+    if (j + NBUF - 1 < nst) stage(j + NBUF - 1);
+    stage_mma<FW, TW, WBYTES>(smem + (j % NBUF) * SBYTES, acc, wa, wb, lane, g, col);
+  }
+
+  // lane holds W rows n = 16f + 4g + r (r = 0..3) for token 16t + col: one 16-B store per tile
+  float* ps = P + (long)s * M * N;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int m = (wb * TW + t) * 16 + col;
+    if (m >= M) continue;
+#pragma unroll
+    for (int f = 0; f < FW; ++f) {
+      const int n = n0 + (wa * FW + f) * 16 + 4 * g;
+      *reinterpret_cast<f32x4*>(ps + (long)m * N + n) = acc[f][t];
+    }
+  }
+}
+
+// Y[m, n] = bf16(sum_s P[s, m, n]) (+ R[m, n], rounded like the unfused GEMM-then-add path)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
+                                                            bf16* __restrict__ Y, int ldy,
+                                                            const bf16* __restrict__ R, int ldr) {
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;  // index of 8 outputs
+  const long total8 = (long)M * N / 8;
+  if (i8 >= total8) return;
+  const int m = (int)(i8 / (N / 8));
+  const int n = (int)(i8 % (N / 8)) * 8;
+  float o[8];
+  {
+    const f32x4* p = reinterpret_cast<const f32x4*>(P + (long)m * N + n);
+    const f32x4 a = p[0], b = p[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = a[j], o[4 + j] = b[j];
+  }
+  for (int s = 1; s < S; ++s) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(P + ((long)s * M + m) * N + n);
+    const f32x4 a = p[0], b = p[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] += a[j], o[4 + j] += b[j];
+  }
+  if (R) {
+    float r[8];
+    unpack8(*reinterpret_cast<const uint4*>(R + (long)m * ldr + n), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)(bf16)o[j] + r[j];
+  }
+  *reinterpret_cast<uint4*>(Y + (long)m * ldy + n) = pack8(o);
+}
+
+template <int NF, int MT, int WA>
+int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, hipStream_t st) {
+  hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
+                     (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
+// aligned (ldx % 8 == 0).  nf: W row groups per workgroup (2, 4 or 8).  P is [S, M, N] f32.
+PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
+                                hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 256 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
+    return (int)hipErrorInvalidValue;
+  const int mt = (M + 15) / 16;
+  float* p = static_cast<float*>(P);
+#define SK_CASE(MT_, WA2_, WA4_, WA8_)                                                 \
+  if (mt <= MT_) {                                                                     \
+    if (nf == 2) return launch<2, MT_, WA2_>(X, ldx, Wt, K, p, M, N, S, stream);       \
+    if (nf == 4) return launch<4, MT_, WA4_>(X, ldx, Wt, K, p, M, N, S, stream);       \
+    return launch<8, MT_, WA8_>(X, ldx, Wt, K, p, M, N, S, stream);                    \
+  }
+  // (NF + MT) even; wave split picked to minimise fragment reads per wave (NF/WA + MT/WB)
+  SK_CASE(2, 2, 2, 2)
+  SK_CASE(4, 1, 1, 2)
+  SK_CASE(6, 2, 2, 2)
+  SK_CASE(8, 1, 1, 2)
+  SK_CASE(12, 1, 1, 2)
+  SK_CASE(16, 1, 1, 2)
+#undef SK_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+PENNY_API int penny_splitk_reduce(const void* P, int S, int M, int N, void* Y, int ldy, const void* R, int ldr,
+                                  hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % 8 || ldy % 8 || (R && ldr % 8)) return (int)hipErrorInvalidValue;
+  const long total8 = (long)M * N / 8;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, stream,
+                     (const float*)P, S, M, N, (bf16*)Y, ldy, (const bf16*)R, ldr);
+  return (int)hipGetLastError();
+}

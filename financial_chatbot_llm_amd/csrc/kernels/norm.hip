@@ -10,10 +10,14 @@
 //   add_ln:   r = x + res (f32); y = ln(r)                     (BERT post-LN: LN(x + sublayer(x)))
 #include "common.h"
 
-template <int CPT, bool ADD_RES>
+// SLAB: x is not a bf16 tensor but the S f32 split-K slabs [S, T, H] of the producing GEMM
+// (gemm_splitk.hip); summing them here IS that GEMM's reduction, fused into the norm's row pass
+// (one workgroup per row keeps >= T workgroups in flight for the extra slab reads).
+template <int CPT, bool ADD_RES, bool SLAB>
 __global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ res,
                                                        const bf16* __restrict__ w, bf16* __restrict__ y,
-                                                       int H, float eps) {
+                                                       int H, float eps, const float* __restrict__ P, int S,
+                                                       int T) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nchunk = H >> 3;
@@ -25,7 +29,8 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(const bf16* __restrict__ 
   for (int c = 0; c < CPT; ++c) {
     const int idx = threadIdx.x + c * blockDim.x;
     if (idx < nchunk) {
-      unpack8(xr[idx], v[c]);
+      if (SLAB) load8_slabs(P + (size_t)row * H + 8 * idx, S, (long)T * H, v[c]);
+      else unpack8(xr[idx], v[c]);
       if (ADD_RES) {
         float r[8];
         unpack8(rr[idx], r);
@@ -204,11 +209,28 @@ PENNY_API int penny_rmsnorm(const void* x, void* res, const void* w, void* y, in
   int threads, cpt;
   pick_geometry(H, &threads, &cpt);
   if (add_residual) {
-    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, true>), dim3(T), dim3(threads), 0, stream,
-                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps));
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, true, false>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps, nullptr, 0, T));
   } else {
-    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, false>), dim3(T), dim3(threads), 0, stream,
-                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps));
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, false, false>), dim3(T), dim3(threads), 0, stream,
+                                         (const bf16*)x, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps, nullptr, 0, T));
+  }
+  PENNY_RETURN_LAUNCH();
+}
+
+// x given as the S split-K slabs P [S, T, H] f32 of the producing GEMM (see rmsnorm_kernel SLAB)
+PENNY_API int penny_rmsnorm_slabs(const void* P, int S, void* res, const void* w, void* y, int T, int H, float eps,
+                                  int add_residual, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 || S < 1) return (int)hipErrorInvalidValue;
+  int threads, cpt;
+  pick_geometry(H, &threads, &cpt);
+  if (add_residual) {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, true, true>), dim3(T), dim3(threads), 0, stream,
+                                         nullptr, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps, (const float*)P, S, T));
+  } else {
+    DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, false, true>), dim3(T), dim3(threads), 0, stream,
+                                         nullptr, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps, (const float*)P, S, T));
   }
   PENNY_RETURN_LAUNCH();
 }

@@ -14,11 +14,13 @@
 #include "common.h"
 #include "kv_layout.h"
 
-template <int D>
+// SLAB: the QKV activation arrives as the S f32 split-K slabs [S, T, width] of the QKV GEMM
+// (gemm_splitk.hip) and is reduced here, in the same pass that rotates and scatters it.
+template <int D, bool SLAB>
 __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restrict__ positions,
                                const float* __restrict__ cos_sin, const int* __restrict__ slots,
                                bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
-                               int Hq, int Hkv, int apply_rope) {
+                               int Hq, int Hkv, int apply_rope, const float* __restrict__ P, int S, int T) {
   constexpr int HALF = D / 2;
   constexpr int RU = HALF / 8;  // rotary units per head (8 pairs each)
   constexpr int VU = D / 8;     // copy units per v head
@@ -27,6 +29,11 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
   const int slot = slots[t];
   const int width = (Hq + 2 * Hkv) * D;
   const bf16* row = qkv + (long)t * width;
+  const float* prow = SLAB ? P + (long)t * width : nullptr;
+  auto load8 = [&](int c0, float* o) {  // 8 activations starting at column c0 of this token's row
+    if constexpr (SLAB) load8_slabs(prow + c0, S, (long)T * width, o);
+    else unpack8(*reinterpret_cast<const uint4*>(row + c0), o);
+  };
   const float* cs = cos_sin + (long)pos * D;
   const int n_rot = (Hq + Hkv) * RU;
   const int total = n_rot + Hkv * VU;
@@ -35,10 +42,9 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
   for (int u = threadIdx.x; u < total; u += blockDim.x) {
     if (u < n_rot) {
       const int h = u / RU, c = u % RU;
-      const bf16* src = row + h * D;
       float x1[8], x2[8];
-      unpack8(*reinterpret_cast<const uint4*>(src + c * 8), x1);
-      unpack8(*reinterpret_cast<const uint4*>(src + HALF + c * 8), x2);
+      load8(h * D + c * 8, x1);
+      load8(h * D + HALF + c * 8, x2);
       if (apply_rope) {
         float co[8], si[8];   // 4 x 16-B loads instead of 16 scalar loads
         *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
@@ -66,28 +72,45 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
     } else if (slot >= 0) {
       const int v = u - n_rot;
       const int h = v / VU, c = v % VU;
-      Pack8 p;
-      p.u = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + h) * D + c * 8);
+      float x[8];
+      load8((Hq + Hkv + h) * D + c * 8, x);
       bf16* base = v_cache + (blk * Hkv + h) * (long)(KV_BS * D);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) base[v_index(off, c * 8 + i, D)] = p.e[i];
+      for (int i = 0; i < 8; ++i) base[v_index(off, c * 8 + i, D)] = (bf16)x[i];
     }
   }
+}
+
+template <bool SLAB>
+static int launch_rope_kv(const void* qkv, const float* P, int S, const int* positions, const float* cos_sin,
+                          const int* slots, void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
+                          int apply_rope, hipStream_t stream) {
+  if (T <= 0) return 0;
+  const int threads = 256;
+  if (D == 128) {
+    hipLaunchKernelGGL((rope_kv_kernel<128, SLAB>), dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions,
+                       cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope, P, S, T);
+  } else if (D == 64) {
+    hipLaunchKernelGGL((rope_kv_kernel<64, SLAB>), dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions,
+                       cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope, P, S, T);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
 }
 
 PENNY_API int penny_rope_kv_write(const void* qkv, const int* positions, const float* cos_sin, const int* slots,
                                   void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
                                   int apply_rope, hipStream_t stream) {
-  if (T <= 0) return 0;
-  const int threads = 256;
-  if (D == 128) {
-    hipLaunchKernelGGL(rope_kv_kernel<128>, dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions, cos_sin,
-                       slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope);
-  } else if (D == 64) {
-    hipLaunchKernelGGL(rope_kv_kernel<64>, dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions, cos_sin,
-                       slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope);
-  } else {
-    return (int)hipErrorInvalidValue;
-  }
-  PENNY_RETURN_LAUNCH();
+  return launch_rope_kv<false>(qkv, nullptr, 0, positions, cos_sin, slots, q_out, k_cache, v_cache, T, Hq, Hkv, D,
+                               apply_rope, stream);
+}
+
+// qkv given as the S split-K slabs P [S, T, (Hq + 2*Hkv) * D] f32 of the QKV GEMM
+PENNY_API int penny_rope_kv_write_slabs(const void* P, int S, const int* positions, const float* cos_sin,
+                                        const int* slots, void* q_out, void* k_cache, void* v_cache, int T, int Hq,
+                                        int Hkv, int D, int apply_rope, hipStream_t stream) {
+  if (S < 1) return (int)hipErrorInvalidValue;
+  return launch_rope_kv<true>(nullptr, (const float*)P, S, positions, cos_sin, slots, q_out, k_cache, v_cache, T, Hq,
+                              Hkv, D, apply_rope, stream);
 }

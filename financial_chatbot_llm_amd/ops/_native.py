@@ -27,12 +27,16 @@ P = c_void_p
 
 _SIGS = {
     "penny_rmsnorm": [P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "penny_rmsnorm_slabs": [P, c_int, P, P, P, c_int, c_int, c_float, c_int, P],
     "penny_layernorm": [P, P, P, P, P, c_int, c_int, c_float, c_int, P],
     "penny_silu_mul": [P, P, c_int, c_int, c_int, P],
     "penny_skinny_gemm": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_splitk_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P],
+    "penny_splitk_reduce": [P, c_int, c_int, c_int, P, c_int, P, c_int, P],
     "penny_gelu": [P, c_long, P],
     "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_rope_kv_write_slabs": [P, c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P],
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from .gemm import Slabs
 
 KV_BS = 64
 
@@ -101,7 +102,17 @@ def write_kv_ref(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache:
 def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
                   slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, Hq: int, Hkv: int,
                   D: int, apply_rope: bool = True) -> torch.Tensor:
-    """Rotate q/k of a fused QKV activation, write k/v into the paged cache, return q [T,Hq,D]."""
+    """Rotate q/k of a fused QKV activation, write k/v into the paged cache, return q [T,Hq,D].
+    ``qkv`` may be the unreduced :class:`~.gemm.Slabs` of the split-K QKV GEMM (summed here)."""
+    if isinstance(qkv, Slabs):
+        S, T, _ = qkv.P.shape
+        if N.use_native(qkv.P):
+            q = torch.empty((T, Hq, D), dtype=torch.bfloat16, device=qkv.P.device)
+            N.call("penny_rope_kv_write_slabs", N.ptr(qkv.P), S, N.ptr(positions),
+                   N.ptr(cos_sin) if apply_rope else None, N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache),
+                   T, Hq, Hkv, D, int(apply_rope), N.stream())
+            return q
+        qkv = qkv.materialize()
     T = qkv.shape[0]
     if N.use_native(qkv):
         q = torch.empty((T, Hq, D), dtype=qkv.dtype, device=qkv.device)

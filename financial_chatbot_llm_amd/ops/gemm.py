@@ -13,7 +13,7 @@ measured on MI355X with ``bench/kernels.py --only skinny`` -- with a heuristic f
 from __future__ import annotations
 
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple, Union
 
 import torch
 import torch.nn.functional as F
@@ -63,13 +63,20 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
-           residual: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+           residual: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
+           slabs: bool = False) -> Union[torch.Tensor, "Slabs"]:
     """y = x @ w.T with an optional fused epilogue ("silu": w is gate|up 16-interleaved).
 
     ``wt`` is the fragment-tiled copy of ``w`` (``tile_weight``); when given, decode-sized
-    batches (M <= 64) run the hand-written MFMA kernel on it."""
+    batches run the hand-written MFMA kernels on it.  ``slabs=True`` lets the caller receive the
+    split-K GEMM's unreduced :class:`Slabs` (the consumer -- ``ops.rms_norm`` /
+    ``ops.rope_kv_write`` -- sums them in its own pass)."""
     M, K = x.shape
     N_ = w.shape[0]
+    if slabs and wt is not None and epilogue is None and residual is None:
+        cfg = splitk_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
+        if cfg is not None:
+            return Slabs(splitk_partials(x, wt, N_, *cfg))
     if skinny_ok(x, w, epilogue, wt):
         ntf, nw = _config(N_, K, epilogue)
         out_n = N_ // 2 if epilogue == "silu" else N_
@@ -121,3 +128,84 @@ def load_gemm_tuning(model: str, tp: int = 1) -> Optional[str]:
     tun.enable(True)
     _LOADED_TUNING = path
     return path
+
+
+# ----------------------------------------------------------------------------------------------
+# Mid-batch decode GEMM (32 < M <= 256): split-K f32 slabs, reduced by the consumer
+# ----------------------------------------------------------------------------------------------
+# (N, K) -> [(max M, S, nf), ...] for the split-K kernel, measured on MI355X against hipBLASLt with
+# the weights streamed from HBM (bench/kernels.py --only splitk, profiles/r1_splitk_v3.jsonl),
+# choosing by GEMM time + the consumer's extra slab read (S*M*N*4 B at ~5 TB/s).  Llama-3-8B:
+# QKV 1.3-1.6x, O 1.5-2.2x, down 1.4-2.8x faster than the library at M = 16..192.
+SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
+    (6144, 4096): [(16, 2, 2), (32, 2, 4), (256, 4, 8)],     # QKV
+    (4096, 4096): [(192, 4, 4)],                             # O (M=256: hipBLASLt is faster)
+    (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
+}
+
+
+def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
+    """(S, nf) for a split-K launch of this shape, or None.  ``PENNY_SPLITK=0`` disables the
+    path; ``PENNY_SPLITK=force`` takes it for any shape the kernel accepts (tests)."""
+    mode = os.environ.get("PENNY_SPLITK", "1")
+    if mode == "0" or M > 256:
+        return None
+    for max_m, S, nf in SPLITK.get((N_, K), ()):
+        if M <= max_m:
+            return S, nf
+    if mode == "force":
+        nf = 4 if N_ % 64 == 0 else 2
+        for S in (4, 2, 1):
+            if K % (64 * S) == 0 and N_ % (16 * nf) == 0:
+                return S, nf
+    return None
+
+
+class Slabs:
+    """A split-K GEMM output left unreduced: f32 partial sums ``P`` [S, M, N].  Consumers that
+    read the activation anyway (``ops.rms_norm``, ``ops.rope_kv_write``) sum the slabs inside
+    their own row pass; anything else calls :meth:`materialize`."""
+
+    __slots__ = ("P",)
+
+    def __init__(self, P: torch.Tensor):
+        self.P = P
+
+    @property
+    def shape(self) -> Tuple[int, int]:
+        return (self.P.shape[1], self.P.shape[2])
+
+    def materialize(self) -> torch.Tensor:
+        return splitk_reduce(self.P)
+
+
+def splitk_partials(x: torch.Tensor, wt: torch.Tensor, N_: int, S: int, nf: int,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """P[s] = x @ w[:, slice s].T as f32 slabs [S, M, N] (``wt`` = ``tile_weight(w)``)."""
+    M, K = x.shape
+    if not N.use_native(x):
+        w = untile_weight(wt).float()
+        xs = x.float().view(M, S, K // S).transpose(0, 1)
+        return torch.einsum("smk,snk->smn", xs, w.view(N_, S, K // S).transpose(0, 1))
+    P = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
+    N.call("penny_splitk_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(P), M, N_, S, nf, N.stream())
+    return P
+
+
+def splitk_reduce(P: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Y = bf16(sum_s P[s]) (+ residual)."""
+    S, M, N_ = P.shape
+    if not N.use_native(P):
+        y = P.sum(0).to(torch.bfloat16)
+        return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
+    y = out if out is not None else torch.empty((M, N_), dtype=torch.bfloat16, device=P.device)
+    N.call("penny_splitk_reduce", N.ptr(P), S, M, N_, N.ptr(y), y.stride(0), N.ptr(residual),
+           residual.stride(0) if residual is not None else 0, N.stream())
+    return y
+
+
+def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``tile_weight``: [N/16, K/32, 64, 8] -> [N, K]."""
+    G, KS = wt.shape[0], wt.shape[1]
+    return wt.view(G, KS, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(G * 16, KS * 32)

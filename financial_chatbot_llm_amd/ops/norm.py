@@ -1,11 +1,12 @@
 """K2/K14 normalisation ops: fused residual-add + RMSNorm, residual-add + LayerNorm."""
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Optional, Tuple, Union
 
 import torch
 
 from . import _native as N
+from .gemm import Slabs
 
 
 def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
@@ -14,10 +15,19 @@ def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     return (y.float() * w.float()).to(x.dtype)
 
 
-def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+def rms_norm(x: Union[torch.Tensor, Slabs], w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
              out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``residual is None``: y = rms(x).  Otherwise residual <- x + residual (in place, bf16) and
-    y = rms(residual) -- the Llama pre-norm pattern, one HBM pass."""
+    y = rms(residual) -- the Llama pre-norm pattern, one HBM pass.  ``x`` may be the unreduced
+    :class:`~.gemm.Slabs` of a split-K GEMM: the slabs are summed in the same pass."""
+    if isinstance(x, Slabs):
+        S, T, H = x.P.shape
+        if N.use_native(x.P):
+            out = torch.empty((T, H), dtype=torch.bfloat16, device=x.P.device) if out is None else out
+            N.call("penny_rmsnorm_slabs", N.ptr(x.P), S, N.ptr(residual), N.ptr(w), N.ptr(out), T, H, float(eps),
+                   int(residual is not None), N.stream())
+            return out
+        x = x.materialize()
     H = x.shape[-1]
     T = x.numel() // H
     if N.use_native(x):

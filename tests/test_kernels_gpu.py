@@ -227,6 +227,62 @@ def test_skinny_gemm(M, cfg):
         gemm.TUNING.pop((N_, K), None)
 
 
+@pytest.mark.parametrize("M", [5, 33, 64, 90, 128, 200, 256])
+@pytest.mark.parametrize("S,nf", [(1, 4), (2, 8), (4, 4), (8, 8), (2, 2)])
+def test_splitk_gemm(M, S, nf):
+    """Mid-batch split-K GEMM (f32 slabs) + slab reduce (+ residual) vs the fp32 reference."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(11)
+    N_, K = 256, 2048
+    x = rnd(M, K, gen=g)
+    w = rnd(N_, K, scale=0.05, gen=g)
+    res = rnd(M, N_, gen=g)
+    wt = gemm.tile_weight(w.to(DEV))
+    P = gemm.splitk_partials(x.to(DEV), wt, N_, S, nf)
+    ref_p = (x.float().view(M, S, K // S).transpose(0, 1) @ w.float().view(N_, S, K // S).permute(1, 2, 0))
+    close(P, ref_p, atol=1e-3)
+    close(gemm.splitk_reduce(P), x.float() @ w.float().t(), atol=2e-2)
+    close(gemm.splitk_reduce(P, residual=res.to(DEV)), x.float() @ w.float().t() + res.float(), atol=3e-2)
+    # strided X (a view into a wider activation buffer) is a supported input
+    xw = torch.zeros(M, K + 64, dtype=torch.bfloat16)
+    xw[:, 32:32 + K] = x
+    P2 = gemm.splitk_partials(xw.to(DEV)[:, 32:32 + K], wt, N_, S, nf)
+    close(P2, ref_p, atol=1e-3)
+
+
+@pytest.mark.parametrize("S,T", [(1, 3), (4, 128), (8, 200)])
+def test_slab_consumers_match_reduce_then_op(S, T):
+    """RMSNorm (+residual) and RoPE/KV-write fed the split-K slabs directly equal the same kernels
+    fed the reduced bf16 activation -- the fused reduction rounds exactly where the GEMM would."""
+    from financial_chatbot_llm_amd.ops.gemm import Slabs, splitk_reduce
+    g = torch.Generator().manual_seed(12)
+    H = 4096
+    P = (torch.randn(S, T, H, generator=g) * 0.3).to(DEV)
+    w = (rnd(H, scale=0.1, gen=g) + 1).to(DEV)
+    res = rnd(T, H, gen=g).to(DEV)
+    r1, r2 = res.clone(), res.clone()
+    y1 = ops.rms_norm(Slabs(P), w, 1e-5, residual=r1)
+    y2 = ops.rms_norm(splitk_reduce(P), w, 1e-5, residual=r2)
+    close(y1, y2, atol=1e-6, rtol=0)
+    close(r1, r2, atol=0, rtol=0)
+    close(ops.rms_norm(Slabs(P), w, 1e-5), ops.rms_norm(splitk_reduce(P), w, 1e-5), atol=1e-6, rtol=0)
+    Hq, Hkv, D = 32, 8, 128
+    W = (Hq + 2 * Hkv) * D
+    Pq = (torch.randn(S, T, W, generator=g) * 0.3).to(DEV)
+    pos = torch.randint(0, 4000, (T,), generator=g, dtype=torch.int32).to(DEV)
+    cs = ops.rope_cos_sin(D, 4096, 500000.0).to(DEV)
+    nblk = (T + KV_BS - 1) // KV_BS + 1
+    slots = torch.randperm(nblk * KV_BS, generator=g)[:T].to(torch.int32).to(DEV)
+    kc1, vc1 = (torch.zeros(nblk, Hkv, KV_BS * D, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    q1 = ops.rope_kv_write(Slabs(Pq), pos, cs, slots, kc1, vc1, Hq, Hkv, D)
+    q2 = ops.rope_kv_write(splitk_reduce(Pq), pos, cs, slots, kc2, vc2, Hq, Hkv, D)
+    # q/k: the rotation's FMA contraction may differ between the two instantiations -> 1 bf16 ulp
+    close(q1, q2, atol=1e-6, rtol=2 ** -7)
+    close(kc1, kc2, atol=1e-6, rtol=2 ** -7)
+    close(vc1, vc2, atol=0, rtol=0)
+
+
 def test_silu_mul_interleaved():
     from financial_chatbot_llm_amd.ops import gemm
     g = torch.Generator().manual_seed(10)

@@ -122,3 +122,23 @@ def test_cascade_plan_groups_shared_prefix_blocks():
     CascadeInputs.pack(None, buf, 8, 3)
     v = CascadeInputs.views(torch.from_numpy(buf), 8)
     assert int(v.nwork[0]) == 0 and int(v.kv_start.abs().sum()) == 0
+
+
+def test_splitk_slabs_cpu_reference_and_consumers():
+    """CPU path of the split-K op: slabs sum to x @ w.T, and the slab-aware consumers
+    (rms_norm, rope_kv_write) equal the same ops on the reduced activation."""
+    from financial_chatbot_llm_amd import ops
+    from financial_chatbot_llm_amd.ops.gemm import Slabs, splitk_partials, tile_weight, untile_weight
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(128, 256, generator=g).to(torch.bfloat16)
+    assert torch.equal(untile_weight(tile_weight(w)), w)
+    x = torch.randn(9, 256, generator=g).to(torch.bfloat16)
+    P = splitk_partials(x, tile_weight(w), 128, 4, 4)
+    assert P.shape == (4, 9, 128)
+    assert torch.allclose(P.sum(0), x.float() @ w.float().t(), atol=1e-4)
+    nw = torch.ones(128, dtype=torch.bfloat16)
+    r1 = torch.randn(9, 128, generator=g).to(torch.bfloat16)
+    r2 = r1.clone()
+    assert torch.equal(ops.rms_norm(Slabs(P), nw, 1e-5, residual=r1), ops.rms_norm(Slabs(P).materialize(), nw, 1e-5,
+                                                                                   residual=r2))
+    assert torch.equal(r1, r2)
