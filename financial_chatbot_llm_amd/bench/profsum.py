@@ -17,6 +17,7 @@ CLASSES = [
     ("attention-decode", r"decode_kernel|decode_reduce"),
     ("attention-prefill", r"prefill_kernel|prefill2_kernel|cascade_kernel"),
     ("gemm-skinny (HIP)", r"skinny"),
+    ("gemm-splitk (HIP)", r"splitk"),
     ("moe (HIP)", r"moe_|quant_rows"),
     ("gemm (hipBLASLt)", r"^Cijk|^Custom_Cijk|gemm"),
     ("norm/rope/act (HIP)", r"rmsnorm|layernorm|rope_kv|silu_mul|gelu|embedding"),
