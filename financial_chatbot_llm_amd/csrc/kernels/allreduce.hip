@@ -1,4 +1,4 @@
-// C1 (custom path): one-shot all-reduce over xGMI peer-to-peer for decode-size TP messages.
+// C1 (custom path): one-shot / two-shot all-reduce over xGMI peer-to-peer for decode-size TP messages.
 //
 // RCCL's ring all-reduce moves a message through n-1 sequential hops, each bound by ONE xGMI link
 // (~153 GB/s) and each paying a hop latency; a decode step's all-reduce is only a few hundred KB,
@@ -34,6 +34,48 @@ struct ArPeers {
   int* sig[AR_MAX_RANKS];    // each rank's signal area: [AR_MAX_RANKS source][AR_MAX_BLOCKS]
 };
 
+// publish `round` for (region, this rank, this block) in every peer's signal area, after every
+// thread's stores are complete at system scope
+__device__ __forceinline__ void ar_publish(const ArPeers& peers, int region, int rank, int nranks, int round) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < nranks)
+    __hip_atomic_store(peers.sig[threadIdx.x] + (region * AR_MAX_RANKS + rank) * AR_MAX_BLOCKS + blockIdx.x, round,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// wait (bounded) until every peer published `round` for (region, this block), then acquire
+__device__ __forceinline__ void ar_wait(const ArPeers& peers, int region, int rank, int nranks, int round,
+                                        int* err) {
+  if (threadIdx.x < nranks) {
+    const int* slot = peers.sig[rank] + (region * AR_MAX_RANKS + threadIdx.x) * AR_MAX_BLOCKS + blockIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
+      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+}
+
+// out[i..i+7] (or any bf16 destination) <- sum over ranks q = 0..n-1 of peers.data[q][src + i], f32,
+// in fixed rank order on every rank -> bit-identical results across the group and across the
+// one-shot / two-shot forms
+__device__ __forceinline__ uint4 ar_sum8(const ArPeers& peers, int nranks, long src) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < nranks; ++q) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(peers.data[q] + src), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  return pack8(acc);
+}
+
 __global__ void __launch_bounds__(256) ar_oneshot_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
                                                          long n, ArPeers peers, const int* __restrict__ counter,
                                                          int* __restrict__ err, int rank, int nranks,
@@ -46,36 +88,44 @@ __global__ void __launch_bounds__(256) ar_oneshot_kernel(const bf16* __restrict_
   bf16* mine = peers.data[rank] + off;
   for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
     *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
-  __threadfence_system();  // every thread's stores complete (system scope) before the flag
-  __syncthreads();
-  if (threadIdx.x < nranks)
-    __hip_atomic_store(peers.sig[threadIdx.x] + rank * AR_MAX_BLOCKS + blockIdx.x, round, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x < nranks) {
-    const int* slot = peers.sig[rank] + threadIdx.x * AR_MAX_BLOCKS + blockIdx.x;
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
-      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  ar_publish(peers, 0, rank, nranks, round);
+  ar_wait(peers, 0, rank, nranks, round, err);
+  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+    *reinterpret_cast<uint4*>(out + i) = ar_sum8(peers, nranks, off + i);
+}
 
-  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int q = 0; q < nranks; ++q) {
-      // fixed rank order on every rank -> bit-identical results across the group
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(peers.data[q] + off + i), v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
-    }
-    *reinterpret_cast<uint4*>(out + i) = pack8(acc);
-  }
+// Two-shot (reduce-scatter, then all-gather) for mid-size messages on > 2 ranks.  One-shot has
+// every rank read the WHOLE message from every peer ((n-1) x bytes over its links); here rank r
+// reduces only chunk r (1/n of the message from each peer), publishes the reduced chunk in its
+// own buffer, and then every rank gathers the n reduced chunks: 2(n-1)/n x bytes per rank, for
+// one more flag round trip.  Block b owns sub-slice b of every chunk in all three phases, so its
+// flags cover exactly the bytes it reads.  Chunk r of rank r's buffer is read and rewritten only
+// by rank r in the reduce phase, so the reduced chunk can overwrite its input in place.
+__global__ void __launch_bounds__(256) ar_twoshot_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                         long n, ArPeers peers, const int* __restrict__ counter,
+                                                         int* __restrict__ err, int rank, int nranks,
+                                                         long half_elems) {
+  const int round = *counter + 1;
+  const long off = (round & 1) * half_elems;
+  const long chunk = n / nranks;
+  const long per = ((chunk + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
+  const long lo = blockIdx.x * per, hi = min(chunk, lo + per);
+
+  bf16* mine = peers.data[rank] + off;
+  for (int q = 0; q < nranks; ++q)
+    for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+      *reinterpret_cast<uint4*>(mine + q * chunk + i) = *reinterpret_cast<const uint4*>(in + q * chunk + i);
+  ar_publish(peers, 0, rank, nranks, round);
+  ar_wait(peers, 0, rank, nranks, round, err);
+  const long base = (long)rank * chunk;
+  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+    *reinterpret_cast<uint4*>(mine + base + i) = ar_sum8(peers, nranks, off + base + i);
+  ar_publish(peers, 1, rank, nranks, round);
+  ar_wait(peers, 1, rank, nranks, round, err);
+  for (int q = 0; q < nranks; ++q)
+    for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+      *reinterpret_cast<uint4*>(out + q * chunk + i) =
+          *reinterpret_cast<const uint4*>(peers.data[q] + off + q * chunk + i);
 }
 
 __global__ void ar_bump_kernel(int* counter) { *counter += 1; }
@@ -107,21 +157,38 @@ PENNY_API int penny_ar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 PENNY_API int penny_ar_free(void* p) { return (int)hipFree(p); }
 
-// data_ptrs / sig_ptrs: host arrays of nranks device pointers (own buffers + opened peer buffers).
-PENNY_API int penny_allreduce_oneshot(const void* in, void* out, long n, void* const* data_ptrs,
-                                      void* const* sig_ptrs, int* counter, int* err, int rank, int nranks,
-                                      long half_elems, int nblocks, hipStream_t stream) {
+static int ar_launch(bool twoshot, const void* in, void* out, long n, void* const* data_ptrs, void* const* sig_ptrs,
+                     int* counter, int* err, int rank, int nranks, long half_elems, int nblocks, hipStream_t stream) {
   if (n <= 0) return 0;
   if (nranks < 1 || nranks > AR_MAX_RANKS || rank < 0 || rank >= nranks || n % 8 || n > half_elems ||
-      nblocks < 1 || nblocks > AR_MAX_BLOCKS)
+      nblocks < 1 || nblocks > AR_MAX_BLOCKS || (twoshot && n % (8L * nranks)))
     return (int)hipErrorInvalidValue;
   ArPeers peers;
   for (int q = 0; q < AR_MAX_RANKS; ++q) {
     peers.data[q] = q < nranks ? (bf16*)data_ptrs[q] : nullptr;
     peers.sig[q] = q < nranks ? (int*)sig_ptrs[q] : nullptr;
   }
-  hipLaunchKernelGGL(ar_oneshot_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
-                     (const int*)counter, err, rank, nranks, half_elems);
+  if (twoshot)
+    hipLaunchKernelGGL(ar_twoshot_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
+                       (const int*)counter, err, rank, nranks, half_elems);
+  else
+    hipLaunchKernelGGL(ar_oneshot_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
+                       (const int*)counter, err, rank, nranks, half_elems);
   hipLaunchKernelGGL(ar_bump_kernel, dim3(1), dim3(1), 0, stream, counter);
   PENNY_RETURN_LAUNCH();
+}
+
+// data_ptrs / sig_ptrs: host arrays of nranks device pointers (own buffers + opened peer buffers).
+// The signal area of each rank is [2 regions][AR_MAX_RANKS source][AR_MAX_BLOCKS] ints.
+PENNY_API int penny_allreduce_oneshot(const void* in, void* out, long n, void* const* data_ptrs,
+                                      void* const* sig_ptrs, int* counter, int* err, int rank, int nranks,
+                                      long half_elems, int nblocks, hipStream_t stream) {
+  return ar_launch(false, in, out, n, data_ptrs, sig_ptrs, counter, err, rank, nranks, half_elems, nblocks, stream);
+}
+
+// n % (8 * nranks) == 0; nblocks splits each rank's chunk
+PENNY_API int penny_allreduce_twoshot(const void* in, void* out, long n, void* const* data_ptrs,
+                                      void* const* sig_ptrs, int* counter, int* err, int rank, int nranks,
+                                      long half_elems, int nblocks, hipStream_t stream) {
+  return ar_launch(true, in, out, n, data_ptrs, sig_ptrs, counter, err, rank, nranks, half_elems, nblocks, stream);
 }

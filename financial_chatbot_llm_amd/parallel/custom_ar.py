@@ -1,10 +1,12 @@
-"""Custom one-shot all-reduce over xGMI P2P (SURVEY C1 custom path, csrc/kernels/allreduce.hip).
+"""Custom one-shot / two-shot all-reduce over xGMI P2P (SURVEY C1 custom path, csrc/kernels/allreduce.hip).
 
 Each rank allocates one uncached data buffer (two halves, alternated per call) and one signal
 area, exports their IPC handles, and maps every peer's pair (``hipIpcOpenMemHandle``).  A call is
 then a single kernel: copy-in, flag every peer, wait for every peer, read the n buffers over the
 direct links and sum (plus a 1-thread counter bump) -- hipGraph-capturable, because the round
-number lives on the device.
+number lives on the device.  Messages of >= 512 KB on > 2 ranks take the two-shot form
+(reduce-scatter + all-gather inside one kernel, 2(n-1)/n instead of (n-1) message-sizes read
+per rank); both forms sum in the same rank order, so their results are bit-identical.
 
 Used by ``comm.tp_all_reduce`` for bf16 messages up to ``max_bytes`` when enabled
 (``PENNY_CUSTOM_AR=1`` or ``enable_custom_all_reduce``); larger messages and every other dtype go
@@ -22,7 +24,8 @@ from ..ops import _native as N
 
 AR_MAX_RANKS = 8
 AR_MAX_BLOCKS = 64
-SIG_BYTES = AR_MAX_RANKS * AR_MAX_BLOCKS * 4
+SIG_BYTES = 2 * AR_MAX_RANKS * AR_MAX_BLOCKS * 4     # [region: copy-in | reduced][source rank][block]
+TWOSHOT_MIN_BYTES = 512 << 10                        # below: latency-bound, one flag round wins
 
 _SIGS = {
     "penny_ar_handle_size": [],
@@ -31,6 +34,9 @@ _SIGS = {
     "penny_ar_close": [ctypes.c_void_p],
     "penny_ar_free": [ctypes.c_void_p],
     "penny_allreduce_oneshot": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_void_p),
+                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_void_p],
+    "penny_allreduce_twoshot": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_void_p],
 }
@@ -94,16 +100,28 @@ class CustomAllReduce:
         return (x.dtype == torch.bfloat16 and x.is_cuda and x.is_contiguous() and x.numel() % 8 == 0
                 and x.numel() * 2 <= self.max_bytes)
 
-    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def method_for(self, n: int) -> str:
+        """one-shot (one flag round, (n-1) x bytes read per rank) for latency-bound messages;
+        two-shot (two rounds, 2(n-1)/n x bytes) once the per-link bytes dominate, at > 2 ranks."""
+        if self.world > 2 and n * 2 >= TWOSHOT_MIN_BYTES and n % (8 * self.world) == 0:
+            return "twoshot"
+        return "oneshot"
+
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                   method: Optional[str] = None) -> torch.Tensor:
         if not self.eligible(x):
             raise ValueError("tensor not eligible for the custom all-reduce")
         out = torch.empty_like(x) if out is None else out
         n = x.numel()
-        nblocks = max(1, min(AR_MAX_BLOCKS, (n + 2047) // 2048))
-        _check(self._lib.penny_allreduce_oneshot(x.data_ptr(), out.data_ptr(), n, self._data, self._sig,
-                                                 self.counter.data_ptr(), self.err.data_ptr(), self.rank, self.world,
-                                                 self.half_elems, nblocks, N.stream()),
-               "penny_allreduce_oneshot")
+        method = method or self.method_for(n)
+        if method not in ("oneshot", "twoshot") or (method == "twoshot" and n % (8 * self.world)):
+            raise ValueError(f"all-reduce method {method!r} not applicable to {n} elements")
+        per_block = n // self.world if method == "twoshot" else n
+        nblocks = max(1, min(AR_MAX_BLOCKS, (per_block + 2047) // 2048))
+        fn = self._lib.penny_allreduce_twoshot if method == "twoshot" else self._lib.penny_allreduce_oneshot
+        _check(fn(x.data_ptr(), out.data_ptr(), n, self._data, self._sig, self.counter.data_ptr(),
+                  self.err.data_ptr(), self.rank, self.world, self.half_elems, nblocks, N.stream()),
+               f"penny_allreduce_{method}")
         return out
 
     def check(self) -> None:

@@ -1,4 +1,4 @@
-"""Custom one-shot all-reduce (C1 custom path) on the GPU box.
+"""Custom one-shot / two-shot all-reduce (C1 custom path) on the GPU box.
 
 Only one MI355X is available to the test runner, so two processes share cuda:0: each exports
 its IPC buffers, maps the peer's, and runs the real kernel protocol (flags, double-buffered
@@ -46,6 +46,14 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             results.append(((out.float().cpu() - ref).abs().max().item(),
                             (xd.float().cpu() - ref).abs().max().item(), ref.abs().max().item()))
+        # two-shot form (reduce-scatter + all-gather): bit-identical to one-shot
+        for i, n in enumerate([16 * world, 4096 * world + 8 * world, 65536 * world]):
+            g = torch.Generator().manual_seed(7000 + 1000 * i + rank)
+            xd = torch.randn(n, generator=g).to(torch.bfloat16).cuda()
+            a = ar.all_reduce(xd, method="oneshot")
+            b = ar.all_reduce(xd, method="twoshot")
+            torch.cuda.synchronize()
+            results.append((float((a.float() - b.float()).abs().max().item()), 0.0, 0.0))
         # hipGraph capture: the round counter advances on the device across replays
         x = torch.full((4096,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
         ar.all_reduce(x)
@@ -57,7 +65,7 @@ def _worker(rank, world, port, q):
             gph.replay()
         torch.cuda.synchronize()
         results.append((float(y.float().mean().item()), float(world * (world + 1) / 2), 0.0))
-        results.append((float(ar.counter.item()), 16.0, 0.0))   # 10 + 1 eager calls + 5 replays
+        results.append((float(ar.counter.item()), 22.0, 0.0))   # 10 + 6 + 1 eager calls + 5 replays
         ar.check()
         dist.barrier()
         ar.close()
