@@ -225,6 +225,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
   // lane-linear global -> LDS copy of block j's K and V tiles into buffer `buf`
   auto stage = [&](int j, int buf) {
     const long phys = bt[j];
+    PENNY_DASSERT(phys >= 0);
     const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     char* kl = smem + buf * 2 * TILE;
@@ -348,6 +349,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
 
   for (int j = blk0 + w; j < blk1; j += 4) {
     const long phys = bt[j];
+    PENNY_DASSERT(phys >= 0);
     const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     Frag kf[4][KC], vf[DT][2];
@@ -512,6 +514,7 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 
   auto stage = [&](int j) {
     const long phys = bt[j];
+    PENNY_DASSERT(phys >= 0);
     const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     char* kl = smem + (j % NBUF) * 2 * TILE;

@@ -12,6 +12,24 @@
 
 #define PENNY_API extern "C" __attribute__((visibility("default")))
 
+// Device-side bounds checks, compiled only into the debug library (PENNY_KERNEL_DEBUG=1 python -m
+// financial_chatbot_llm_amd._build --debug -> _lib/libpenny_kernels_debug.so, loaded when
+// PENNY_KERNEL_DEBUG=1): print the failing condition and trap at the first bad index, instead of
+// an out-of-bounds access that faults somewhere later.  The production library has none of them.
+#ifdef PENNY_KERNEL_DEBUG
+#include <stdio.h>
+#define PENNY_DASSERT(cond)                                                                         \
+  do {                                                                                              \
+    if (!(cond)) {                                                                                  \
+      printf("[penny] device assert failed: %s (%s:%d, block %d thread %d)\n", #cond, __FILE__,     \
+             __LINE__, (int)blockIdx.x, (int)threadIdx.x);                                          \
+      __builtin_trap();                                                                             \
+    }                                                                                               \
+  } while (0)
+#else
+#define PENNY_DASSERT(cond) ((void)0)
+#endif
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

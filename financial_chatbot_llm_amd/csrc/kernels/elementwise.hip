@@ -51,6 +51,7 @@ __global__ void embedding_kernel(const int* __restrict__ ids, const bf16* __rest
                                  int H, int vocab_start, int vocab_end) {
   const int t = blockIdx.x;
   const int id = ids[t];
+  PENNY_DASSERT(id >= 0);
   const bool mine = id >= vocab_start && id < vocab_end;
   const uint4* src = reinterpret_cast<const uint4*>(table + (long)(mine ? id - vocab_start : 0) * H);
   uint4* dst = reinterpret_cast<uint4*>(out + (long)t * H);

@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
   const int s = blockIdx.x % S, tile = blockIdx.x / S;
+  PENNY_DASSERT(M <= 16 * MT && (tile + 1) * 16 * NF <= N && K % (64 * S) == 0);
   const int n0 = tile * 16 * NF;
   const int kc = K / S, k0 = s * kc;
   const int nst = kc / 64;

@@ -27,6 +27,7 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
   const int t = blockIdx.x;
   const int pos = positions[t];
   const int slot = slots[t];
+  PENNY_DASSERT(pos >= 0 && slot >= -1);
   const int width = (Hq + 2 * Hkv) * D;
   const bf16* row = qkv + (long)t * width;
   const float* prow = SLAB ? P + (long)t * width : nullptr;

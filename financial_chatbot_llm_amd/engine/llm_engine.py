@@ -19,6 +19,7 @@ from ..ops.attention import KV_BS
 from ..parallel import comm
 from ..parallel.dist import state as pstate
 from ..utils.logging import get_logger
+from ..utils.profiling import StepProfiler, marker
 from .block_manager import make_block_manager
 from .model_runner import ModelRunner, build_step_inputs
 from .scheduler import Scheduler
@@ -76,6 +77,7 @@ class LLMEngine:
         self.async_scheduling = bool(getattr(cfg, "async_scheduling", True))
         self._inflight = None      # (batch, samplers, PendingStep) of the step on the GPU
         self.ps = pstate()
+        self.profiler = StepProfiler(rank=self.ps.rank)
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
                     f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
                     f"init={time.perf_counter() - t0:.1f}s")
@@ -108,7 +110,9 @@ class LLMEngine:
         """One engine iteration.  Overlap mode (``async_scheduling``): schedule + launch step N+1
         while step N is still on the GPU, then collect N -- the host's scheduling, input packing
         and token bookkeeping hide behind the device instead of idling it between steps."""
-        return self._step_overlap() if self.async_scheduling else self._step_sync()
+        self.profiler.on_step()
+        with marker("engine.step"):
+            return self._step_overlap() if self.async_scheduling else self._step_sync()
 
     # -- overlap (one-step lookahead) ------------------------------------------------------------
     def _samplers(self, batch) -> List[Sequence]:

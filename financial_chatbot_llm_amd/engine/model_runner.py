@@ -23,6 +23,7 @@ from ..models.common import AttentionMetadata, KVCache
 from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade
 from ..parallel import comm
 from ..utils.logging import get_logger
+from ..utils.profiling import marker
 from .scheduler import ScheduledBatch
 from .sequence import Sequence
 
@@ -242,9 +243,11 @@ class ModelRunner:
             return PendingStep(None, 0, None, None)
         if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
                 and not (si.top_k > 0).any() and not (si.top_p < 1).any()):
-            out = self._graph_decode(si)
+            with marker(f"decode.graph[{si.num_decode}]"):
+                out = self._graph_decode(si)
         else:
-            out = self.sample(self.forward_logits(si), si)
+            with marker(f"forward.eager[{len(si.ids)}]"):
+                out = self.sample(self.forward_logits(si), si)
         n = len(si.logits_idx)
         self.last_sampled[:n].copy_(out[:n].to(torch.int32), non_blocking=True)
         if not self.on_gpu:
@@ -285,9 +288,14 @@ class ModelRunner:
         self._static["slots"].fill_(-1)
         self._static["ctx"].fill_(1)
         self._static["src"].fill_(-1)
-        self._pinned_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32).pin_memory()
-        self._pinned_f = torch.zeros(B, dtype=torch.float32).pin_memory()
-        self._pinned_l = torch.zeros(B, dtype=torch.int64).pin_memory()
+        # two pinned staging sets, alternated per graph step: in overlap mode the host packs step
+        # N+1 while step N's H2D copy may still be queued behind step N-1 on the stream, so a
+        # single buffer could be overwritten before the DMA reads it
+        self._pinned_sets = [(torch.zeros(self._cas_off + n_cas, dtype=torch.int32).pin_memory(),
+                              torch.zeros(B, dtype=torch.float32).pin_memory(),
+                              torch.zeros(B, dtype=torch.int64).pin_memory()) for _ in range(2)]
+        self._pin_flip = 0
+        self._pinned_i32, self._pinned_f, self._pinned_l = self._pinned_sets[0]
 
     def _run_static(self, B: int) -> torch.Tensor:
         s = self._static
@@ -332,6 +340,8 @@ class ModelRunner:
         B = self._bucket(n)
         G = self.graphs[B]
         S, W = self.max_decode_batch, self.max_blocks
+        self._pinned_i32, self._pinned_f, self._pinned_l = self._pinned_sets[self._pin_flip]
+        self._pin_flip ^= 1
         buf = self._pinned_i32.numpy()
         # layout: ids | pos | slots | ctx | bt  (each section sized for the largest bucket)
         buf[0:n] = si.ids

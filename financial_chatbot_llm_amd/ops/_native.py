@@ -50,8 +50,9 @@ _SIGS = {
 
 
 def lib_path() -> str:
-    from .._build import KERNEL_LIB
-    return KERNEL_LIB
+    """The production kernel library, or its bounds-checked debug build with PENNY_KERNEL_DEBUG=1."""
+    from .._build import kernel_lib
+    return kernel_lib(os.environ.get("PENNY_KERNEL_DEBUG") == "1")
 
 
 def load(build_if_missing: bool = True) -> ctypes.CDLL:
@@ -64,7 +65,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
         path = lib_path()
         if not os.path.exists(path) and build_if_missing:
             from .._build import build_kernels
-            build_kernels()
+            build_kernels(debug=os.environ.get("PENNY_KERNEL_DEBUG") == "1")
         try:
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
