@@ -104,6 +104,7 @@ class EngineConfig:
     model: str = "llama3-8b"                # registry key in models.configs
     dtype: str = "bf16"
     moe_parallel: str = "tp"                # Mixtral under TP: "tp" (FFN-sharded experts) | "ep" (all-to-all)
+    sequence_parallel: bool = False         # TP prefills >= 1024 rows: reduce-scatter/all-gather (Megatron SP)
     async_scheduling: bool = True           # overlap host scheduling of step N+1 with GPU step N
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
@@ -140,6 +141,7 @@ class EngineConfig:
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),
+            sequence_parallel=_env_bool("PENNY_SEQUENCE_PARALLEL", False),
             async_scheduling=_env_bool("PENNY_ASYNC_SCHEDULING", True),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),

@@ -17,6 +17,7 @@ def build_model(engine_cfg, device, seed: int = 0):
         model = LlamaModel(cfg, device=device)
     else:
         raise ValueError(f"{cfg.name} is not a decoder")
+    model.sequence_parallel = bool(getattr(engine_cfg, "sequence_parallel", False))
     if engine_cfg.weights:
         from .weights import load_decoder_weights
         load_decoder_weights(model, engine_cfg.weights)

@@ -50,6 +50,10 @@ class DecoderModel:
         self.vocab_start, self.vocab_end = vocab_range(cfg.vocab_size, self.tp_rank, self.tp_size)
         self.w: Dict[str, torch.Tensor] = {}
         self.wt: Dict[str, torch.Tensor] = {}
+        # sequence parallelism for long prefills under TP (dense MLP only): steps of at least
+        # sp_min_tokens rows run forward_sp (reduce-scatter / all-gather instead of all-reduce)
+        self.sequence_parallel = False
+        self.sp_min_tokens = 1024
         self.cos_sin = ops.rope_cos_sin(self.D, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
                                         device=self.device)
 
@@ -142,15 +146,15 @@ class DecoderModel:
         x = ops.embedding(ids, self.w["embed"], self.vocab_start, self.vocab_end)
         return comm.tp_all_reduce(x) if self.tp_size > 1 else x
 
-    def mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True) -> torch.Tensor:
         p = f"layers.{i}."
         a = linear(h, self.w[p + "gate_up"], epilogue="silu")   # fused SiLU(gate)*up
         # TP=1: decode-size batches return split-K slabs, reduced by the next add+RMSNorm
         out = linear(a, self.w[p + "down"], wt=self.wt.get(p + "down"), slabs=self.tp_size == 1)
-        return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+        return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
 
     def attention(self, i: int, h: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata,
-                  kv: KVCache) -> torch.Tensor:
+                  kv: KVCache, reduce: bool = True) -> torch.Tensor:
         p = f"layers.{i}."
         T = h.shape[0]
         qkv = linear(h, self.w[p + "qkv"], wt=self.wt.get(p + "qkv"), slabs=self.tp_size == 1)
@@ -166,9 +170,44 @@ class DecoderModel:
                        workspace=meta.decode_ws, out=attn[tp:], cascade=meta.cascade)
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"),
                      slabs=self.tp_size == 1)
-        return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+        return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
+
+    def uses_sp(self, T: int) -> bool:
+        return (self.sequence_parallel and self.tp_size > 1 and T >= self.sp_min_tokens
+                and self.cfg.arch == "llama")
+
+    def forward_sp(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata,
+                   kv: KVCache) -> torch.Tensor:
+        """Sequence-parallel forward (Megatron SP) for long prefills under TP.
+
+        Between the row-parallel outputs and the next column-parallel input the residual stream
+        is sharded by rows: reduce-scatter after the vocab-parallel embedding / O / down, norm +
+        residual add on the local T/tp rows, all-gather before QKV / gate|up.  Rows are padded to
+        a multiple of tp (padding rows never reach attention: they are cut before QKV)."""
+        c, n = self.cfg, self.tp_size
+        T = ids.shape[0]
+        Tp = -(-T // n) * n
+
+        def pad(t: torch.Tensor) -> torch.Tensor:
+            return t if Tp == T else torch.cat([t, t.new_zeros((Tp - T,) + tuple(t.shape[1:]))])
+
+        x = comm.tp_reduce_scatter_rows(pad(ops.embedding(ids, self.w["embed"], self.vocab_start, self.vocab_end)))
+        residual = x
+        h = ops.rms_norm(x, self.w["layers.0.in_norm"], c.norm_eps)
+        for i in range(c.num_layers):
+            p = f"layers.{i}."
+            if i > 0:
+                h = ops.rms_norm(x, self.w[p + "in_norm"], c.norm_eps, residual=residual)
+            a = self.attention(i, comm.tp_all_gather_rows(h)[:T], positions, meta, kv, reduce=False)
+            a = comm.tp_reduce_scatter_rows(pad(a))
+            h = ops.rms_norm(a, self.w[p + "post_norm"], c.norm_eps, residual=residual)
+            x = comm.tp_reduce_scatter_rows(pad(self.mlp(i, comm.tp_all_gather_rows(h)[:T], reduce=False)))
+        h = ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
+        return comm.tp_all_gather_rows(h)[:T]
 
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata, kv: KVCache) -> torch.Tensor:
+        if self.uses_sp(ids.shape[0]):
+            return self.forward_sp(ids, positions, meta, kv)
         c = self.cfg
         x = self.embed(ids)
         residual = x

@@ -5,6 +5,9 @@
   the decode hipGraph together with the GEMMs.
 * C2 ``tp_all_gather_last``: vocab-parallel LM-head logits ([B, V/tp] -> [B, V]); embedding
   partials are summed with C1.
+* SP ``tp_reduce_scatter_rows`` / ``tp_all_gather_rows``: sequence-parallel prefill (Megatron
+  SP) -- the residual stream is sharded by rows between the row-parallel and column-parallel
+  GEMMs (reduce-scatter after O/down, all-gather before QKV/gate-up).
 * C4 ``broadcast_object``: the TP leader's scheduler decisions (token ids, positions, block
   tables) for a step, so non-leader ranks replay the identical forward.
 
@@ -58,6 +61,44 @@ def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     parts = [torch.empty_like(x) for _ in range(s.tp_size)]
     dist.all_gather(parts, x.contiguous(), group=s.tp_group)
     return torch.cat(parts, dim=-1)
+
+
+def _is_gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+def tp_reduce_scatter_rows(x: torch.Tensor) -> torch.Tensor:
+    """Sequence parallel (SP): [T, H] partial sums -> this rank's [T/tp, H] row block of the sum.
+    Replaces C1's all-reduce after the row-parallel O/down projections in long prefills: the
+    same bytes on the wire (RS + AG = AR for ring algorithms), but the residual stream, the
+    norms and the residual adds then touch 1/tp of the rows.  T must be a multiple of tp."""
+    s = state()
+    if s.tp_size == 1:
+        return x
+    T = x.shape[0]
+    if T % s.tp_size:
+        raise ValueError(f"{T} rows not divisible by tp={s.tp_size}")
+    if _is_gloo(s.tp_group):   # gloo has no reduce_scatter: same result through all_reduce (CI)
+        dist.all_reduce(x, group=s.tp_group)
+        return x.chunk(s.tp_size)[s.tp_rank].contiguous()
+    out = torch.empty((T // s.tp_size,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x.contiguous(), group=s.tp_group)
+    return out
+
+
+def tp_all_gather_rows(x: torch.Tensor) -> torch.Tensor:
+    """SP: every rank's [T/tp, H] row block -> the full [T, H] (rank order)."""
+    s = state()
+    if s.tp_size == 1:
+        return x
+    x = x.contiguous()
+    if _is_gloo(s.tp_group):
+        parts = [torch.empty_like(x) for _ in range(s.tp_size)]
+        dist.all_gather(parts, x, group=s.tp_group)
+        return torch.cat(parts, 0)
+    out = torch.empty((x.shape[0] * s.tp_size,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    return out
 
 
 def broadcast_object(obj: Any) -> Any:

@@ -2,7 +2,8 @@
 
 Each rank owns half the heads / half the MLP columns / half the vocabulary; row-parallel outputs
 are all-reduced (C1), vocab-parallel logits all-gathered (C2), and the engine leader broadcasts
-each step's packed inputs to the follower (C4).  TP=2 must reproduce TP=1.
+each step's packed inputs to the follower (C4).  TP=2 must reproduce TP=1, with and without
+sequence parallelism (reduce-scatter / all-gather of the row-sharded residual stream).
 """
 import os
 import socket
@@ -35,6 +36,11 @@ def _worker(rank, world, port, q):
         tp = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=7, std=0.05)
         ids = list(range(3, 140))
         logits_tp = _prefill_logits(tp, ids)
+        tp.sequence_parallel, tp.sp_min_tokens = True, 1     # 137 rows: not a multiple of 2 or 4
+        assert tp.uses_sp(len(ids))
+        logits_sp = _prefill_logits(tp, ids)
+        tp.sequence_parallel = False
+        logits_tp = (logits_tp, logits_sp)
         ecfg = EngineConfig(model="unused", device="cpu", num_kv_blocks=32, max_model_len=1024,
                             max_num_batched_tokens=64, use_cuda_graph=False)
         eng = LLMEngine(ecfg, model=tp, tokenizer=SyntheticLlamaTokenizer(cfg.vocab_size))
@@ -79,7 +85,9 @@ def test_tp_matches_tp1(world):
     ref = LlamaModel(cfg, device="cpu", tp_rank=0, tp_size=1, dtype=torch.float32).init_random(seed=7, std=0.05)
     ref_logits = _prefill_logits(ref, list(range(3, 140)))
     for r in range(world):
-        assert torch.allclose(res[r][0], ref_logits, atol=1e-4, rtol=1e-4)
+        plain, sp = res[r][0]
+        assert torch.allclose(plain, ref_logits, atol=1e-4, rtol=1e-4)
+        assert torch.allclose(sp, ref_logits, atol=1e-4, rtol=1e-4)      # sequence-parallel prefill
     ecfg = EngineConfig(model="unused", device="cpu", num_kv_blocks=32, max_model_len=1024,
                         max_num_batched_tokens=64, use_cuda_graph=False)
     eng = LLMEngine(ecfg, model=ref, tokenizer=SyntheticLlamaTokenizer(cfg.vocab_size))
