@@ -200,7 +200,7 @@ def bench_skinny(dev) -> List[Dict]:
     return out
 
 
-def bench_splitk(dev) -> List[Dict]:
+def bench_splitk(dev, names=("qkv", "o", "down")) -> List[Dict]:
     """Mid-batch split-K GEMM (+ slab reduce) vs hipBLASLt on the Llama-3-8B decode projections.
 
     Weights rotate over enough copies (>= 768 MB) that every call streams W from HBM, not from
@@ -209,6 +209,8 @@ def bench_splitk(dev) -> List[Dict]:
     out = []
     shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
     for name, (N, K) in shapes.items():
+        if name not in names:
+            continue
         copies = max(2, (768 << 20) // (N * K * 2))
         ws = [torch.randn((N, K), device=dev).to(torch.bfloat16) for _ in range(copies)]
         wts = [gemm.tile_weight(w) for w in ws]
@@ -226,7 +228,7 @@ def bench_splitk(dev) -> List[Dict]:
                    "hipblaslt_GBps": round(wbytes / base / 1e3, 1)}
             best = None
             for S in (1, 2, 4, 7, 8):
-                for nf in (2, 4, 8):
+                for nf in (2, 4, 6, 8):
                     if K % (64 * S) or N % (16 * nf):
                         continue
                     P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
@@ -299,7 +301,8 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk, "moe": bench_moe}[name](dev)
+                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
+                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "moe": bench_moe}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

@@ -221,11 +221,12 @@ int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N
 }  // namespace
 
 // Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
-// aligned (ldx % 8 == 0).  nf: W row groups per workgroup (2, 4 or 8).  P is [S, M, N] f32.
+// aligned (ldx % 8 == 0).  nf: W row groups per workgroup (2, 4, 6 or 8;
+// 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4).  P is [S, M, N] f32.
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
                                 hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 256 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
+  if (M > 256 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
   const int mt = (M + 15) / 16;
   float* p = static_cast<float*>(P);
@@ -233,6 +234,7 @@ PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, v
   if (mt <= MT_) {                                                                     \
     if (nf == 2) return launch<2, MT_, WA2_>(X, ldx, Wt, K, p, M, N, S, stream);       \
     if (nf == 4) return launch<4, MT_, WA4_>(X, ldx, Wt, K, p, M, N, S, stream);       \
+    if (nf == 6) return launch<6, MT_, 2>(X, ldx, Wt, K, p, M, N, S, stream);          \
     return launch<8, MT_, WA8_>(X, ldx, Wt, K, p, M, N, S, stream);                    \
   }
   // (NF + MT) even; wave split picked to minimise fragment reads per wave (NF/WA + MT/WB)

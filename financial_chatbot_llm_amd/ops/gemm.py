@@ -136,9 +136,11 @@ def load_gemm_tuning(model: str, tp: int = 1) -> Optional[str]:
 # (N, K) -> [(max M, S, nf), ...] for the split-K kernel, measured on MI355X against hipBLASLt with
 # the weights streamed from HBM (bench/kernels.py --only splitk, profiles/r1_splitk_v3.jsonl),
 # choosing by GEMM time + the consumer's extra slab read (S*M*N*4 B at ~5 TB/s).  Llama-3-8B:
-# QKV 1.3-1.6x, O 1.5-2.2x, down 1.4-2.8x faster than the library at M = 16..192.
+# QKV 1.4-1.9x, O 1.5-2.2x, down 1.4-2.8x faster than the library at M = 16..192.  Every chosen
+# config launches exactly 256 workgroups (one per CU): QKV 64 tiles x S=4, O 64 x 4, down 32 x 8
+# (profiles/r1_splitk_v4_qkv.jsonl: the 96-row QKV tile beats 128 rows x 192 workgroups by 10 %).
 SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
-    (6144, 4096): [(16, 2, 2), (32, 2, 4), (256, 4, 8)],     # QKV
+    (6144, 4096): [(256, 4, 6)],                             # QKV: 96-row tiles -> 256 workgroups
     (4096, 4096): [(192, 4, 4)],                             # O (M=256: hipBLASLt is faster)
     (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
 }

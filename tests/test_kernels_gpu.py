@@ -228,12 +228,12 @@ def test_skinny_gemm(M, cfg):
 
 
 @pytest.mark.parametrize("M", [5, 33, 64, 90, 128, 200, 256])
-@pytest.mark.parametrize("S,nf", [(1, 4), (2, 8), (4, 4), (8, 8), (2, 2)])
+@pytest.mark.parametrize("S,nf", [(1, 4), (2, 8), (4, 4), (8, 8), (2, 2), (4, 6)])
 def test_splitk_gemm(M, S, nf):
     """Mid-batch split-K GEMM (f32 slabs) + slab reduce (+ residual) vs the fp32 reference."""
     from financial_chatbot_llm_amd.ops import gemm
     g = torch.Generator().manual_seed(11)
-    N_, K = 256, 2048
+    N_, K = 384, 2048
     x = rnd(M, K, gen=g)
     w = rnd(N_, K, scale=0.05, gen=g)
     res = rnd(M, N_, gen=g)
