@@ -140,13 +140,11 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
   }
   auto stage = [&](int j) {
     char* base = smem + (j % NBUF) * SBYTES;
+    // default cache policy on W too: the nt hint measured 4-7 % slower at M >= 48 (2-3 % faster
+    // only at M <= 32; profiles/r1_splitk_v5_qkv_nont.jsonl vs r1_splitk_v4_qkv.jsonl)
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      if (w * LOADS + i < 2 * NF)  // weights are read once per decode step: non-temporal (aux = nt)
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 2);
-      else
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 0);
-    }
+    for (int i = 0; i < LOADS; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 0);
   };
 
   f32x4 acc[FW][TW];
