@@ -250,6 +250,42 @@ def bench_splitk(dev, names=("qkv", "o", "down")) -> List[Dict]:
     return out
 
 
+def bench_gateup(dev) -> List[Dict]:
+    """Fused gate|up + SiLU*up MFMA kernel vs hipBLASLt GEMM + silu_mul on the Llama-3-8B MLP
+    (N = 2*14336, K = 4096), weights rotated so every call streams W from HBM."""
+    from ..ops import activation, gemm
+    gemm.load_gemm_tuning("llama3-8b")   # the baseline runs the curated solutions, as in serving
+    out = []
+    N, K = 28672, 4096
+    copies = max(2, (768 << 20) // (N * K * 2))
+    ws = [torch.randn((N, K), device=dev).to(torch.bfloat16) for _ in range(copies)]
+    wts = [gemm.tile_weight(w) for w in ws]
+    it = [0]
+
+    def nxt():
+        it[0] = (it[0] + 1) % copies
+        return it[0]
+
+    for M in (8, 16, 32, 48, 64, 96, 128, 192, 256):
+        x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+        y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
+        base = timeit(lambda: activation.silu_mul(torch.nn.functional.linear(x, ws[nxt()]), interleave16=True),
+                      iters=copies * 2)
+        row = {"op": "gateup", "M": M, "hipblaslt_silu_us": round(base, 1)}
+        best = None
+        for nf in (4, 8):
+            us = timeit(lambda: gemm.gateup_silu(x, wts[nxt()], N, nf, out=y), iters=copies * 2)
+            row[f"nf{nf}_us"] = round(us, 1)
+            row[f"nf{nf}_GBps"] = round(N * K * 2 / us / 1e3, 1)
+            if best is None or us < best[1]:
+                best = (nf, us)
+        row["best_nf"], row["speedup"] = best[0], round(base / best[1], 2)
+        out.append(row)
+    del ws, wts
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_moe(dev) -> List[Dict]:
     """Mixtral-8x7B MoE layer (E=8, top-2, H=4096, F=14336): HIP fp8 pipeline vs bf16 per-expert
     hipBLASLt GEMMs (the eager bucketed path)."""
@@ -302,7 +338,7 @@ def main(argv=None) -> int:
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
-                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "moe": bench_moe}[name](dev)
+                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

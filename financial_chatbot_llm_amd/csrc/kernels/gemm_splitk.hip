@@ -87,14 +87,19 @@ __device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (
   }
 }
 
-template <int NF, int MT, int WA>
+// SILU: W is the 16-row-interleaved gate|up weight (ops/gemm.py interleave16) and S == 1; the
+// epilogue writes Y[m, f] = silu(gate) * up as bf16 [M, N/2] (ldy) instead of f32 slabs -- each
+// wave owns whole (gate, up) row-group pairs, so the pair meets in one lane's registers.
+template <int NF, int MT, int WA, bool SILU = false>
 __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restrict__ X, int ldx,
                                                              const bf16* __restrict__ Wt, int K,
-                                                             float* __restrict__ P, int M, int N, int S) {
+                                                             float* __restrict__ P, int M, int N, int S,
+                                                             bf16* __restrict__ Y = nullptr, int ldy = 0) {
   constexpr int WB = 4 / WA;
   constexpr int FW = NF / WA;   // W row groups per wave
   constexpr int TW = MT / WB;   // token tiles per wave
   static_assert(NF % WA == 0 && MT % WB == 0, "wave split");
+  static_assert(!SILU || FW % 2 == 0, "SiLU epilogue needs (gate, up) row-group pairs per wave");
   constexpr int NBUF = Ring<NF, MT>::NBUF;
   static_assert(NBUF >= 3, "ring too shallow");
   constexpr int WBYTES = NF * 2 * 1024;        // W pieces of one BK=64 stage
@@ -164,6 +169,27 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
     stage_mma<FW, TW, WBYTES>(smem + (j % NBUF) * SBYTES, acc, wa, wb, lane, g, col);
   }
 
+  if constexpr (SILU) {
+    // row group G = n0/16 + wa*FW + f is gate (G even) / up (G odd) of output cols 16*(G/2)..+15
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int m = (wb * TW + t) * 16 + col;
+      if (m >= M) continue;
+#pragma unroll
+      for (int f = 0; f < FW; f += 2) {
+        const int G = n0 / 16 + wa * FW + f;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // same roundings as GEMM -> bf16 gate|up -> silu_mul (HF: silu in the activation dtype)
+          const float gt = (float)(bf16)acc[f][t][r], up = (float)(bf16)acc[f + 1][t][r];
+          o[r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
+        }
+        *reinterpret_cast<bf16x4*>(Y + (long)m * ldy + (G >> 1) * 16 + 4 * g) = o;
+      }
+    }
+    return;
+  }
   // lane holds W rows n = 16f + 4g + r (r = 0..3) for token 16t + col: one 16-B store per tile
   float* ps = P + (long)s * M * N;
 #pragma unroll
@@ -216,7 +242,39 @@ int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N
   return (int)hipGetLastError();
 }
 
+template <int NF, int MT, int WA>
+int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, hipStream_t st) {
+  hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
+                     (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
+
+// Fused gate|up + SiLU*up for 16 < M <= 256 (K9 at mid-batch decode): W = tile_weight(interleave16
+// gate|up) [N = 2F rows], Y [M, F] bf16 with row stride ldy.  No split-K: N = 28672 already gives
+// N/(16*nf) = 224 (nf 8) or 448 (nf 4) workgroups.  Contract (checked): N % (16*nf) == 0,
+// nf in {4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0.
+PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
+                                     int nf, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 4 && nf != 8) || N % (16 * nf))
+    return (int)hipErrorInvalidValue;
+  const int mt = (M + 15) / 16;
+#define GU_CASE(MT_, WA4_, WA8_)                                                          \
+  if (mt <= MT_) {                                                                      \
+    if (nf == 4) return launch_silu<4, MT_, WA4_>(X, ldx, Wt, K, Y, ldy, M, N, stream); \
+    return launch_silu<8, MT_, WA8_>(X, ldx, Wt, K, Y, ldy, M, N, stream);              \
+  }
+  GU_CASE(2, 2, 2)
+  GU_CASE(4, 1, 2)
+  GU_CASE(6, 2, 2)
+  GU_CASE(8, 1, 2)
+  GU_CASE(12, 1, 2)
+  GU_CASE(16, 1, 2)
+#undef GU_CASE
+  return (int)hipErrorInvalidValue;
+}
 
 // Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
 // aligned (ldx % 8 == 0).  nf: W row groups per workgroup (2, 4, 6 or 8;

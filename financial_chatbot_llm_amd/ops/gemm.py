@@ -77,6 +77,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
         cfg = splitk_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if cfg is not None:
             return Slabs(splitk_partials(x, wt, N_, *cfg))
+    if epilogue == "silu" and wt is not None and residual is None:
+        nf = gateup_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
+        if nf is not None:
+            return gateup_silu(x, wt, N_, nf)
     if skinny_ok(x, w, epilogue, wt):
         ntf, nw = _config(N_, K, epilogue)
         out_n = N_ // 2 if epilogue == "silu" else N_
@@ -161,6 +165,42 @@ def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
             if K % (64 * S) == 0 and N_ % (16 * nf) == 0:
                 return S, nf
     return None
+
+
+# (N, K) of the interleave16 gate|up weight -> [(min M, max M, nf), ...] for the fused
+# gate|up + SiLU*up MFMA kernel (penny_gateup_silu_gemm; no split-K), measured against hipBLASLt
+# (curated solutions) + silu_mul with W streamed from HBM (bench/kernels.py --only gateup,
+# profiles/r1_gateup_v1.jsonl): 1.4x at M <= 16, 1.22-1.35x at M = 32..96, 1.14x at M = 128; at
+# M >= 192 the 3-deep ring of the 256-token tile is MFMA/LDS-latency bound and the library wins.
+GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
+    (28672, 4096): [(1, 160, 8)],
+}
+
+
+def gateup_config(M: int, N_: int, K: int) -> Optional[int]:
+    """nf for the fused gate|up kernel at this shape, or None (``PENNY_GATEUP=0`` disables;
+    ``PENNY_GATEUP=force`` takes it for any shape the kernel accepts)."""
+    mode = os.environ.get("PENNY_GATEUP", "1")
+    if mode == "0" or M > 256 or K % 64:
+        return None
+    for lo, hi, nf in GATEUP.get((N_, K), ()):
+        if lo <= M <= hi:
+            return nf
+    if mode == "force":
+        return 8 if N_ % 128 == 0 else (4 if N_ % 64 == 0 else None)
+    return None
+
+
+def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) from the fragment-tiled interleave16 gate|up weight ``wt``."""
+    M, K = x.shape
+    if not N.use_native(x):
+        return silu_mul(F.linear(x, untile_weight(wt)), interleave16=True)
+    y = out if out is not None else torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
+    N.call("penny_gateup_silu_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), y.stride(0), M, N_, nf,
+           N.stream())
+    return y
 
 
 class Slabs:

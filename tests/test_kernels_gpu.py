@@ -250,6 +250,31 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [1, 17, 48, 100, 128, 256])
+@pytest.mark.parametrize("nf", [4, 8])
+def test_gateup_silu_gemm(M, nf):
+    """Fused gate|up GEMM + SiLU*up (interleave16 weight, fragment-tiled) vs the fp32 reference
+    silu(x gate^T) * (x up^T), and vs the unfused hipBLASLt + silu_mul path it replaces."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(5)
+    Fr, K = 512, 1024
+    x = rnd(M, K, gen=g)
+    gate, up = rnd(Fr, K, scale=0.05, gen=g), rnd(Fr, K, scale=0.05, gen=g)
+    wi = gemm.interleave16(gate, up).to(DEV).contiguous()
+    y = gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, nf)
+    gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
+    close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
+    unfused = ops.silu_mul(torch.nn.functional.linear(x.to(DEV), wi), interleave16=True)
+    close(y, unfused, atol=2e-2)
+    # strided X is a supported input; output rows land at the given stride
+    xw = torch.zeros(M, K + 64, dtype=torch.bfloat16)
+    xw[:, 32:32 + K] = x
+    out = torch.zeros(M, Fr + 8, dtype=torch.bfloat16, device=DEV)
+    gemm.gateup_silu(xw.to(DEV)[:, 32:32 + K], gemm.tile_weight(wi), 2 * Fr, nf, out=out[:, :Fr])
+    close(out[:, :Fr], y, atol=0, rtol=0)
+    assert (out[:, Fr:] == 0).all()
+
+
 @pytest.mark.parametrize("S,T", [(1, 3), (4, 128), (8, 200)])
 def test_slab_consumers_match_reduce_then_op(S, T):
     """RMSNorm (+residual) and RoPE/KV-write fed the split-K slabs directly equal the same kernels
