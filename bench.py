@@ -49,7 +49,8 @@ def parse(argv=None):
     ap.add_argument("--corpus", type=int, default=1_000_000)
     ap.add_argument("--users", type=int, default=10_000)
     ap.add_argument("--max-model-len", type=int, default=8192)
-    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-batched-tokens", type=int, default=4096,
+                    help="per-step token budget (measured: 4096 beats 3072-16384 by 2-4 %% turns/s, profiles/r1_sweep_max_batched_tokens.txt)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tool-steps", type=int, default=1,
                     help=">1: multi-step agent with the plot tool bound (north-star config 4)")
