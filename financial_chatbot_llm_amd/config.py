@@ -113,7 +113,7 @@ class EngineConfig:
     kv_mem_fraction: float = 0.80           # of free HBM after weights (288 GB per MI355X)
     num_kv_blocks: Optional[int] = None     # explicit override (tests)
     max_num_seqs: int = 256                 # running-batch cap
-    max_num_batched_tokens: int = 16384     # per-step token budget (chunked prefill)
+    max_num_batched_tokens: int = 4096      # per-step token budget (chunked prefill; measured best: profiles/r1_sweep_max_batched_tokens.txt)
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on

@@ -162,7 +162,8 @@ class ModelRunner:
         self.graphs: Dict[int, _DecodeGraph] = {}
         self._static = None
         self.graph_pool = None
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0}
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0,
+                      "prefill_steps": 0, "prefill_step_tokens": 0}
         # sampled ids of the latest step stay on the device: the next step gathers its decode ids
         # from here when it was launched before this one's ids reached the host (overlap mode)
         self.max_samplers = max(self.max_decode_batch, max_decode_batch) + 1024
@@ -238,6 +239,9 @@ class ModelRunner:
         sampled ids reach the host through ``PendingStep.result()`` (pinned D2H + event)."""
         self.stats["steps"] += 1
         self.stats["tokens"] += len(si.ids)
+        if si.num_prefill_tokens:   # GEMM M of the steps that run the prefill (library) GEMMs
+            self.stats["prefill_steps"] += 1
+            self.stats["prefill_step_tokens"] += len(si.ids)
         if len(si.logits_idx) == 0:
             self._forward_only(si)
             return PendingStep(None, 0, None, None)
