@@ -70,6 +70,21 @@ class AsyncEngine:
         if eng.device.type == "cuda":
             import torch
             torch.cuda.set_device(eng.device)
+        prof_dir = os.environ.get("PENNY_PYPROFILE")   # host-side cProfile of the engine thread
+        prof = None
+        if prof_dir:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
+        try:
+            self._run_loop(eng)
+        finally:
+            if prof is not None:
+                prof.disable()
+                os.makedirs(prof_dir, exist_ok=True)
+                prof.dump_stats(os.path.join(prof_dir, f"engine_r{os.environ.get('RANK', '0')}.prof"))
+
+    def _run_loop(self, eng: LLMEngine) -> None:
         while not self._stop:
             with self._lock:
                 pending, self._pending = self._pending, []

@@ -298,4 +298,11 @@ class LLMEngine:
                 "cascade_rows": self.runner.stats["cascade_rows"],
                 "prefill_steps": self.runner.stats["prefill_steps"],
                 "prefill_step_tokens_mean": round(self.runner.stats["prefill_step_tokens"]
-                                                  / max(1, self.runner.stats["prefill_steps"]), 1)}
+                                                  / max(1, self.runner.stats["prefill_steps"]), 1),
+                # device time per step (PENNY_STEP_GPU_TIMING=1): compare with step_p50_ms (host cadence)
+                "gpu_graph_ms_mean": round(1e3 * self.runner.stats["gpu_graph_s"]
+                                           / max(1, self.runner.stats["graph_steps"]), 3),
+                "gpu_eager_ms_mean": round(1e3 * self.runner.stats["gpu_eager_s"]
+                                           / max(1, self.runner.stats["steps"] - self.runner.stats["graph_steps"]), 3),
+                "gpu_idle_between_steps_s": round(self.runner.stats["gpu_idle_s"], 3),
+                "gpu_idle_gaps": self.runner.stats["gpu_idle_gaps"]}

@@ -12,6 +12,7 @@ layers of a decode step become one launch, removing ~1.5 us x 300+ launch gaps p
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -124,8 +125,10 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
 class PendingStep:
     """Sampled ids of a launched step (host copy in flight)."""
 
-    def __init__(self, cpu_out: Optional[torch.Tensor], n: int, host: Optional[torch.Tensor], event):
+    def __init__(self, cpu_out: Optional[torch.Tensor], n: int, host: Optional[torch.Tensor], event,
+                 start_event=None, stats: Optional[Dict] = None, key: str = ""):
         self._cpu, self.n, self._host, self._event = cpu_out, n, host, event
+        self._start, self._stats, self._key = start_event, stats, key
 
     def result(self) -> List[int]:
         if self.n == 0:
@@ -133,6 +136,17 @@ class PendingStep:
         if self._cpu is not None:
             return self._cpu.tolist()
         self._event.synchronize()
+        if self._start is not None:   # device time of the step (PENNY_STEP_GPU_TIMING=1)
+            st = self._stats
+            st[self._key] += self._start.elapsed_time(self._event) / 1e3
+            # device idle between consecutive steps: this step's start - the previous step's end
+            prev_end = st.get("_prev_end_ev")
+            if prev_end is not None:
+                gap = prev_end.elapsed_time(self._start) / 1e3
+                if gap > 0:
+                    st["gpu_idle_s"] += gap
+                    st["gpu_idle_gaps"] += 1
+            st["_prev_end_ev"] = self._event
         return self._host[:self.n].tolist()
 
 
@@ -163,7 +177,9 @@ class ModelRunner:
         self._static = None
         self.graph_pool = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0,
-                      "prefill_steps": 0, "prefill_step_tokens": 0}
+                      "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
+                      "gpu_idle_s": 0.0, "gpu_idle_gaps": 0, "_prev_end_ev": None}
+        self._gpu_timing = self.on_gpu and os.environ.get("PENNY_STEP_GPU_TIMING", "0") == "1"
         # sampled ids of the latest step stay on the device: the next step gathers its decode ids
         # from here when it was launched before this one's ids reached the host (overlap mode)
         self.max_samplers = max(self.max_decode_batch, max_decode_batch) + 1024
@@ -245,10 +261,16 @@ class ModelRunner:
         if len(si.logits_idx) == 0:
             self._forward_only(si)
             return PendingStep(None, 0, None, None)
+        start_ev = None
+        if self._gpu_timing:
+            start_ev = torch.cuda.Event(enable_timing=True)
+            start_ev.record()
+        graph = False
         if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
                 and not (si.top_k > 0).any() and not (si.top_p < 1).any()):
             with marker(f"decode.graph[{si.num_decode}]"):
                 out = self._graph_decode(si)
+            graph = True
         else:
             with marker(f"forward.eager[{len(si.ids)}]"):
                 out = self.sample(self.forward_logits(si), si)
@@ -259,9 +281,9 @@ class ModelRunner:
         host = self._pinned_out[self._out_flip]
         self._out_flip ^= 1
         host[:n].copy_(out[:n], non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=start_ev is not None)
         ev.record()
-        return PendingStep(None, n, host, ev)
+        return PendingStep(None, n, host, ev, start_ev, self.stats, "gpu_graph_s" if graph else "gpu_eager_s")
 
     def _forward_only(self, si: StepInputs) -> None:
         ids = self._to_dev(si.ids)
