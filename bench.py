@@ -49,8 +49,10 @@ def parse(argv=None):
     ap.add_argument("--corpus", type=int, default=1_000_000)
     ap.add_argument("--users", type=int, default=10_000)
     ap.add_argument("--max-model-len", type=int, default=8192)
-    ap.add_argument("--max-batched-tokens", type=int, default=4096,
-                    help="per-step token budget (measured: 4096 beats 3072-16384 by 2-4 %% turns/s, profiles/r1_sweep_max_batched_tokens.txt)")
+    ap.add_argument("--max-batched-tokens", type=int, default=None,
+                    help="per-step token budget; default 4096 for dense models (beats 3072-16384 by 2-4 %% "
+                         "turns/s, profiles/r1_sweep_max_batched_tokens.txt), 16384 for MoE (bigger chunks give "
+                         "every expert more rows: 20.8 vs 19.1 turns/s, profiles/r1_bench_mixtral8x7b_fp8_v12.txt)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tool-steps", type=int, default=1,
                     help=">1: multi-step agent with the plot tool bound (north-star config 4)")
@@ -149,6 +151,8 @@ async def run(args, ps):
 
 def main(argv=None) -> int:
     args = parse(argv)
+    if args.max_batched_tokens is None:
+        args.max_batched_tokens = 16384 if args.model.startswith("mixtral") else 4096
     os.environ.setdefault("LOG_LEVEL", "WARNING")
     import torch
     import torch.distributed as dist

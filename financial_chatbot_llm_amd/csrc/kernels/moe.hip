@@ -211,16 +211,20 @@ __global__ void __launch_bounds__(NW * 64) moe_gemm_kernel(
 // ---------------------------------------------------------------------------------------------
 // 5. combine the K expert outputs of each token
 // ---------------------------------------------------------------------------------------------
-__global__ void moe_combine_kernel(const bf16* __restrict__ Y2, const int* __restrict__ inv, int K, int H,
-                                   bf16* __restrict__ out) {
+// W (optional, prefill path): routing weight of each sorted pair, applied here in f32 (the decode
+// path already scaled its rows inside the W2 GEMM epilogue)
+__global__ void moe_combine_kernel(const bf16* __restrict__ Y2, const int* __restrict__ inv,
+                                   const float* __restrict__ W, int K, int H, bf16* __restrict__ out) {
   const int t = blockIdx.x;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < K; ++j) {
+      const int pos = inv[t * K + j];
+      const float wj = W ? W[pos] : 1.f;
       float f[8];
-      unpack8(reinterpret_cast<const uint4*>(Y2 + (long)inv[t * K + j] * H)[c], f);
+      unpack8(reinterpret_cast<const uint4*>(Y2 + (long)pos * H)[c], f);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+      for (int i = 0; i < 8; ++i) acc[i] += wj * f[i];
     }
     reinterpret_cast<uint4*>(out + (long)t * H)[c] = pack8(acc);
   }
@@ -272,6 +276,17 @@ PENNY_API int penny_moe_gemm_fp8(const void* Xq, const float* xs, const int* row
 
 PENNY_API int penny_moe_combine(const void* Y2, const int* inv, int T, int K, int H, void* out, hipStream_t stream) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, stream, (const bf16*)Y2, inv, K, H, (bf16*)out);
+  if (H % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, stream, (const bf16*)Y2, inv, (const float*)nullptr,
+                     K, H, (bf16*)out);
+  PENNY_RETURN_LAUNCH();
+}
+
+// out[t] = sum_j W[inv[t*K+j]] * Y2[inv[t*K+j]]  (f32 accumulate; prefill combine, no atomics)
+PENNY_API int penny_moe_combine_weighted(const void* Y2, const int* inv, const float* W, int T, int K, int H,
+                                         void* out, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, stream, (const bf16*)Y2, inv, W, K, H, (bf16*)out);
   PENNY_RETURN_LAUNCH();
 }

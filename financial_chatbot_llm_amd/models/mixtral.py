@@ -39,9 +39,16 @@ from .llama import DecoderModel
 
 
 class MixtralModel(DecoderModel):
-    def __init__(self, *a, fp8: bool = False, moe_parallel: str = "tp", prefill_dequant_cache: bool = True, **kw):
+    def __init__(self, *a, fp8: bool = False, moe_parallel: str = "tp", prefill_dequant_cache: bool = True,
+                 prefill_fp8: bool = True, **kw):
         super().__init__(*a, **kw)
-        self.prefill_dequant_cache = prefill_dequant_cache
+        # fp8 experts, prefill-size chunks: hipBLASLt fp8 x fp8 GEMMs (torch._scaled_mm, per-row
+        # activation x per-row weight scales) on an untiled copy of the SAME quantized experts --
+        # the arithmetic of the decode fp8 MFMA pipeline (dynamic per-row fp8 activations) at
+        # 1.4-1.8x the bf16 GEMM rate (profiles/r1_scaled_mm_probe.jsonl); otherwise a resident bf16
+        # dequantized copy (``prefill_dequant_cache``) or per-step dequantization
+        self.prefill_fp8 = prefill_fp8 and self.device.type == "cuda" and hasattr(torch, "_scaled_mm")
+        self.prefill_dequant_cache = prefill_dequant_cache and not self.prefill_fp8
         if moe_parallel not in ("tp", "ep"):
             raise ValueError(f"moe_parallel must be 'tp' or 'ep', got {moe_parallel!r}")
         self.fp8 = fp8
@@ -77,7 +84,9 @@ class MixtralModel(DecoderModel):
                 q, s = moe_ops.quantize_fp8_rowwise(w)
                 self.w[k + "_t"] = moe_ops.tile_fp8_weight(q)
                 self.w[k + "_scale"] = s.float().contiguous()
-                if self.prefill_dequant_cache:
+                if self.prefill_fp8:
+                    self.w[k + "_q"] = q.contiguous()          # [E, N, K] e4m3, row-major
+                elif self.prefill_dequant_cache:
                     # the SAME quantized values in bf16 for the prefill GEMMs (hipBLASLt): ~90 GB for
                     # 8x7B -- HBM3E has it, and prefill stops re-dequantizing 2.8 GB per layer per step
                     self.w[k + "_deq"] = moe_ops.dequant_fp8(q, s, self.dtype)
@@ -102,8 +111,19 @@ class MixtralModel(DecoderModel):
                                                 f_local, self.device)
         return self._moe_ws
 
+    def _expert_fp8(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
+        """One expert on its routed rows with fp8 x fp8 hipBLASLt GEMMs (prefill-size buckets)."""
+        xq, xs = moe_ops.quant_rows_fp8(rows)
+        y13 = torch._scaled_mm(xq, self.w[p + "w13_q"][e].t(), scale_a=xs[:, None],
+                               scale_b=self.w[p + "w13_scale"][e][None, :], out_dtype=self.dtype)
+        aq, as_ = moe_ops.quant_rows_fp8(ops.silu_mul(y13, interleave16=True))
+        return torch._scaled_mm(aq, self.w[p + "w2_q"][e].t(), scale_a=as_[:, None],
+                                scale_b=self.w[p + "w2_scale"][e][None, :], out_dtype=self.dtype)
+
     def _expert(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
         """One (local) expert on its routed rows (eager path)."""
+        if self.fp8 and self.prefill_fp8 and (p + "w13_q") in self.w:
+            return self._expert_fp8(p, rows, e)
         if self.fp8:
             act = ops.silu_mul(F.linear(rows, self._dequant(p, "w13", e)), interleave16=True)
             return F.linear(act, self._dequant(p, "w2", e))
@@ -119,7 +139,7 @@ class MixtralModel(DecoderModel):
                           group=pstate().tp_group)
         # fp8 MFMA pipeline while the step is weight-bandwidth-bound; bigger prefill chunks go to
         # hipBLASLt on the cached bf16 copy of the same quantized experts (compute-bound regime)
-        fp8_limit = 1024 if self.prefill_dequant_cache else 4096
+        fp8_limit = 1024 if (self.prefill_dequant_cache or self.prefill_fp8) else 4096
         if self.fp8 and ops._native.use_native(h) and T * c.top_k_experts <= fp8_limit:
             out = moe_ops.moe_decode_fp8(h.contiguous(), logits.contiguous(), self.w[p + "w13_t"],
                                          self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
@@ -129,11 +149,11 @@ class MixtralModel(DecoderModel):
         order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
         offs = offsets.tolist()
         xs = h.index_select(0, tok_idx)
-        ys = torch.zeros_like(xs)
+        ys = torch.empty_like(xs)
         for e in range(c.num_experts):
             a, b = offs[e], offs[e + 1]
             if b > a:
                 ys[a:b] = self._expert(p, xs[a:b], e)
-        out = torch.zeros_like(h)
-        out.index_add_(0, tok_idx, (ys.float() * tok_w[:, None]).to(h.dtype))
+        # every sorted row is written above (the buckets tile [0, T*k)); weighted gather-combine
+        out = moe_ops.combine_weighted(ys, order, tok_w, T, c.top_k_experts)
         return comm.tp_all_reduce(out) if self.tp_size > 1 else out

@@ -36,6 +36,38 @@ def route(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
     return order, offsets, tok_idx, tok_w
 
 
+def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-row e4m3 quantisation on the device (HIP ``penny_quant_rows_fp8``, the decode
+    pipeline's activation quantiser): x [M, K] bf16 -> (fp8 [M, K], f32 scale [M])."""
+    from . import _native as N
+    M, K = x.shape
+    if not N.use_native(x):
+        q, s = quantize_fp8_rowwise(x)
+        return q, s.float()
+    q = torch.empty((M, K), dtype=torch.uint8, device=x.device)
+    s = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.call("penny_quant_rows_fp8", N.ptr(x), x.stride(0), M, K, N.ptr(q), N.ptr(s), N.stream())
+    return q.view(FP8), s
+
+
+def combine_weighted(ys: torch.Tensor, order: torch.Tensor, tok_w: torch.Tensor, T: int, k: int) -> torch.Tensor:
+    """out[t] = sum_j w * ys[pos(t, j)] for expert-sorted rows ``ys`` [T*k, H] (``order``/``tok_w``
+    from :func:`route`): a gather per token with f32 accumulation (HIP ``penny_moe_combine_weighted``)
+    instead of float copies + a scaled ``index_add_`` over the sorted rows."""
+    from . import _native as N
+    H = ys.shape[1]
+    inv = torch.empty_like(order)
+    inv[order] = torch.arange(order.numel(), device=order.device, dtype=order.dtype)
+    if not N.use_native(ys):
+        w = ys.float() * tok_w[:, None].float()
+        return w[inv].view(T, k, H).sum(1).to(ys.dtype)
+    inv32 = inv.to(torch.int32)
+    w32 = tok_w.float().contiguous()
+    out = torch.empty((T, H), dtype=ys.dtype, device=ys.device)
+    N.call("penny_moe_combine_weighted", N.ptr(ys), N.ptr(inv32), N.ptr(w32), T, k, H, N.ptr(out), N.stream())
+    return out
+
+
 def quantize_fp8_rowwise(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """w [..., out, in] -> (fp8 e4m3fn, f32 scale [..., out]) with w ~= q * scale[..., None]."""
     amax = w.float().abs().amax(dim=-1).clamp_min(1e-12)

@@ -82,6 +82,26 @@ def test_mixtral_fp8_experts_close_to_bf16():
     assert (got.argmax(-1) == ref.argmax(-1)).float().mean() > 0.8
 
 
+def test_mixtral_fp8_prefill_scaled_mm_path():
+    """Prefill-size MoE chunks (T*k > 1024) run fp8 x fp8 hipBLASLt GEMMs (torch._scaled_mm) on the
+    untiled quantized experts: equal to the fp32 reference with per-row fp8 activations, and to
+    the decode fp8 MFMA pipeline run over the same rows in decode-size chunks."""
+    from financial_chatbot_llm_amd.ops import moe
+    cfg = get_model_config("mixtral-tiny")
+    m = MixtralModel(cfg, device="cuda", tp_rank=0, tp_size=1, fp8=True).init_random(seed=5, std=0.05)
+    assert m.prefill_fp8 and "layers.0.w13_q" in m.w and "layers.0.w13_deq" not in m.w
+    g = torch.Generator().manual_seed(1)
+    h = torch.randn(601, cfg.hidden_size, generator=g).to(torch.bfloat16).cuda()
+    got = m.mlp(0, h)                                             # 1202 pairs -> prefill path
+    p = "layers.0."
+    ref = moe.moe_fp8_reference(h.float(), m.w[p + "router"], m.w[p + "w13_q"], m.w[p + "w13_scale"],
+                                m.w[p + "w2_q"], m.w[p + "w2_scale"], cfg.top_k_experts, quant_act=True)
+    scale = ref.float().abs().max().item()
+    assert (got.float() - ref.float()).abs().max().item() < 0.05 * scale
+    dec = torch.cat([m.mlp(0, h[i:i + 200]) for i in range(0, 601, 200)])   # decode pipeline chunks
+    assert (got.float() - dec.float()).abs().max().item() < 0.05 * scale
+
+
 def test_bge_encoder_gpu_matches_cpu():
     from financial_chatbot_llm_amd.models.bert import BertEncoder
     cfg = get_model_config("bert-tiny")

@@ -250,6 +250,21 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("T,k", [(1, 2), (37, 2), (300, 2), (64, 1)])
+def test_moe_combine_weighted(T, k):
+    """Prefill MoE combine: weighted gather over the expert-sorted rows == scaled index_add."""
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(3)
+    E, H = 8, 512
+    logits = torch.randn(T, E, generator=g)
+    topw, topi = moe.topk_softmax(logits, k)
+    order, offsets, tok_idx, tok_w = moe.route(topi.to(DEV), topw.to(DEV), E)
+    ys = rnd(T * k, H, gen=g).to(DEV)
+    ref = torch.zeros(T, H, dtype=torch.float32, device=DEV)
+    ref.index_add_(0, tok_idx, ys.float() * tok_w[:, None])
+    close(moe.combine_weighted(ys, order, tok_w, T, k), ref, atol=2e-2)
+
+
 @pytest.mark.parametrize("M", [1, 17, 48, 100, 128, 256])
 @pytest.mark.parametrize("nf", [4, 8])
 def test_gateup_silu_gemm(M, nf):
