@@ -11,8 +11,9 @@
 //   4. quant_rows on [P, F], then moe_gemm<SCALE_W>: x W2_e, output scaled by the routing weight.
 //   5. moe_combine: out[t] = sum over its K pairs (inverse map, no atomics).
 // Weights are pre-tiled (ops/moe.py tile_fp8_weight): fragment pair (row group, 2 k-steps) is
-// 1 KiB contiguous -- lane l holds 8 bytes of k-step 2p then 8 bytes of k-step 2p+1 -- so each
-// weight load is one coalesced 16-byte-per-lane instruction; fp8 halves the bytes streamed per
+// 1 KiB contiguous -- lane 16g+r holds 16 contiguous k of row r, feeding both MFMAs of the pair --
+// so each weight load is one coalesced 16-byte-per-lane instruction, and the activation operand
+// (same k permutation) is one 16-byte load per token row too; fp8 halves the bytes streamed per
 // decode step versus bf16 (the whole expert bank is touched at decode batch sizes).
 #include "common.h"
 
@@ -139,28 +140,33 @@ __global__ void __launch_bounds__(NW * 64) moe_gemm_kernel(
     for (int f = 0; f < NTF; ++f)
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[f][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // lane (g, col) owns physical k = 64p + 16g .. +15 of its token row: one 16-B load per row tile
+    // and k-pair, matching the weight tiling (ops/moe.py tile_fp8_weight); bytes 0-7 feed the
+    // first MFMA of the pair, bytes 8-15 the second
     const unsigned char* xr[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int pr = c0 + min(16 * m + col, nrow - 1);
       const int src = rows ? rows[pr] : pr;
-      xr[m] = Xq + (long)src * K + kb + 8 * g;
+      xr[m] = Xq + (long)src * K + kb + 16 * g;
     }
     for (int k = 0; k < kper; k += 64) {
-      uint4 wv[NTF];
+      uint4 wv[NTF], xv[4];
 #pragma unroll
       for (int f = 0; f < NTF; ++f)
         wv[f] = *reinterpret_cast<const uint4*>(We + (((long)(n0 / 16 + f) * kpairs + (kb + k) / 64) * 64 + lane) * 16);
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        long xv[4];
+      for (int m = 0; m < 4; ++m) xv[m] = *reinterpret_cast<const uint4*>(xr[m] + k);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) xv[m] = *reinterpret_cast<const long*>(xr[m] + k + 32 * half);
+      for (int half = 0; half < 2; ++half) {
 #pragma unroll
         for (int f = 0; f < NTF; ++f) {
           const long a = half ? ((long)wv[f].w << 32 | wv[f].z) : ((long)wv[f].y << 32 | wv[f].x);
 #pragma unroll
-          for (int m = 0; m < 4; ++m) acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, xv[m], acc[f][m], 0, 0, 0);
+          for (int m = 0; m < 4; ++m) {
+            const long b = half ? ((long)xv[m].w << 32 | xv[m].z) : ((long)xv[m].y << 32 | xv[m].x);
+            acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, acc[f][m], 0, 0, 0);
+          }
         }
       }
     }
@@ -247,12 +253,10 @@ PENNY_API int penny_quant_rows_fp8(const void* x, int ld, int rows, int n, void*
   PENNY_RETURN_LAUNCH();
 }
 
-// epi 1: SiLU-gated (W13 interleaved, Y [P, N/2]); epi 2: scale by routing weight (Y [P, N])
-PENNY_API int penny_moe_gemm_fp8(const void* Xq, const float* xs, const int* rows, const int* offsets, const void* Wt,
-                                 const float* ws, const float* route_w, void* Y, int E, int N, int K, int epi,
-                                 hipStream_t stream) {
-  constexpr int NTF = 2;
-  if (N % (16 * NTF) || K % 64) return (int)hipErrorInvalidValue;
+template <int NTF>
+static int moe_gemm_launch(const void* Xq, const float* xs, const int* rows, const int* offsets, const void* Wt,
+                           const float* ws, const float* route_w, void* Y, int E, int N, int K, int epi,
+                           hipStream_t stream) {
   dim3 grid(N / (16 * NTF), E);
   // waves split K: as many as divide it into whole 64-wide k-pairs (4 for every real model)
 #define MOE_LAUNCH(NW_)                                                                                          \
@@ -272,6 +276,16 @@ PENNY_API int penny_moe_gemm_fp8(const void* Xq, const float* xs, const int* row
   else MOE_LAUNCH(1)
 #undef MOE_LAUNCH
   PENNY_RETURN_LAUNCH();
+}
+
+// epi 1: SiLU-gated (W13 interleaved, Y [P, N/2]); epi 2: scale by routing weight (Y [P, N]).
+// ntf: 16-row weight groups per workgroup (2 or 4).
+PENNY_API int penny_moe_gemm_fp8(const void* Xq, const float* xs, const int* rows, const int* offsets, const void* Wt,
+                                 const float* ws, const float* route_w, void* Y, int E, int N, int K, int epi,
+                                 int ntf, hipStream_t stream) {
+  if ((ntf != 2 && ntf != 4) || N % (16 * ntf) || K % 64) return (int)hipErrorInvalidValue;
+  if (ntf == 4) return moe_gemm_launch<4>(Xq, xs, rows, offsets, Wt, ws, route_w, Y, E, N, K, epi, stream);
+  return moe_gemm_launch<2>(Xq, xs, rows, offsets, Wt, ws, route_w, Y, E, N, K, epi, stream);
 }
 
 PENNY_API int penny_moe_combine(const void* Y2, const int* inv, int T, int K, int H, void* out, hipStream_t stream) {

@@ -4,6 +4,7 @@ gfx950 uses the OCP ``e4m3fn`` encoding (not MI300's ``fnuz``), which is torch.f
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -85,16 +86,18 @@ def dequant_fp8(q: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> t
 # ----------------------------------------------------------------------------------------------
 def tile_fp8_weight(q: torch.Tensor) -> torch.Tensor:
     """fp8 [E, N, K] -> uint8 [E, N/16, K/64, 64, 16]: fragment pair (row group, 2 k-steps) is
-    1 KiB contiguous; lane 16g+r holds row r, k = 64p + 32s + 8g + j at byte 8s + j."""
+    1 KiB contiguous; lane 16g+r holds row r, k = 64p + 16g + 8s + j at byte 8s + j -- 16
+    CONTIGUOUS k of the row, so the activation operand of the same lane is one 16-byte load too
+    (the MFMA's k slots are a permutation of the physical k, applied to both operands)."""
     E, N_, K = q.shape
     assert N_ % 16 == 0 and K % 64 == 0
-    u = q.view(torch.uint8).view(E, N_ // 16, 16, K // 64, 2, 4, 8)      # e rg r kp s g j
-    return u.permute(0, 1, 3, 5, 2, 4, 6).reshape(E, N_ // 16, K // 64, 64, 16).contiguous()
+    u = q.view(torch.uint8).view(E, N_ // 16, 16, K // 64, 4, 2, 8)      # e rg r kp g s j
+    return u.permute(0, 1, 3, 4, 2, 5, 6).reshape(E, N_ // 16, K // 64, 64, 16).contiguous()
 
 
 def untile_fp8_weight(t: torch.Tensor) -> torch.Tensor:
     E, RG, KP, _, _ = t.shape
-    u = t.view(E, RG, KP, 4, 16, 2, 8).permute(0, 1, 4, 2, 5, 3, 6)       # e rg r kp s g j
+    u = t.view(E, RG, KP, 4, 16, 2, 8).permute(0, 1, 4, 2, 3, 5, 6)       # e rg r kp g s j
     return u.reshape(E, RG * 16, KP * 64).contiguous().view(FP8)
 
 
@@ -129,6 +132,11 @@ def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act: bool = 
     return out.to(h.dtype)
 
 
+# 16-row weight groups per workgroup for the (W13, W2) grouped fp8 GEMMs (PENNY_MOE_NTF="a,b"):
+# 4,4 measured 6-16 % faster than 2,2 at T = 64-256 decode tokens (profiles/r1_moe_ntf.jsonl)
+MOE_NTF = tuple(int(v) for v in os.environ.get("PENNY_MOE_NTF", "4,4").split(","))
+
+
 class MoEWorkspace:
     """Device buffers for one decode-sized MoE step (reused across layers; graph-capturable)."""
 
@@ -161,11 +169,12 @@ def moe_decode_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Ten
     N.call("penny_moe_route", N.ptr(router_logits), T, E, top_k, N.ptr(ws.sorted_tok), N.ptr(ws.sorted_w),
            N.ptr(ws.offsets), N.ptr(ws.inv), st)
     N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(ws.xq), N.ptr(ws.xs), st)
+    ntf13, ntf2 = MOE_NTF
     N.call("penny_moe_gemm_fp8", N.ptr(ws.xq), N.ptr(ws.xs), N.ptr(ws.sorted_tok), N.ptr(ws.offsets), N.ptr(w13t),
-           N.ptr(s13), None, N.ptr(ws.a), E, F2, H, 1, st)
+           N.ptr(s13), None, N.ptr(ws.a), E, F2, H, 1, ntf13, st)
     N.call("penny_quant_rows_fp8", N.ptr(ws.a), F_, P, F_, N.ptr(ws.aq), N.ptr(ws.as_), st)
     N.call("penny_moe_gemm_fp8", N.ptr(ws.aq), N.ptr(ws.as_), None, N.ptr(ws.offsets), N.ptr(w2t), N.ptr(s2),
-           N.ptr(ws.sorted_w), N.ptr(ws.y2), E, H, F_, 2, st)
+           N.ptr(ws.sorted_w), N.ptr(ws.y2), E, H, F_, 2, ntf2, st)
     out = torch.empty_like(h)
     N.call("penny_moe_combine", N.ptr(ws.y2), N.ptr(ws.inv), T, top_k, H, N.ptr(out), st)
     return out
