@@ -25,6 +25,8 @@
 // runs the sequence index fastest so the workgroups that read the SAME shared-prefix blocks
 // (every turn's system prompt is a prefix-cache hit) are in flight together and hit in L2/MALL.
 #include "common.h"
+
+#include <cstdlib>
 #include "kv_layout.h"
 
 #define LOG2E 1.4426950408889634f
@@ -313,7 +315,12 @@ __global__ void __launch_bounds__(256, 2) cascade_kernel(
 // ------------------------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------------------------
-template <int D>
+// HEAD_FAST: grid (Hkv, B, nparts) -- the kv head is the fastest-varying workgroup index, so with
+// round-robin dispatch over the 8 XCDs (Hkv == 8 for every model served here) each XCD owns ONE
+// kv head for every sequence and its 4 MB L2 holds that head's shared-prefix blocks (~0.5 MB per
+// head per layer for a 1k-token system prompt).  Otherwise grid (B, nparts, Hkv), sequence
+// fastest: each XCD streams whole sequences, whose 8 heads of a KV block are contiguous.
+template <int D, bool HEAD_FAST>
 __global__ void __launch_bounds__(256) decode_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -323,7 +330,9 @@ __global__ void __launch_bounds__(256) decode_kernel(
   __shared__ float s_m[4][16], s_l[4][16];
   __shared__ float s_o[4][16][D + 4];
 
-  const int b = blockIdx.x, p = blockIdx.y, h = blockIdx.z;
+  const int b = HEAD_FAST ? blockIdx.y : blockIdx.x;
+  const int p = HEAD_FAST ? blockIdx.z : blockIdx.y;
+  const int h = HEAD_FAST ? blockIdx.x : blockIdx.z;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
   const int blk0 = (kv_start ? kv_start[b] : 0) + p * pb;  // cascade: shared blocks are done elsewhere
@@ -641,15 +650,27 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   if (cascade && (chunk_blocks <= 0 || grid_work <= 0 || 128 % (Hq / Hkv) ||
                   part_stride < nparts + (g_max_blocks + chunk_blocks - 1) / chunk_blocks))
     return (int)hipErrorInvalidValue;
-  dim3 grid(B, nparts, Hkv);  // sequence fastest: shared-prefix blocks are read concurrently
+  // measured (profiles/r1_decode_head_fast.txt): head-fastest wins at B <= 16 (18.5 vs 21.6 us at
+  // ctx 2048 / 1024 shared), sequence-fastest at B >= 64 (a sequence's 8 heads of a KV block are
+  // one contiguous 128 KB run, read by one XCD); PENNY_DECODE_HEAD_FAST=0/1 forces either
+  static const int head_fast_env = [] {
+    const char* v = getenv("PENNY_DECODE_HEAD_FAST");
+    return v ? atoi(v) : -1;
+  }();
+  const bool head_fast = head_fast_env >= 0 ? head_fast_env != 0 : B <= 16;
+  const dim3 grid = head_fast ? dim3(Hkv, B, nparts) : dim3(B, nparts, Hkv);
   const float sl2 = scale * LOG2E;
   const CascadeArgs ca{members, work, nwork, part_m, part_l, part_o, part_stride, nparts, chunk_blocks};
 #define DECODE_LAUNCH(DD)                                                                                         \
   if (cascade && (phases & 1))                                                                                  \
     hipLaunchKernelGGL(cascade_kernel<DD>, dim3(grid_work, Hkv), dim3(256), 0, stream, (const bf16*)q, cu_g, g_ctx,  \
                        g_bt, (const bf16*)k_cache, (const bf16*)v_cache, sl2, Hq, Hkv, g_max_blocks, ca);         \
-  if (phases & 2)                                                                                               \
-    hipLaunchKernelGGL(decode_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start,          \
+  if ((phases & 2) && head_fast)                                                                                \
+    hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start,  \
+                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
+                       part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
+  if ((phases & 2) && !head_fast)                                                                               \
+    hipLaunchKernelGGL((decode_kernel<DD, false>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start, \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
                        part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
   if ((phases & 4) && (nparts > 1 || cascade))                                                                  \
