@@ -225,6 +225,12 @@ PENNY_API int penny_rmsnorm_slabs(const void* P, int S, void* res, const void* w
   if (H % 8 || S < 1) return (int)hipErrorInvalidValue;
   int threads, cpt;
   pick_geometry(H, &threads, &cpt);
+  if (T <= 512 && H / 8 <= 1024 && (H / 8) % 64 == 0) {
+    // decode-size T: one 16-B chunk (x S slabs) per thread -- twice the waves per row, so the
+    // S-deep slab reads of a T-row batch (T workgroups) have more latency hiding
+    threads = H / 8;
+    cpt = 1;
+  }
   if (add_residual) {
     DISPATCH_CPT(cpt, hipLaunchKernelGGL((rmsnorm_kernel<CPT, true, true>), dim3(T), dim3(threads), 0, stream,
                                          nullptr, (bf16*)res, (const bf16*)w, (bf16*)y, H, eps, (const float*)P, S, T));

@@ -40,7 +40,9 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
   const int total = n_rot + Hkv * VU;
   const long blk = slot >= 0 ? slot / KV_BS : 0;
   const int off = slot >= 0 ? slot % KV_BS : 0;
-  for (int u = threadIdx.x; u < total; u += blockDim.x) {
+  // gridDim.y workgroups share a token's units (decode-size T: T workgroups alone would leave
+  // half the CUs idle while the split-K slabs are read)
+  for (int u = threadIdx.x + blockIdx.y * blockDim.x; u < total; u += blockDim.x * gridDim.y) {
     if (u < n_rot) {
       const int h = u / RU, c = u % RU;
       float x1[8], x2[8];
@@ -88,11 +90,12 @@ static int launch_rope_kv(const void* qkv, const float* P, int S, const int* pos
                           int apply_rope, hipStream_t stream) {
   if (T <= 0) return 0;
   const int threads = 256;
+  const dim3 grid(T, T <= 512 ? 2 : 1);
   if (D == 128) {
-    hipLaunchKernelGGL((rope_kv_kernel<128, SLAB>), dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions,
+    hipLaunchKernelGGL((rope_kv_kernel<128, SLAB>), grid, dim3(threads), 0, stream, (const bf16*)qkv, positions,
                        cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope, P, S, T);
   } else if (D == 64) {
-    hipLaunchKernelGGL((rope_kv_kernel<64, SLAB>), dim3(T), dim3(threads), 0, stream, (const bf16*)qkv, positions,
+    hipLaunchKernelGGL((rope_kv_kernel<64, SLAB>), grid, dim3(threads), 0, stream, (const bf16*)qkv, positions,
                        cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, apply_rope, P, S, T);
   } else {
     return (int)hipErrorInvalidValue;
