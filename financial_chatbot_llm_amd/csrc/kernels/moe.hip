@@ -112,6 +112,58 @@ __global__ void quant_rows_kernel(const bf16* __restrict__ x, int ld, int n, uns
   }
 }
 
+// 2b. prefill experts: SiLU(gate) * up of the 16-row-interleaved W13 GEMM output, quantised per row
+//     to fp8 in the same pass (one workgroup per row, the row held in registers between the amax
+//     and the quantise sweeps): the bf16 activation never round-trips through HBM.
+template <int CPT>
+__global__ void __launch_bounds__(256) silu_quant_rows_kernel(const bf16* __restrict__ gu, int F,
+                                                              unsigned char* __restrict__ q,
+                                                              float* __restrict__ scale) {
+  __shared__ float red[4];
+  const long row = blockIdx.x;
+  const uint4* gr = reinterpret_cast<const uint4*>(gu + row * 2L * F);
+  const int nchunk = F >> 3;   // 8 outputs per chunk: output cols 8c..8c+7 = pair c/2, half c&1
+  float a[CPT][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nchunk) {
+      float g[8], u[8];
+      const int pair = c >> 1, half = c & 1;
+      unpack8(gr[pair * 4 + half], g);
+      unpack8(gr[pair * 4 + 2 + half], u);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        // silu in the activation dtype, like silu_mul_kernel: bf16(silu(g)) * u, rounded to bf16
+        a[i][k] = (float)(bf16)((float)(bf16)(g[k] / (1.f + __expf(-g[k]))) * u[k]);
+        amax = fmaxf(amax, fabsf(a[i][k]));
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = amax > 0.f ? amax / FP8_MAX : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) scale[row] = sc;
+  uint2* qr = reinterpret_cast<uint2*>(q + row * (long)F);
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nchunk) {
+      uint32_t w0 = 0, w1 = 0;
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][0] * inv, a[i][1] * inv, w0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][2] * inv, a[i][3] * inv, w0, true);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][4] * inv, a[i][5] * inv, w1, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][6] * inv, a[i][7] * inv, w1, true);
+      qr[c] = make_uint2(w0, w1);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // 3/4. grouped fp8 GEMM over expert buckets
 // ---------------------------------------------------------------------------------------------
@@ -243,6 +295,22 @@ PENNY_API int penny_moe_route(const void* logits, int T, int E, int K, int* sort
   hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(1024), 0, stream, (const bf16*)logits, T, E, K, sorted_tok,
                      sorted_w, offsets, inv);
   PENNY_RETURN_LAUNCH();
+}
+
+// gu [rows, 2F] bf16 (16-column-interleaved gate|up) -> q [rows, F] e4m3, scale [rows] f32
+PENNY_API int penny_silu_quant_rows_fp8(const void* gu, int rows, int F, void* q, float* scale, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (F % 16) return (int)hipErrorInvalidValue;
+  const int cpt = (F / 8 + 255) / 256;
+#define SQ_CASE(C)                                                                                        \
+  if (cpt <= C) {                                                                                         \
+    hipLaunchKernelGGL(silu_quant_rows_kernel<C>, dim3(rows), dim3(256), 0, stream, (const bf16*)gu, F,   \
+                       (unsigned char*)q, scale);                                                         \
+    PENNY_RETURN_LAUNCH();                                                                                \
+  }
+  SQ_CASE(1) SQ_CASE(2) SQ_CASE(4) SQ_CASE(8) SQ_CASE(16)
+#undef SQ_CASE
+  return (int)hipErrorInvalidValue;
 }
 
 PENNY_API int penny_quant_rows_fp8(const void* x, int ld, int rows, int n, void* q, float* scale, hipStream_t stream) {

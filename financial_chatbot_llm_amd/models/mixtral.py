@@ -116,7 +116,7 @@ class MixtralModel(DecoderModel):
         xq, xs = moe_ops.quant_rows_fp8(rows)
         y13 = torch._scaled_mm(xq, self.w[p + "w13_q"][e].t(), scale_a=xs[:, None],
                                scale_b=self.w[p + "w13_scale"][e][None, :], out_dtype=self.dtype)
-        aq, as_ = moe_ops.quant_rows_fp8(ops.silu_mul(y13, interleave16=True))
+        aq, as_ = moe_ops.silu_quant_rows_fp8(y13)
         return torch._scaled_mm(aq, self.w[p + "w2_q"][e].t(), scale_a=as_[:, None],
                                 scale_b=self.w[p + "w2_scale"][e][None, :], out_dtype=self.dtype)
 

@@ -51,6 +51,20 @@ def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return q.view(FP8), s
 
 
+def silu_quant_rows_fp8(gu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """silu(gate) * up of a 16-interleaved gate|up GEMM output [M, 2F], quantised per row to e4m3 in
+    the same pass (HIP ``penny_silu_quant_rows_fp8``): -> (fp8 [M, F], f32 scale [M])."""
+    from . import _native as N
+    from .activation import silu_mul
+    M, F2 = gu.shape
+    if not N.use_native(gu):
+        return quant_rows_fp8(silu_mul(gu, interleave16=True))
+    q = torch.empty((M, F2 // 2), dtype=torch.uint8, device=gu.device)
+    s = torch.empty(M, dtype=torch.float32, device=gu.device)
+    N.call("penny_silu_quant_rows_fp8", N.ptr(gu.contiguous()), M, F2 // 2, N.ptr(q), N.ptr(s), N.stream())
+    return q.view(FP8), s
+
+
 def combine_weighted(ys: torch.Tensor, order: torch.Tensor, tok_w: torch.Tensor, T: int, k: int) -> torch.Tensor:
     """out[t] = sum_j w * ys[pos(t, j)] for expert-sorted rows ``ys`` [T*k, H] (``order``/``tok_w``
     from :func:`route`): a gather per token with f32 accumulation (HIP ``penny_moe_combine_weighted``)

@@ -250,6 +250,18 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,F", [(1, 384), (37, 14336), (300, 2048)])
+def test_silu_quant_rows_fp8_matches_two_pass(M, F):
+    """Fused SiLU*up + per-row fp8 quantisation == silu_mul then quant_rows (same arithmetic)."""
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(4)
+    gu = rnd(M, 2 * F, gen=g).to(DEV)
+    q1, s1 = moe.silu_quant_rows_fp8(gu)
+    q2, s2 = moe.quant_rows_fp8(ops.silu_mul(gu, interleave16=True))
+    assert torch.equal(s1, s2)
+    assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8))
+
+
 @pytest.mark.parametrize("T,k", [(1, 2), (37, 2), (300, 2), (64, 1)])
 def test_moe_combine_weighted(T, k):
     """Prefill MoE combine: weighted gather over the expert-sorted rows == scaled index_add."""
