@@ -141,7 +141,9 @@ def main(argv=None) -> int:
     if args.runtime_only:
         print(f"built {build_runtime(verbose=True)}")
         return 0
-    build_all(jobs=args.j, verbose=True, debug=args.debug or os.environ.get("PENNY_KERNEL_DEBUG") == "1")
+    # an in-tree debug library is kept in sync with the sources too (a stale one would miss symbols)
+    debug = args.debug or os.environ.get("PENNY_KERNEL_DEBUG") == "1" or os.path.exists(KERNEL_LIB_DEBUG)
+    build_all(jobs=args.j, verbose=True, debug=debug)
     print(f"built {KERNEL_LIB}")
     return 0
 
