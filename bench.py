@@ -64,6 +64,8 @@ def parse(argv=None):
                          "child process (engine core) so its host work never shares the serving GIL.  Measured "
                          "equal turns/s here (the GPU is already never idle between steps, "
                          "PENNY_STEP_GPU_TIMING=1), ~60 ms higher p50 TTFT from the IPC hop")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: contract tests of the bench itself with tiny models (gloo for >1 rank)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -78,7 +80,12 @@ async def run(args, ps):
     from financial_chatbot_llm_amd.parallel.dist import barrier
     from financial_chatbot_llm_amd.retrieval import BgeEmbedder, DeviceVectorStore, RetrievalService
 
-    dev = torch.device("cuda", torch.cuda.current_device())
+    on_gpu = args.device == "cuda"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+
+    def sync() -> None:
+        if on_gpu:
+            torch.cuda.synchronize()
     t0 = time.perf_counter()
     embedder = BgeEmbedder(args.embed_model, device=str(dev), seed=ps.rank)
     store = DeviceVectorStore(embedder.dim, device=str(dev))
@@ -89,10 +96,10 @@ async def run(args, ps):
     sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
                         max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
-                        graph_batch_sizes=sizes, seed=0, device="cuda", dtype=args.dtype)
+                        graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype)
     if args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
         from financial_chatbot_llm_amd.engine.process_engine import ProcessAsyncEngine
-        engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device())
+        engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device() if on_gpu else None)
     else:
         engine = AsyncEngine(ecfg)
     log(f"engine ready in {time.perf_counter() - t0:.1f}s")
@@ -112,7 +119,7 @@ async def run(args, ps):
                 r = await wl.run_wave()
         log(f"warmup ({args.warmup} turns/conv): {r.seconds:.2f}s turns={r.turns} errors={r.errors}")
 
-    torch.cuda.synchronize()
+    sync()
     barrier()
     prof = None
     if os.environ.get("PENNY_PYPROFILE"):   # host-side cProfile of the serving event loop
@@ -132,7 +139,7 @@ async def run(args, ps):
             results.append(r)
             log(f"wave {k}: {r.seconds:.2f}s turns={r.turns} errors={r.errors} retrievals={r.retrievals} "
                 f"ttft_p50={1e3 * statistics.median(r.ttfts) if r.ttfts else float('nan'):.0f}ms")
-    torch.cuda.synchronize()
+    sync()
     barrier()
     elapsed = time.perf_counter() - t_start
     if prof is not None:
@@ -158,7 +165,7 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     from financial_chatbot_llm_amd.parallel.dist import init_distributed
-    ps = init_distributed(tp_size=1)
+    ps = init_distributed(tp_size=1, device_type=args.device)
     if ps.world_size != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ps.world_size}")
     res = asyncio.run(run(args, ps))
@@ -181,7 +188,7 @@ def main(argv=None) -> int:
             "dtype": "bf16" if args.dtype == "bf16" else "bf16 (fp8 e4m3 MoE experts)",
             "data": f"synthetic conversations + {args.corpus:,}-vector synthetic corpus per GPU; "
                     "random-init weights of the real architectures",
-            "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": "bge-base-en", "global_batch": args.convs * ps.world_size,
+            "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": args.embed_model, "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
                        "tool_steps": args.tool_steps,

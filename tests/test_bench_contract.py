@@ -1,0 +1,57 @@
+"""The driver contract of ``bench.py`` (task spec): ONE JSON line from rank 0 with the BASELINE.json
+metric, the whole-job aggregate ``value`` (total turns / max-over-ranks time), ``n_gpus`` =
+WORLD_SIZE, weak scaling and the dp parallelism label -- exercised on CPU with tiny models, single
+process and 2 ranks over gloo (the 8-GPU scaling run uses the same code path with RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--device", "cpu", "--model", "llama-tiny", "--embed-model", "bert-tiny", "--corpus", "2000", "--users",
+        "20", "--convs", "3", "--steps", "1", "--warmup", "1", "--respond-tokens", "4", "--max-model-len", "1024"]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out: str):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def _check(d, n):
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == n and d["steps"] == 1 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["unit"] == "turns/s"
+    assert d["config"]["parallelism"] == f"dp{n}" and d["config"]["global_batch"] == 3 * n
+    assert d["turn_errors"] == 0 and d["value"] > 0
+    # value = whole-job turns / max-over-ranks wall time of the K timed steps
+    assert abs(d["ms_per_step"] - 1e3 * (3 * n) / d["value"]) / d["ms_per_step"] < 0.02
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_process_json_contract():
+    r = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 1)
+
+
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_gloo_json_contract():
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=380, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1          # rank 0 only
+    _check(lines[0], 2)
