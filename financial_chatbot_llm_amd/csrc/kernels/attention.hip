@@ -494,7 +494,7 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int D, int NW, int NBUF>
+template <int D, int NW, int NBUF, bool HEAD_FAST>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -506,8 +506,15 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   static_assert(PIECES >= 1 && TILE % (1024 * NW) == 0, "tile must split evenly over the waves");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][K|V]
 
-  // causal tiles grow with their index: dispatch the longest first so they do not form the tail
-  const int s = blockIdx.z, h = blockIdx.y, tile = gridDim.x - 1 - blockIdx.x;
+  // causal tiles grow with their index: dispatch the longest first so they do not form the tail.
+  // HEAD_FAST grid (Hkv, tiles, seqs): with round-robin dispatch over the 8 XCDs every tile of a
+  // (sequence, kv head) lands on the same XCD, so its K/V blocks are fetched into one L2 and
+  // re-read from there by the other tiles (grid (tiles, Hkv, seqs) spreads them over all 8 L2s)
+  const int s = blockIdx.z;
+  const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
+  const int tile = HEAD_FAST ? gridDim.y - 1 - blockIdx.y : gridDim.x - 1 - blockIdx.x;
+  const int ntiles = HEAD_FAST ? gridDim.y : gridDim.x;
+  (void)ntiles;
   const int G = Hq / Hkv;
   const int TQ = NW * 32 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
@@ -614,12 +621,24 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   // 4-wave tile (a 256-row tile would be mostly padding)
   const bool big = (long)max_q_len * G > 128;
   const int TQ = (big ? 256 : 128) / G;
-  dim3 grid((max_q_len + TQ - 1) / TQ, Hkv, num_seqs);
+  const int ntiles = (max_q_len + TQ - 1) / TQ;
+  // XCD-per-kv-head order measured +5-47 % TF/s (profiles/r1_prefill_head_fast.txt: 457 -> 672 at
+  // 4 x 2048 causal, 687 -> 905 at 1 x 8192); PENNY_PREFILL_HEAD_FAST=0 restores tile-fastest
+  static const int head_fast_env = [] {
+    const char* v = getenv("PENNY_PREFILL_HEAD_FAST");
+    return v ? atoi(v) : 1;
+  }();
+  const bool head_fast = head_fast_env != 0;
+  dim3 grid(ntiles, Hkv, num_seqs);
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big)                                                                                                       \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens,  \
-                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \
-                       max_blocks, causal);                                                                        \
+  if (big && head_fast)                                                                                          \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), dim3(Hkv, ntiles, num_seqs), dim3(512), 0, stream,     \
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);                                              \
+  else if (big)                                                                                                  \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, false>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q,     \
+                       ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,    \
+                       Hkv, max_blocks, causal);                                                                   \
   else                                                                                                           \
     hipLaunchKernelGGL(prefill_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens,           \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \
