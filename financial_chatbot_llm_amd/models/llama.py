@@ -24,7 +24,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.dist import state as pstate
-from ..ops.gemm import GATEUP, interleave16, linear, tile_weight
+from ..ops.gemm import interleave16, linear, tile_weight, uses_tiled_weight
 from ..parallel.layers import shard_cols, shard_rows, shard_sections, vocab_range
 from .common import AttentionMetadata, KVCache, random_tensor
 from .configs import ModelConfig
@@ -129,14 +129,14 @@ class DecoderModel:
         """Fragment-tiled copies of the projections the decode MFMA kernels stream (QKV, O, the
         interleaved gate|up and the dense down-projection): +13.8 GB for Llama-3-8B next to 288 GB
         of HBM3E, against ~1.2 ms (split-K QKV/O/down) + the gate|up saving per B=128 decode step.
-        gate|up is only tiled where ``ops.gemm.GATEUP`` has a measured config for its shape."""
+        Only shapes some decode kernel has a measured config for are tiled (``uses_tiled_weight``)."""
         self.wt: Dict[str, torch.Tensor] = {}
         if self.device.type != "cuda":
             return
         for name, t in self.w.items():
             if t.dim() != 2 or t.shape[0] % 16 or t.shape[1] % 32:
                 continue
-            if name.endswith((".qkv", ".o", ".down")) or (name.endswith(".gate_up") and tuple(t.shape) in GATEUP):
+            if name.endswith((".qkv", ".o", ".down", ".gate_up")) and uses_tiled_weight(*t.shape):
                 self.wt[name] = tile_weight(t)
 
     def num_bytes(self) -> int:

@@ -150,6 +150,15 @@ SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
 }
 
 
+def uses_tiled_weight(N_: int, K: int) -> bool:
+    """Does any decode kernel stream a fragment-tiled copy of an [N, K] weight?  Only shapes with a
+    measured entry (``TUNING`` skinny, ``SPLITK``, ``GATEUP``) do; everything else stays on
+    hipBLASLt and a tiled copy would only take HBM from the KV pool (Llama-3-70B at TP=1: 62 GB)."""
+    if os.environ.get("PENNY_SPLITK", "1") == "force":
+        return True
+    return (N_, K) in TUNING or (N_, K) in SPLITK or (N_, K) in GATEUP
+
+
 def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
     """(S, nf) for a split-K launch of this shape, or None.  ``PENNY_SPLITK=0`` disables the
     path; ``PENNY_SPLITK=force`` takes it for any shape the kernel accepts (tests)."""
