@@ -200,14 +200,18 @@ def bench_skinny(dev) -> List[Dict]:
     return out
 
 
-def bench_splitk(dev, names=("qkv", "o", "down")) -> List[Dict]:
+SHAPES_8B = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
+SHAPES_70B = {"qkv": (10240, 8192), "o": (8192, 8192), "down": (8192, 28672)}
+
+
+def bench_splitk(dev, names=("qkv", "o", "down"), shapes=None) -> List[Dict]:
     """Mid-batch split-K GEMM (+ slab reduce) vs hipBLASLt on the Llama-3-8B decode projections.
 
     Weights rotate over enough copies (>= 768 MB) that every call streams W from HBM, not from
     the 256 MB Infinity Cache -- the situation of a 32-layer decode step."""
     from ..ops import gemm
     out = []
-    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
+    shapes = shapes or SHAPES_8B
     for name, (N, K) in shapes.items():
         if name not in names:
             continue
@@ -239,6 +243,10 @@ def bench_splitk(dev, names=("qkv", "o", "down")) -> List[Dict]:
                     row[f"s{S}nf{nf}_red_us"] = round(red, 1)
                     if best is None or us + red < best[1]:
                         best = ((S, nf), us + red, us)
+            S_, nf_ = best[0]
+            P = torch.empty((S_, M, N), dtype=torch.float32, device=dev)
+            row["best_rowmajor_gemm_us"] = round(timeit(
+                lambda: gemm.splitk_partials(x, ws[nxt()], N, S_, nf_, out=P, rowmajor=True), iters=copies * 2), 1)
             row["best"] = list(best[0])
             row["best_gemm_us"] = round(best[2], 1)
             row["best_total_us"] = round(best[1], 1)
@@ -250,13 +258,13 @@ def bench_splitk(dev, names=("qkv", "o", "down")) -> List[Dict]:
     return out
 
 
-def bench_gateup(dev) -> List[Dict]:
+def bench_gateup(dev, N: int = 28672, K: int = 4096) -> List[Dict]:
     """Fused gate|up + SiLU*up MFMA kernel vs hipBLASLt GEMM + silu_mul on the Llama-3-8B MLP
     (N = 2*14336, K = 4096), weights rotated so every call streams W from HBM."""
     from ..ops import activation, gemm
-    gemm.load_gemm_tuning("llama3-8b")   # the baseline runs the curated solutions, as in serving
+    if (N, K) == (28672, 4096):
+        gemm.load_gemm_tuning("llama3-8b")   # the baseline runs the curated solutions, as in serving
     out = []
-    N, K = 28672, 4096
     copies = max(2, (768 << 20) // (N * K * 2))
     ws = [torch.randn((N, K), device=dev).to(torch.bfloat16) for _ in range(copies)]
     wts = [gemm.tile_weight(w) for w in ws]
@@ -276,6 +284,8 @@ def bench_gateup(dev) -> List[Dict]:
         for nf in (4, 8):
             us = timeit(lambda: gemm.gateup_silu(x, wts[nxt()], N, nf, out=y), iters=copies * 2)
             row[f"nf{nf}_us"] = round(us, 1)
+            rm = timeit(lambda: gemm.gateup_silu(x, ws[nxt()], N, nf, out=y, rowmajor=True), iters=copies * 2)
+            row[f"rowmajor_nf{nf}_us"] = round(rm, 1)
             row[f"nf{nf}_GBps"] = round(N * K * 2 / us / 1e3, 1)
             if best is None or us < best[1]:
                 best = (nf, us)
@@ -338,7 +348,9 @@ def main(argv=None) -> int:
     for name in args.only.split(","):
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
-                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe}[name](dev)
+                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
+                "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
+                "gateup70b": lambda d: bench_gateup(d, 57344, 8192)}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

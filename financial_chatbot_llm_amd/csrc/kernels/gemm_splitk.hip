@@ -65,15 +65,21 @@ __device__ __forceinline__ void wait_stage(int younger) {
 // alias-scope metadata, which is what lets hipcc's waitcnt pass leave the younger stages' LDS-DMA
 // in flight -- without it the pass cannot tell them apart from this stage and drains vmcnt(0)
 // before the first ds_read of every stage (measured: the ring then degenerates to one stage).
-template <int FW, int TW, int WBYTES>
+template <int FW, int TW, int WBYTES, bool WROW>
 __device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (&acc)[FW][TW], int wa, int wb,
                                           int lane, int g, int col) {
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     Frag wf[FW], xf[TW];
 #pragma unroll
-    for (int f = 0; f < FW; ++f)
-      wf[f].u = *reinterpret_cast<const uint4*>(base + ((wa * FW + f) * 2 + kk) * 1024 + lane * 16);
+    for (int f = 0; f < FW; ++f) {
+      if constexpr (WROW) {   // row-major W staged like X: row r at r*128, swizzled 16-B chunks
+        const int r = (wa * FW + f) * 16 + col;
+        wf[f].u = *reinterpret_cast<const uint4*>(base + r * 128 + xswz(r, 4 * kk + g) * 16);
+      } else {
+        wf[f].u = *reinterpret_cast<const uint4*>(base + ((wa * FW + f) * 2 + kk) * 1024 + lane * 16);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       const int r = (wb * TW + t) * 16 + col;
@@ -90,7 +96,10 @@ __device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (
 // SILU: W is the 16-row-interleaved gate|up weight (ops/gemm.py interleave16) and S == 1; the
 // epilogue writes Y[m, f] = silu(gate) * up as bf16 [M, N/2] (ldy) instead of f32 slabs -- each
 // wave owns whole (gate, up) row-group pairs, so the pair meets in one lane's registers.
-template <int NF, int MT, int WA, bool SILU = false>
+// WROW: W is the plain row-major [N, K] weight (no fragment-tiled copy): its stage pieces are
+// 8 rows x 128 B with the same source-side XOR swizzle as X, so every glds instruction still reads
+// whole 128-B lines and the fragment reads stay conflict-free.
+template <int NF, int MT, int WA, bool SILU = false, bool WROW = false>
 __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restrict__ X, int ldx,
                                                              const bf16* __restrict__ Wt, int K,
                                                              float* __restrict__ P, int M, int N, int S,
@@ -127,7 +136,13 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
 #pragma unroll
   for (int i = 0; i < LOADS; ++i) {
     const int q = w * LOADS + i;
-    if (q < 2 * NF) {
+    if (q < 2 * NF && WROW) {
+      const int r = q * 8 + (lane >> 3);                    // weight row within the tile
+      const int c = xswz(r, lane & 7);
+      src[i] = reinterpret_cast<const char*>(Wt + (long)(n0 + r) * K + k0 + 8 * c);
+      step[i] = 128;       // 64 k per stage
+      dst[i] = q * 1024;
+    } else if (q < 2 * NF) {
       const int f = q >> 1, kk = q & 1;
       src[i] = reinterpret_cast<const char*>(Wt) +
                (((long)(n0 / 16 + f) * ksteps + k0 / 32 + kk) * 64 + lane) * 16;
@@ -166,7 +181,7 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
     // stages j+1 .. min(j+NBUF-2, nst-1) may stay in flight
     wait_stage<LOADS, NBUF - 2>(min(NBUF - 2, nst - 1 - j));
     if (j + NBUF - 1 < nst) stage(j + NBUF - 1);
-    stage_mma<FW, TW, WBYTES>(smem + (j % NBUF) * SBYTES, acc, wa, wb, lane, g, col);
+    stage_mma<FW, TW, WBYTES, WROW>(smem + (j % NBUF) * SBYTES, acc, wa, wb, lane, g, col);
   }
 
   if constexpr (SILU) {
@@ -236,16 +251,25 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 }
 
 template <int NF, int MT, int WA>
-int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, hipStream_t st) {
-  hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
-                     (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S);
+int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
+  if (wrow)
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, false, true>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
+  else
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
   return (int)hipGetLastError();
 }
 
 template <int NF, int MT, int WA>
-int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, hipStream_t st) {
-  hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
-                     (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
+int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
+                hipStream_t st) {
+  if (wrow)
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
+  else
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
   return (int)hipGetLastError();
 }
 
@@ -256,15 +280,15 @@ int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy,
 // N/(16*nf) = 224 (nf 8) or 448 (nf 4) workgroups.  Contract (checked): N % (16*nf) == 0,
 // nf in {4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0.
 PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
-                                     int nf, hipStream_t stream) {
+                                     int nf, int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 4 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
   const int mt = (M + 15) / 16;
 #define GU_CASE(MT_, WA4_, WA8_)                                                          \
   if (mt <= MT_) {                                                                      \
-    if (nf == 4) return launch_silu<4, MT_, WA4_>(X, ldx, Wt, K, Y, ldy, M, N, stream); \
-    return launch_silu<8, MT_, WA8_>(X, ldx, Wt, K, Y, ldy, M, N, stream);              \
+    if (nf == 4) return launch_silu<4, MT_, WA4_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream); \
+    return launch_silu<8, MT_, WA8_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);              \
   }
   GU_CASE(2, 2, 2)
   GU_CASE(4, 1, 2)
@@ -277,10 +301,10 @@ PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int
 }
 
 // Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
-// aligned (ldx % 8 == 0).  nf: W row groups per workgroup (2, 4, 6 or 8;
+// aligned (ldx % 8 == 0).  wrow: Wt is the row-major [N, K] weight instead of tile_weight's copy.  nf: W row groups per workgroup (2, 4, 6 or 8;
 // 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4).  P is [S, M, N] f32.
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
-                                hipStream_t stream) {
+                                int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 256 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
@@ -288,10 +312,10 @@ PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, v
   float* p = static_cast<float*>(P);
 #define SK_CASE(MT_, WA2_, WA4_, WA8_)                                                 \
   if (mt <= MT_) {                                                                     \
-    if (nf == 2) return launch<2, MT_, WA2_>(X, ldx, Wt, K, p, M, N, S, stream);       \
-    if (nf == 4) return launch<4, MT_, WA4_>(X, ldx, Wt, K, p, M, N, S, stream);       \
-    if (nf == 6) return launch<6, MT_, 2>(X, ldx, Wt, K, p, M, N, S, stream);          \
-    return launch<8, MT_, WA8_>(X, ldx, Wt, K, p, M, N, S, stream);                    \
+    if (nf == 2) return launch<2, MT_, WA2_>(X, ldx, Wt, K, p, M, N, S, wrow, stream); \
+    if (nf == 4) return launch<4, MT_, WA4_>(X, ldx, Wt, K, p, M, N, S, wrow, stream); \
+    if (nf == 6) return launch<6, MT_, 2>(X, ldx, Wt, K, p, M, N, S, wrow, stream);    \
+    return launch<8, MT_, WA8_>(X, ldx, Wt, K, p, M, N, S, wrow, stream);              \
   }
   // (NF + MT) even; wave split picked to minimise fragment reads per wave (NF/WA + MT/WB)
   SK_CASE(2, 2, 2, 2)

@@ -73,14 +73,18 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
     ``ops.rope_kv_write`` -- sums them in its own pass)."""
     M, K = x.shape
     N_ = w.shape[0]
-    if slabs and wt is not None and epilogue is None and residual is None:
+    # the decode kernels stream either the fragment-tiled copy or (DECODE_WEIGHTS == "rowmajor",
+    # or no copy was made) the row-major weight itself
+    src = wt if wt is not None else (w if w.is_contiguous() else None)
+    rowmajor = wt is None
+    if slabs and src is not None and epilogue is None and residual is None:
         cfg = splitk_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if cfg is not None:
-            return Slabs(splitk_partials(x, wt, N_, *cfg))
-    if epilogue == "silu" and wt is not None and residual is None:
+            return Slabs(splitk_partials(x, src, N_, *cfg, rowmajor=rowmajor))
+    if epilogue == "silu" and src is not None and residual is None:
         nf = gateup_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if nf is not None:
-            return gateup_silu(x, wt, N_, nf)
+            return gateup_silu(x, src, N_, nf, rowmajor=rowmajor)
     if skinny_ok(x, w, epilogue, wt):
         ntf, nw = _config(N_, K, epilogue)
         out_n = N_ // 2 if epilogue == "silu" else N_
@@ -147,16 +151,32 @@ SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     (6144, 4096): [(256, 4, 6)],                             # QKV: 96-row tiles -> 256 workgroups
     (4096, 4096): [(192, 4, 4)],                             # O (M=256: hipBLASLt is faster)
     (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
+    # Llama-3-70B (TP=1), streamed row-major (profiles/r1_splitk_70b.jsonl): down 1.2-1.9x hipBLASLt
+    # at M = 32..256; O 1.1-1.5x from M = 96 (S = 0: the library is as fast below that)
+    (8192, 28672): [(16, 4, 8), (48, 2, 4), (128, 8, 8), (256, 4, 8)],
+    (8192, 8192): [(64, 0, 0), (256, 4, 8)],
 }
+# shapes whose row-major stream measured as fast as the tiled copy: never tiled (70B: 48 GB saved)
+TILE_FREE = {(8192, 28672), (8192, 8192)}
+
+
+# "tiled": the decode kernels stream a fragment-tiled copy of each measured projection (made once
+# at load, ``tile_weight``; 3-10 % faster for gate|up); "rowmajor": they always stream the
+# row-major weights directly (no extra HBM).  Shapes without a tiled copy use row-major anyway.
+DECODE_WEIGHTS = os.environ.get("PENNY_DECODE_WEIGHTS", "tiled")
 
 
 def uses_tiled_weight(N_: int, K: int) -> bool:
     """Does any decode kernel stream a fragment-tiled copy of an [N, K] weight?  Only shapes with a
     measured entry (``TUNING`` skinny, ``SPLITK``, ``GATEUP``) do; everything else stays on
     hipBLASLt and a tiled copy would only take HBM from the KV pool (Llama-3-70B at TP=1: 62 GB)."""
+    if (N_, K) in TUNING:                 # the skinny kernel reads tiled weights only
+        return True
+    if DECODE_WEIGHTS == "rowmajor" or (N_, K) in TILE_FREE:
+        return False
     if os.environ.get("PENNY_SPLITK", "1") == "force":
         return True
-    return (N_, K) in TUNING or (N_, K) in SPLITK or (N_, K) in GATEUP
+    return (N_, K) in SPLITK or (N_, K) in GATEUP
 
 
 def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
@@ -167,7 +187,7 @@ def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
         return None
     for max_m, S, nf in SPLITK.get((N_, K), ()):
         if M <= max_m:
-            return S, nf
+            return (S, nf) if S > 0 else None
     if mode == "force":
         nf = 4 if N_ % 64 == 0 else 2
         for S in (4, 2, 1):
@@ -201,14 +221,15 @@ def gateup_config(M: int, N_: int, K: int) -> Optional[int]:
 
 
 def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """silu(x @ gate.T) * (x @ up.T) from the fragment-tiled interleave16 gate|up weight ``wt``."""
+                out: Optional[torch.Tensor] = None, rowmajor: bool = False) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) from the interleave16 gate|up weight: its fragment-tiled copy
+    ``wt`` or (``rowmajor``) the [N, K] weight itself."""
     M, K = x.shape
     if not N.use_native(x):
-        return silu_mul(F.linear(x, untile_weight(wt)), interleave16=True)
+        return silu_mul(F.linear(x, wt if rowmajor else untile_weight(wt)), interleave16=True)
     y = out if out is not None else torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
     N.call("penny_gateup_silu_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), y.stride(0), M, N_, nf,
-           N.stream())
+           int(rowmajor), N.stream())
     return y
 
 
@@ -231,15 +252,17 @@ class Slabs:
 
 
 def splitk_partials(x: torch.Tensor, wt: torch.Tensor, N_: int, S: int, nf: int,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """P[s] = x @ w[:, slice s].T as f32 slabs [S, M, N] (``wt`` = ``tile_weight(w)``)."""
+                    out: Optional[torch.Tensor] = None, rowmajor: bool = False) -> torch.Tensor:
+    """P[s] = x @ w[:, slice s].T as f32 slabs [S, M, N] (``wt`` = ``tile_weight(w)``, or ``w``
+    itself with ``rowmajor``)."""
     M, K = x.shape
     if not N.use_native(x):
-        w = untile_weight(wt).float()
+        w = (wt if rowmajor else untile_weight(wt)).float()
         xs = x.float().view(M, S, K // S).transpose(0, 1)
         return torch.einsum("smk,snk->smn", xs, w.view(N_, S, K // S).transpose(0, 1))
     P = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
-    N.call("penny_splitk_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(P), M, N_, S, nf, N.stream())
+    N.call("penny_splitk_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(P), M, N_, S, nf, int(rowmajor),
+           N.stream())
     return P
 
 

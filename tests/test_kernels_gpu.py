@@ -241,6 +241,8 @@ def test_splitk_gemm(M, S, nf):
     P = gemm.splitk_partials(x.to(DEV), wt, N_, S, nf)
     ref_p = (x.float().view(M, S, K // S).transpose(0, 1) @ w.float().view(N_, S, K // S).permute(1, 2, 0))
     close(P, ref_p, atol=1e-3)
+    # the row-major weight (no tiled copy) runs the identical MFMA sequence: bit-equal slabs
+    assert torch.equal(gemm.splitk_partials(x.to(DEV), w.to(DEV), N_, S, nf, rowmajor=True), P)
     close(gemm.splitk_reduce(P), x.float() @ w.float().t(), atol=2e-2)
     close(gemm.splitk_reduce(P, residual=res.to(DEV)), x.float() @ w.float().t() + res.float(), atol=3e-2)
     # strided X (a view into a wider activation buffer) is a supported input
@@ -289,6 +291,7 @@ def test_gateup_silu_gemm(M, nf):
     gate, up = rnd(Fr, K, scale=0.05, gen=g), rnd(Fr, K, scale=0.05, gen=g)
     wi = gemm.interleave16(gate, up).to(DEV).contiguous()
     y = gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, nf)
+    assert torch.equal(gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, nf, rowmajor=True), y)
     gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
     close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
     unfused = ops.silu_mul(torch.nn.functional.linear(x.to(DEV), wi), interleave16=True)
