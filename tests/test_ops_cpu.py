@@ -142,3 +142,36 @@ def test_splitk_slabs_cpu_reference_and_consumers():
     assert torch.equal(ops.rms_norm(Slabs(P), nw, 1e-5, residual=r1), ops.rms_norm(Slabs(P).materialize(), nw, 1e-5,
                                                                                    residual=r2))
     assert torch.equal(r1, r2)
+
+
+def test_decode_gemm_dispatch_tables(monkeypatch):
+    """Which decode kernel a projection shape gets, and whether it keeps a tiled weight copy."""
+    from financial_chatbot_llm_amd.ops import gemm
+    # Llama-3-8B: measured split-K / fused gate|up configs, tiled copies
+    assert gemm.splitk_config(128, 6144, 4096) == (4, 6)
+    assert gemm.splitk_config(300, 6144, 4096) is None              # prefill size: hipBLASLt
+    assert gemm.gateup_config(128, 28672, 4096) == 8 and gemm.gateup_config(200, 28672, 4096) is None
+    assert gemm.uses_tiled_weight(6144, 4096) and gemm.uses_tiled_weight(28672, 4096)
+    # Llama-3-70B: library below the measured crossover (S = 0), row-major stream above, no copies
+    assert gemm.splitk_config(32, 8192, 8192) is None and gemm.splitk_config(128, 8192, 8192) == (4, 8)
+    assert gemm.splitk_config(128, 8192, 28672) == (8, 8)
+    assert not gemm.uses_tiled_weight(8192, 28672) and not gemm.uses_tiled_weight(8192, 8192)
+    # unmeasured shapes stay on the library without copies unless forced
+    assert gemm.splitk_config(64, 1536, 256) is None and not gemm.uses_tiled_weight(1536, 256)
+    monkeypatch.setenv("PENNY_SPLITK", "force")
+    assert gemm.splitk_config(64, 1536, 256) is not None and gemm.uses_tiled_weight(1536, 256)
+
+
+def test_rowmajor_and_tiled_decode_gemm_agree_on_cpu():
+    """The CPU fallbacks of the split-K / gate|up kernels accept either weight form."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(5, 256, generator=g).to(torch.bfloat16)
+    w = torch.randn(64, 256, generator=g).to(torch.bfloat16)
+    P1 = gemm.splitk_partials(x, gemm.tile_weight(w), 64, 2, 2)
+    P2 = gemm.splitk_partials(x, w, 64, 2, 2, rowmajor=True)
+    assert torch.allclose(P1, P2)
+    wi = gemm.interleave16(w[:32], w[32:])
+    y1 = gemm.gateup_silu(x, gemm.tile_weight(wi), 64, 4)
+    y2 = gemm.gateup_silu(x, wi, 64, 4, rowmajor=True)
+    assert torch.equal(y1, y2)
