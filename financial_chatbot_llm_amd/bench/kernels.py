@@ -202,6 +202,7 @@ def bench_skinny(dev) -> List[Dict]:
 
 SHAPES_8B = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
 SHAPES_70B = {"qkv": (10240, 8192), "o": (8192, 8192), "down": (8192, 28672)}
+SHAPES_70B_TP8 = {"qkv": (1280, 8192), "o": (8192, 1024), "down": (8192, 3584)}   # per-rank shards
 
 
 def bench_splitk(dev, names=("qkv", "o", "down"), shapes=None) -> List[Dict]:
@@ -350,7 +351,9 @@ def main(argv=None) -> int:
                 "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
-                "gateup70b": lambda d: bench_gateup(d, 57344, 8192)}[name](dev)
+                "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
+                "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
+                "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192)}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

@@ -160,7 +160,9 @@ class DecoderModel:
                   kv: KVCache, reduce: bool = True) -> torch.Tensor:
         p = f"layers.{i}."
         T = h.shape[0]
-        qkv = linear(h, self.w[p + "qkv"], wt=self.wt.get(p + "qkv"), slabs=self.tp_size == 1)
+        # QKV is column-parallel: even under TP its split-K slabs go straight to the RoPE/KV-write
+        # pass (no all-reduce in between), unlike the row-parallel O / down projections
+        qkv = linear(h, self.w[p + "qkv"], wt=self.wt.get(p + "qkv"), slabs=True)
         kc, vc = kv.k(i), kv.v(i)
         q = ops.rope_kv_write(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv, self.D)
         attn = torch.empty_like(q)

@@ -155,9 +155,12 @@ SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     # at M = 32..256; O 1.1-1.5x from M = 96 (S = 0: the library is as fast below that)
     (8192, 28672): [(16, 4, 8), (48, 2, 4), (128, 8, 8), (256, 4, 8)],
     (8192, 8192): [(64, 0, 0), (256, 4, 8)],
+    # Llama-3-70B TP=8 per-rank QKV shard (column-parallel: the RoPE/KV-write pass consumes the
+    # slabs, no all-reduce in between): 1.6-2.4x hipBLASLt at M = 16..256 (r1_splitk_70b_tp8.jsonl)
+    (1280, 8192): [(256, 8, 4)],
 }
 # shapes whose row-major stream measured as fast as the tiled copy: never tiled (70B: 48 GB saved)
-TILE_FREE = {(8192, 28672), (8192, 8192)}
+TILE_FREE = {(8192, 28672), (8192, 8192), (1280, 8192)}
 
 
 # "tiled": the decode kernels stream a fragment-tiled copy of each measured projection (made once

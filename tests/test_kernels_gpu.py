@@ -252,6 +252,17 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])
+def test_splitk_rowmajor_tp_and_70b_shapes(N_, K, S, nf):
+    """The table shapes that stream the row-major weight (70B, TP=8 shards) vs the fp32 reference."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(8)
+    x = rnd(96, K, gen=g).to(DEV)
+    w = rnd(N_, K, scale=0.02, gen=g).to(DEV)
+    y = gemm.splitk_reduce(gemm.splitk_partials(x, w, N_, S, nf, rowmajor=True))
+    close(y, x.float() @ w.float().t(), atol=3e-2)
+
+
 @pytest.mark.parametrize("M,F", [(1, 384), (37, 14336), (300, 2048)])
 def test_silu_quant_rows_fp8_matches_two_pass(M, F):
     """Fused SiLU*up + per-row fp8 quantisation == silu_mul then quant_rows (same arithmetic)."""
