@@ -1,14 +1,19 @@
-"""Projection GEMMs: hand-written MFMA skinny GEMM for decode (M <= 64), hipBLASLt otherwise.
+"""Projection GEMMs: hand-written weight-streaming MFMA kernels for decode, hipBLASLt for prefill.
 
-``linear(x, w, epilogue=...)`` is the single entry point the models use:
+``linear(x, w, epilogue=..., wt=..., slabs=...)`` is the single entry point the models use.  For a
+decode-size M on the GPU, in order:
 
-* M <= 64 on the GPU -> ``penny_skinny_gemm`` (weight-streaming MFMA kernel, fused epilogues:
-  ``"silu"`` for the 16-row-interleaved gate|up weight, ``"residual"`` add);
-* otherwise (prefill) -> hipBLASLt via ``torch.nn.functional.linear`` followed by the matching
-  HIP epilogue kernel (``silu_mul(interleave16=True)``) or a fused add.
+* ``slabs=True`` and a ``SPLITK`` entry -> ``penny_splitk_gemm``: split-K f32 slabs left unreduced
+  for the consumer (RMSNorm / RoPE-KV-write sum them in their own row pass);
+* ``epilogue="silu"`` and a ``GATEUP`` entry -> ``penny_gateup_silu_gemm``: the interleaved
+  gate|up GEMM with SiLU(gate)*up fused into its epilogue;
+* a ``TUNING`` entry -> ``penny_skinny_gemm`` (M <= 16-32, fused SiLU / residual epilogues).
 
-Per-shape launch configs (rows per workgroup, waves per workgroup) come from ``TUNING`` --
-measured on MI355X with ``bench/kernels.py --only skinny`` -- with a heuristic fallback.
+These kernels stream either the fragment-tiled copy ``wt`` (``tile_weight``; made at load only
+for shapes with an entry, see ``uses_tiled_weight``) or the row-major weight itself.  Everything
+else (prefill-size M, unmeasured shapes) runs hipBLASLt via ``torch.nn.functional.linear``, plus
+the matching HIP epilogue kernel (``silu_mul(interleave16=True)``) or a fused add.  Every table
+entry was measured on MI355X with ``bench/kernels.py`` (profiles named next to each table).
 """
 from __future__ import annotations
 
