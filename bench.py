@@ -96,7 +96,9 @@ async def run(args, ps):
     sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
                         max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
-                        graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype)
+                        graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype,
+                        # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
+                        kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)))
     if args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
         from financial_chatbot_llm_amd.engine.process_engine import ProcessAsyncEngine
         engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device() if on_gpu else None)
