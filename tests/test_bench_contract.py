@@ -55,3 +55,19 @@ def test_bench_two_ranks_gloo_json_contract():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1          # rank 0 only
     _check(lines[0], 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_on_one_gpu_json_contract():
+    """The dpN bench path on the device: two ranks share cuda:0 (gloo control plane, each engine takes
+    a slice of HBM through PENNY_KV_FRACTION), tiny models through the HIP kernels."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", PENNY_DIST_BACKEND="gloo", PENNY_KV_FRACTION="0.05")
+    gpu_args = ["--device" if a == "--device" else ("cuda" if a == "cpu" else a) for a in ARGS]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *gpu_args]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 2)
