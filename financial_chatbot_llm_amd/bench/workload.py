@@ -93,7 +93,6 @@ class RagWorkload:
             doc = context_doc(rank * 100000 + i, uid, self.rng)
             self.db.put_context(doc)
             self.convs.append(doc)
-        self.ts = 1_700_000_000
         self.turn_of = [0] * num_convs            # next turn index per conversation
         self.conv_index = {d["conversation_id"]: i for i, d in enumerate(self.convs)}
 
@@ -102,8 +101,9 @@ class RagWorkload:
         doc, k = self.convs[i], self.turn_of[i]
         pool = SPEND_QUESTIONS if (i + k) % 2 == 0 else ADVICE_QUESTIONS
         text = pool[(i // 2 + k) % len(pool)]
-        self.ts += 1
-        self.db.put_user_message(doc["conversation_id"], text, doc["user_id"], self.ts)
+        # wall-clock seconds, like the AI replies saved by the worker (database.py:100): history is
+        # sorted by timestamp (database.py:77), so a synthetic clock would misorder the two senders
+        self.db.put_user_message(doc["conversation_id"], text, doc["user_id"], int(time.time()))
         self.kafka.producer.produce(config.USER_MESSAGE_TOPIC, key=doc["conversation_id"],
                                     value=json.dumps({"message": text, "conversation_id": doc["conversation_id"],
                                                       "user_id": doc["user_id"]}))
