@@ -56,6 +56,9 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--tool-steps", type=int, default=1,
                     help=">1: multi-step agent with the plot tool bound (north-star config 4)")
+    ap.add_argument("--no-tools", action="store_true",
+                    help="BASELINE config 2: single-turn chat without tools (legacy llm_service.py chain); "
+                         "no decide step, no retrieval")
     ap.add_argument("--arrival", default="closed", choices=["closed", "wave"],
                     help="closed: each conversation sends its next turn when its last completes (default); "
                          "wave: all conversations send in lock-step waves")
@@ -108,7 +111,7 @@ async def run(args, ps):
     llm = EngineLLM(engine, max_model_len=args.max_model_len, decide_script=decide_script,
                     respond_ignore_eos=True, respond_tokens=args.respond_tokens)
     wl = RagWorkload(llm, retrieval, args.convs, args.users, args.respond_tokens, rank=ps.rank,
-                     max_tool_steps=args.tool_steps)
+                     max_tool_steps=args.tool_steps, tools=not args.no_tools)
     wl.kafka.setup_consumer()
     consumer = asyncio.create_task(wl.worker.consume_messages())
 
@@ -123,6 +126,8 @@ async def run(args, ps):
 
     sync()
     barrier()
+    tok0 = {p: dict(v) for p, v in llm.token_stats.items()}
+    stats0 = engine.stats()
     prof = None
     if os.environ.get("PENNY_PYPROFILE"):   # host-side cProfile of the serving event loop
         import cProfile
@@ -152,10 +157,22 @@ async def run(args, ps):
     await consumer
     stats = engine.stats()
     engine.shutdown()
+    turns = sum(r.turns for r in results)
+    # prompt-token accounting of the timed turns (account for every prefill token)
+    tokens = {}
+    for p, v in llm.token_stats.items():
+        d = {k: v[k] - tok0.get(p, {}).get(k, 0) for k in v}
+        tokens[p] = {"calls": d["calls"], "prompt_per_turn": round(d["prompt"] / max(turns, 1), 1),
+                     "prefilled_per_turn": round(d["prefilled"] / max(turns, 1), 1),
+                     "cached_fraction": round(1 - d["prefilled"] / max(d["prompt"], 1), 3)}
+    tokens["prefilled_per_turn"] = round(sum(t["prefilled_per_turn"] for t in tokens.values()), 1)
+    tokens["kv_evictions"] = stats.get("kv_evictions", 0) - stats0.get("kv_evictions", 0)
+    tokens["preemptions"] = stats.get("preemptions", 0) - stats0.get("preemptions", 0)
     stages = {k: [v for r in results for v in r.stages.get(k, [])] for k in ("decide", "retrieval", "respond_first_token")}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
             "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
-            "stages": stages, "engine": stats}
+            "stages": stages, "engine": stats, "tokens": tokens,
+            "plots_ok": sum(r.plots_ok for r in results), "plots_failed": sum(r.plots_failed for r in results)}
 
 
 def main(argv=None) -> int:
@@ -193,15 +210,18 @@ def main(argv=None) -> int:
             "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": args.embed_model, "global_batch": args.convs * ps.world_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
-                       "tool_steps": args.tool_steps,
+                       "tool_steps": 0 if args.no_tools else args.tool_steps,
+                       "agent": "single-chain chat (no tools)" if args.no_tools else "tool-calling RAG agent",
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},
             "p50_ttft_ms": None if p50 is None else round(p50, 1),
             "p99_ttft_ms": None if p99 is None else round(p99, 1),
             "turn_errors": sum(r["errors"] for r in allr),
             "retrieval_turns": sum(r["retrievals"] for r in allr),
+            "plots": {"ok": sum(r["plots_ok"] for r in allr), "failed": sum(r["plots_failed"] for r in allr)},
             "ttft_p50_breakdown_ms": {k: round(1e3 * statistics.median(v), 1) if v else None
                                       for k, v in allr[0]["stages"].items()},
+            "prompt_tokens_rank0": allr[0]["tokens"],
             "engine_rank0": allr[0]["engine"],
         }
         line = json.dumps(out)

@@ -53,8 +53,15 @@ class _Cursor:
 
 
 class InMemoryCollection:
+    """Dict-backed collection.  Documents are indexed by ``conversation_id`` (every DAO query
+    filters on it), so a turn's ``find`` touches that conversation's documents only instead of
+    scanning (and deep-copying) the whole collection -- the bench ends with thousands of them."""
+
+    INDEXED = "conversation_id"
+
     def __init__(self):
         self._docs: List[Dict[str, Any]] = []
+        self._by_key: Dict[Any, List[Dict[str, Any]]] = {}
         self._lock = threading.Lock()
         self._next_id = 0
 
@@ -64,25 +71,32 @@ class InMemoryCollection:
             d.setdefault("_id", self._next_id)
             self._next_id += 1
             self._docs.append(d)
+            if self.INDEXED in d:
+                self._by_key.setdefault(d[self.INDEXED], []).append(d)
         return d["_id"]
 
     def insert_many(self, docs: Iterable[Dict[str, Any]]):
         return [self.insert_one(d) for d in docs]
 
+    def _candidates(self, flt: Mapping[str, Any]) -> List[Dict[str, Any]]:
+        if self.INDEXED in flt:
+            return self._by_key.get(flt[self.INDEXED], [])
+        return self._docs
+
     def find_one(self, flt: Mapping[str, Any]) -> Optional[Dict[str, Any]]:
         with self._lock:
-            for d in self._docs:
+            for d in self._candidates(flt):
                 if _match(d, flt):
                     return copy.deepcopy(d)
         return None
 
     def find(self, flt: Mapping[str, Any]) -> _Cursor:
         with self._lock:
-            return _Cursor([copy.deepcopy(d) for d in self._docs if _match(d, flt)])
+            return _Cursor([copy.deepcopy(d) for d in self._candidates(flt) if _match(d, flt)])
 
     def count_documents(self, flt: Mapping[str, Any]) -> int:
         with self._lock:
-            return sum(1 for d in self._docs if _match(d, flt))
+            return sum(1 for d in self._candidates(flt) if _match(d, flt))
 
 
 class InMemoryMongo:

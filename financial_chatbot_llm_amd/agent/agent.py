@@ -43,12 +43,14 @@ class AgentState(TypedDict):
     retrieved_transactions: List[str]
     final_response: Optional[str]
     tool_results: List[Dict[str, Any]]
+    transaction_records: List[Dict[str, Any]]   # structured rows of the hits (plot tool input)
 
 
 def initial_state(user_query: str, user_id: str, user_context: str, chat_history: Sequence[ChatMessage]) -> AgentState:
     return {"user_query": user_query, "user_id": user_id, "tool_calls": deque(),
             "user_context": user_context, "chat_history": list(chat_history),
-            "retrieved_transactions": [], "final_response": None, "tool_results": []}
+            "retrieved_transactions": [], "final_response": None, "tool_results": [],
+            "transaction_records": []}
 
 
 class LLMAgent:
@@ -56,7 +58,8 @@ class LLMAgent:
                  temperature: float = config.DEFAULT_TEMPERATURE, max_response_tokens: int = 512,
                  max_decide_tokens: int = 160, max_tool_steps: int = 1,
                  today_fn: Callable[[], _dt.date] = _dt.date.today,
-                 system_prompt: Optional[str] = None, tool_prompt: Optional[str] = None):
+                 system_prompt: Optional[str] = None, tool_prompt: Optional[str] = None,
+                 max_transaction_tokens: Optional[int] = config.MAX_TRANSACTION_TOKENS):
         self.llm = llm
         self.retrieval_tool = retrieval_tool
         self.tools: Dict[str, Tool] = {retrieval_tool.name: retrieval_tool}
@@ -69,6 +72,7 @@ class LLMAgent:
         self.max_response_tokens = max_response_tokens
         self.max_decide_tokens = max_decide_tokens
         self.max_tool_steps = max_tool_steps
+        self.max_transaction_tokens = max_transaction_tokens
         self.today_fn = today_fn
         self.system_prompt = system_prompt if system_prompt is not None else _load_system_prompt()
         self.tool_prompt = tool_prompt if tool_prompt is not None else _load_tool_prompt()
@@ -84,7 +88,11 @@ class LLMAgent:
         g.set_entry_point("decide_retrieval")
         g.add_conditional_edges("decide_retrieval", self._should_retrieve,
                                 {"retrieve": "retrieve_data", "respond": "generate_response"})
-        g.add_edge("retrieve_data", "generate_response")
+        if self.max_tool_steps > 1:   # multi-step agent: tool results go back to the decider
+            g.add_conditional_edges("retrieve_data", self._after_tool,
+                                    {"decide": "decide_retrieval", "respond": "generate_response"})
+        else:
+            g.add_edge("retrieve_data", "generate_response")
         g.add_edge("generate_response", END)
         return g.compile()
 
@@ -96,7 +104,15 @@ class LLMAgent:
         return build_messages(sp, ctx, state["chat_history"], state["user_query"])
 
     def respond_messages(self, state: AgentState) -> List[ChatMessage]:
-        ctx = respond_context(state["user_context"], state["retrieved_transactions"])
+        # token-budget step 1: the reference stuffs up to 10,000 hits
+        # (qdrant_tool.py:145, llm_agent.py:234-236); keep the best-scoring ones that fit
+        from ..engine.chat_template import clamp_transactions
+        txns = clamp_transactions(state["retrieved_transactions"], self.max_transaction_tokens,
+                                  self.llm.count_tokens)
+        if len(txns) < len(state["retrieved_transactions"]):
+            logger.info(f"Clamped {len(state['retrieved_transactions'])} transactions to {len(txns)} "
+                        f"({self.max_transaction_tokens} tokens)")
+        ctx = respond_context(state["user_context"], txns)
         if len(state["tool_results"]) > 1 or any(r["name"] != self.retrieval_tool.name for r in state["tool_results"]):
             extra = [l for l in self._tool_result_lines(state) if not l.startswith("[retrieve_transactions]")]
             if extra:
@@ -143,12 +159,14 @@ class LLMAgent:
             if tool is self.retrieval_tool:
                 args["user_id"] = state["user_id"]   # server-side id always wins (llm_agent.py:120)
             elif tc.name == "create_financial_plot" and "transactions_json" not in args:
-                args["transactions_json"] = json.dumps(
-                    [{"text": t} for t in state["retrieved_transactions"]])
+                # the reference tool plots a transactions JSON with real columns
+                # (plot_tool.py:29-63): hand it the structured rows of the retrieval hits
+                args["transactions_json"] = json.dumps(state.get("transaction_records") or [])
             result = await tool.ainvoke(args)
             state["tool_results"].append({"name": tc.name, "args": args, "result": result})
             if tool is self.retrieval_tool:
                 state["retrieved_transactions"] = list(result)
+                state["transaction_records"] = list(getattr(result, "records", []) or [])
                 logger.info(f"Retrieved {len(result)} transactions")
         except Exception as e:  # noqa: BLE001
             logger.error(f"Error retrieving transactions: {e}")
@@ -164,6 +182,9 @@ class LLMAgent:
         state["final_response"] = "".join(parts)
         logger.info("Final response generated")
         return state
+
+    def _after_tool(self, state: AgentState) -> Literal["decide", "respond"]:
+        return "decide" if len(state["tool_results"]) < self.max_tool_steps else "respond"
 
     def _should_retrieve(self, state: AgentState) -> Literal["retrieve", "respond"]:
         if len(state["tool_calls"]) > 0:
@@ -194,11 +215,19 @@ class LLMAgent:
         retrieved_any = False
         while self._should_retrieve(state) == "retrieve" and steps < self.max_tool_steps:
             yield {"type": "status", "message": "Retrieving relevant transaction data..."}
+            n_results = len(state["tool_results"])
             state = await self._retrieve_data_node(state)
             steps += 1
             retrieved_any = True
-            n = len(state["retrieved_transactions"])
-            yield {"type": "retrieval_complete", "count": n, "message": f"Retrieved {n} transactions"}
+            last = state["tool_results"][-1] if len(state["tool_results"]) > n_results else None
+            if last is not None and last["name"] != self.retrieval_tool.name:
+                res = last["result"]
+                ok = isinstance(res, str) and res.startswith("data:image/png;base64,")
+                yield {"type": "tool_complete", "name": last["name"], "ok": ok,
+                       "message": f"{last['name']} {'succeeded' if ok else 'failed'}"}
+            else:
+                n = len(state["retrieved_transactions"])
+                yield {"type": "retrieval_complete", "count": n, "message": f"Retrieved {n} transactions"}
             if steps < self.max_tool_steps:
                 state = await self._decide_retrieval_node(state)
         if not retrieved_any:

@@ -41,6 +41,10 @@ class LLMBackend:
                 max_tokens: int = 512, **kw) -> AsyncIterator[str]:
         raise NotImplementedError
 
+    def count_tokens(self, text: str) -> int:
+        """Prompt-budget estimate of ``text`` (backends with a tokenizer count exactly)."""
+        return len(text) // 4 + 1
+
 
 _RETRIEVAL_CUES = re.compile(
     r"\b(spen[dt]|spending|transactions?|purchases?|bought|paid|charges?|groceries|grocery|"

@@ -26,7 +26,7 @@ from typing import Dict, List, Optional
 
 from .. import config
 from ..adapters import Database, InMemoryBroker, KafkaClient
-from ..agent import LLMAgent, scripted_decision
+from ..agent import LLMAgent, LLMService, scripted_decision
 from ..agent.toolcall import format_tool_call
 from ..retrieval import RetrievalService
 from ..retrieval.store import MERCHANTS, user_name
@@ -73,19 +73,25 @@ class WaveResult:
     errors: int
     retrievals: int
     stages: Dict[str, List[float]] = field(default_factory=dict)   # TTFT anatomy per turn (s)
+    plots_ok: int = 0
+    plots_failed: int = 0
 
 
 class RagWorkload:
     """Owns the fakes, the worker and the synthetic conversations for one GPU replica."""
 
     def __init__(self, llm, retrieval: RetrievalService, num_convs: int, num_users: int,
-                 respond_tokens: int, seed: int = 0, rank: int = 0, max_tool_steps: int = 1):
+                 respond_tokens: int, seed: int = 0, rank: int = 0, max_tool_steps: int = 1,
+                 tools: bool = True):
         self.rng = random.Random(seed * 7919 + rank)
         self.broker = InMemoryBroker(num_partitions=16)
         self.db = Database(uri="")
         self.kafka = KafkaClient(broker=self.broker)
-        self.agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
-                              max_response_tokens=respond_tokens, max_tool_steps=max_tool_steps)
+        if tools:
+            self.agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
+                                  max_response_tokens=respond_tokens, max_tool_steps=max_tool_steps)
+        else:   # BASELINE config 2: legacy single-chain chat (llm_service.py), no decide/retrieval
+            self.agent = LLMService(llm, max_response_tokens=respond_tokens)
         self.worker = ChatWorker(self.db, self.kafka, self.agent, max_concurrent_turns=4 * num_convs)
         self.convs = []
         for i in range(num_convs):
@@ -135,8 +141,7 @@ class RagWorkload:
                     self._send(i)
         dt = time.perf_counter() - t0
         traces = self.worker.traces[n0:target]
-        return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
-                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces), ttft_stages(traces))
+        return _result(dt, traces)
 
     async def run_wave(self) -> WaveResult:
         n0 = len(self.worker.traces)
@@ -147,8 +152,13 @@ class RagWorkload:
             await asyncio.sleep(0.002)
         dt = time.perf_counter() - t0
         traces = self.worker.traces[n0:target]
-        return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
-                          sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces), ttft_stages(traces))
+        return _result(dt, traces)
+
+
+def _result(dt: float, traces) -> WaveResult:
+    return WaveResult(dt, [t.ttft for t in traces if t.ttft is not None], len(traces),
+                      sum(t.error for t in traces), sum(t.retrieved > 0 for t in traces), ttft_stages(traces),
+                      plots_ok=sum(t.tools_ok for t in traces), plots_failed=sum(t.tools_failed for t in traces))
 
 
 def ttft_stages(traces) -> Dict[str, List[float]]:
@@ -166,8 +176,11 @@ def ttft_stages(traces) -> Dict[str, List[float]]:
     return out
 
 
-PLOT_CALL = ToolCall("create_financial_plot", {"plot_config": {"plot_type": "bar", "x_axis": "date",
-                                                                "title": "Spending"}})
+# spending per category over the retrieved rows (the retrieval tool hands the plot tool the
+# hits' structured columns: date, amount, merchant, category)
+PLOT_CALL = ToolCall("create_financial_plot", {"plot_config": {"plot_type": "bar", "x_axis": "category",
+                                                                "y_axis": "amount", "group_by": "category",
+                                                                "title": "Spending by category"}})
 
 
 def decide_script(messages, tools) -> str:

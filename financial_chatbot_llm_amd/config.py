@@ -44,6 +44,7 @@ KAFKA_SESSION_TIMEOUT_MS = "45000"  # kafka_client.py:15
 DEFAULT_TEMPERATURE = 0.5          # llm_agent.py:37,44
 RETRIEVAL_DEFAULT_LIMIT = 10000    # tools/qdrant_tool.py:145
 RETRIEVAL_HNSW_EF = 128            # tools/qdrant_tool.py:99 (we search exactly; kept for API parity)
+MAX_TRANSACTION_TOKENS = 3000      # token-budget clamp of stuffed transactions (new)
 
 
 def _env(name: str, default: str = "") -> str:
@@ -154,8 +155,10 @@ class RetrievalConfig:
     embed_model: str = "bge-base-en"
     corpus_size: int = 1_000_000
     num_users: int = 10_000
-    limit_default: int = RETRIEVAL_DEFAULT_LIMIT
-    max_limit_tokens: int = 3000            # token-budget clamp for stuffed transactions
+    max_limit_tokens: int = MAX_TRANSACTION_TOKENS   # clamp of stuffed transactions
+    weights: Optional[str] = None           # bge safetensors dir (None: random init)
+    vocab: Optional[str] = None             # BERT vocab.txt / tokenizer.json (None: hashed word ids)
+    corpus_path: Optional[str] = None       # JSONL/Parquet transactions or a store snapshot to load
     device: str = "cuda"
 
     @classmethod
@@ -164,6 +167,10 @@ class RetrievalConfig:
             embed_model=_env("PENNY_EMBED_MODEL", cls.embed_model),
             corpus_size=_env_int("PENNY_CORPUS_SIZE", cls.corpus_size),
             num_users=_env_int("PENNY_CORPUS_USERS", cls.num_users),
+            max_limit_tokens=_env_int("PENNY_MAX_TRANSACTION_TOKENS", cls.max_limit_tokens),
+            weights=os.getenv("PENNY_EMBED_WEIGHTS") or None,
+            vocab=os.getenv("PENNY_EMBED_VOCAB") or None,
+            corpus_path=os.getenv("PENNY_CORPUS_PATH") or None,
             device=_env("PENNY_DEVICE", cls.device),
         )
         return dataclasses.replace(c, **overrides)
@@ -178,8 +185,11 @@ class ServingConfig:
     temperature: float = DEFAULT_TEMPERATURE
     max_response_tokens: int = 512
     max_decide_tokens: int = 96
-    history_token_budget: int = 4096        # oldest messages dropped past this
+    # history beyond this many tokens is cut oldest-first in prefix-stable steps;
+    # None: only what max_model_len forces (the reference re-sends the whole history)
+    history_token_budget: Optional[int] = None
     backend: str = "engine"                 # "engine" | "stub"
+    tools: bool = True                      # False: legacy single-chain chat, no decide step (A9)
 
     @classmethod
     def from_env(cls, **overrides) -> "ServingConfig":
@@ -187,7 +197,10 @@ class ServingConfig:
             port=_env_int("PORT", cls.port),
             max_concurrent_turns=_env_int("PENNY_MAX_CONCURRENT_TURNS", cls.max_concurrent_turns),
             max_response_tokens=_env_int("PENNY_MAX_RESPONSE_TOKENS", cls.max_response_tokens),
+            max_decide_tokens=_env_int("PENNY_MAX_DECIDE_TOKENS", cls.max_decide_tokens),
+            history_token_budget=(_env_int("PENNY_HISTORY_TOKEN_BUDGET", 0) or None),
             backend=_env("PENNY_BACKEND", cls.backend),
+            tools=_env_bool("PENNY_TOOLS", True),
         )
         return dataclasses.replace(c, **overrides)
 

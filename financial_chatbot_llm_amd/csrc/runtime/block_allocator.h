@@ -64,6 +64,7 @@ class BlockAllocator {
   int block_size() const { return bs_; }
   long hits() const { return hits_; }
   long queries() const { return queries_; }
+  long evictions() const { return evictions_; }
 
   int blocks_needed(int seq, int total_tokens) const {
     auto it = seqs_.find(seq);
@@ -211,6 +212,7 @@ class BlockAllocator {
     } else if (lru_head_ >= 0) {
       b = lru_head_;
       lru_remove(b);
+      ++evictions_;
       Block& blk = blocks_[b];
       auto it = cache_.find(blk.hash);
       if (it != cache_.end() && it->second == b) cache_.erase(it);
@@ -253,7 +255,7 @@ class BlockAllocator {
   std::unordered_map<uint64_t, int> cache_;
   std::unordered_map<int, SeqState> seqs_;
   int lru_head_ = -1, lru_tail_ = -1, lru_size_ = 0;
-  long hits_ = 0, queries_ = 0;
+  long hits_ = 0, queries_ = 0, evictions_ = 0;
 };
 
 }  // namespace penny

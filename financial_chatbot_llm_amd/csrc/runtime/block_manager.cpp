@@ -26,5 +26,6 @@ PYBIND11_MODULE(_penny_runtime, m) {
       .def("usage", &BlockAllocator::usage)
       .def("check_invariants", &BlockAllocator::check_invariants)
       .def_property_readonly("hits", &BlockAllocator::hits)
-      .def_property_readonly("queries", &BlockAllocator::queries);
+      .def_property_readonly("queries", &BlockAllocator::queries)
+      .def_property_readonly("evictions", &BlockAllocator::evictions);
 }

@@ -17,7 +17,7 @@ from ..agent.toolcall import parse_tool_calls
 from ..tools.base import Tool
 from ..wire import ChatMessage
 from .async_engine import AsyncEngine
-from .chat_template import encode_chat
+from .chat_template import ChatEncoder
 from .sequence import SamplingParams
 from .tokenizer import IncrementalDetokenizer
 
@@ -26,19 +26,37 @@ class EngineLLM(LLMBackend):
     def __init__(self, engine: AsyncEngine, max_model_len: int = 8192,
                  decide_script: Optional[Callable[[Sequence[ChatMessage], Sequence[Tool]], str]] = None,
                  respond_ignore_eos: bool = False, respond_tokens: Optional[int] = None,
-                 stream_chunk_tokens: int = 1):
+                 stream_chunk_tokens: int = 1, history_token_budget: Optional[int] = None):
         self.engine = engine
         self.tok = engine.tokenizer
+        self.encoder = ChatEncoder(self.tok)
         self.max_model_len = max_model_len
+        self.history_token_budget = history_token_budget
         self.decide_script = decide_script
         self.respond_ignore_eos = respond_ignore_eos
         self.respond_tokens = respond_tokens
         self.stream_chunk_tokens = max(1, stream_chunk_tokens)
         self.eot = self.tok.special.get("<|eot_id|>")
         self.last_prompt_tokens = 0
+        # per-purpose prompt accounting: calls, prompt tokens, tokens actually prefilled
+        # (prompt - prefix-cache hits + preemption recomputes), generated tokens
+        self.token_stats = {p: {"calls": 0, "prompt": 0, "prefilled": 0, "generated": 0}
+                            for p in ("decide", "respond")}
+
+    def _account(self, purpose: str, prompt_len: int, seq) -> None:
+        st = self.token_stats.setdefault(purpose, {"calls": 0, "prompt": 0, "prefilled": 0, "generated": 0})
+        st["calls"] += 1
+        st["prompt"] += prompt_len
+        # prefill chunks also cover forced tokens appended after the prompt (jump-forward)
+        st["prefilled"] += min(getattr(seq, "num_prefilled", 0), prompt_len)
+        st["generated"] += len(seq.output_ids)
+
+    def count_tokens(self, text: str) -> int:
+        return self.encoder.count(text)
 
     def _encode(self, messages, tools, max_tokens) -> list:
-        ids = encode_chat(self.tok, messages, tools, max_prompt_tokens=self.max_model_len - max_tokens - 1)
+        ids = self.encoder.encode(messages, tools, max_prompt_tokens=self.max_model_len - max_tokens - 1,
+                                  history_token_budget=self.history_token_budget)
         self.last_prompt_tokens = len(ids)
         return ids
 
@@ -51,6 +69,7 @@ class EngineLLM(LLMBackend):
             forced = self.tok.encode(text, allow_special=False)[: max_tokens - 1] + ([self.eot] if self.eot is not None else [])
         params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced)
         out = await self.engine.generate_all(ids, params)
+        self._account(kw.get("purpose", "decide"), len(ids), out.seq)
         text = self.tok.decode(out.seq.output_ids)
         return LLMResult(text=text, tool_calls=parse_tool_calls(text, tools), prompt_tokens=len(ids),
                          completion_tokens=len(out.seq.output_ids))
@@ -64,6 +83,8 @@ class EngineLLM(LLMBackend):
         async for o in self.engine.generate(ids, params):
             buf.append(detok.push(o.new_token_ids))
             k += 1
+            if o.finished:
+                self._account(kw.get("purpose", "respond"), len(ids), o.seq)
             if k % self.stream_chunk_tokens == 0 or o.finished:
                 text = "".join(buf)
                 buf = []

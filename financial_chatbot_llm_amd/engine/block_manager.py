@@ -35,6 +35,7 @@ class PyBlockManager:
         self.seq_hashes: Dict[int, List[int]] = {}
         self.hits = 0
         self.queries = 0
+        self.evictions = 0          # cached blocks recycled (their prefix KV lost)
 
     # -- capacity ------------------------------------------------------------------------
     def num_free(self) -> int:
@@ -52,6 +53,7 @@ class PyBlockManager:
             b = self.free_list.pop()
         elif self.evictable:
             b, _ = self.evictable.popitem(last=False)
+            self.evictions += 1
             h = self.hash_of[b]
             if h is not None and self.cache.get(h) == b:
                 del self.cache[h]

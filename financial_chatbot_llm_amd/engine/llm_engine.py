@@ -291,6 +291,8 @@ class LLMEngine:
     def stats(self) -> Dict[str, float]:
         return {"running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
                 "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
+                "kv_blocks": self.bm.num_blocks, "kv_evictions": int(getattr(self.bm, "evictions", 0)),
+                "preemptions": self.scheduler.num_preemptions,
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
                 "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),

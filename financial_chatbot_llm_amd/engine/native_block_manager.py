@@ -25,6 +25,10 @@ class NativeBlockManager:
     def queries(self) -> int:
         return self.core.queries
 
+    @property
+    def evictions(self) -> int:
+        return self.core.evictions
+
     def num_free(self) -> int:
         return self.core.num_free()
 

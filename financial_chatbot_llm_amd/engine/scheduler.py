@@ -102,6 +102,7 @@ class Scheduler:
             if not self.bm.grow(seq, seq.num_computed + n):
                 continue
             batch.prefill.append((seq, seq.num_computed, n))
+            seq.num_prefilled += n
             budget -= n
         # 3) admit waiting sequences
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
@@ -119,6 +120,7 @@ class Scheduler:
             seq.status = SeqStatus.RUNNING
             self.running.append(seq)
             batch.prefill.append((seq, seq.num_computed, n))
+            seq.num_prefilled += n
             budget -= n
         return batch
 

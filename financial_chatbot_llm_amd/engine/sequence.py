@@ -43,6 +43,7 @@ class Sequence:
         self.block_table: List[int] = []
         self.num_computed = 0          # tokens whose KV is in the cache
         self.num_cached_prompt = 0     # prefix-cache hit (tokens)
+        self.num_prefilled = 0         # tokens run through prefill chunks (recomputes included)
         self.arrival = time.perf_counter() if arrival is None else arrival
         self.first_token_time: Optional[float] = None
         self.finish_reason: Optional[str] = None

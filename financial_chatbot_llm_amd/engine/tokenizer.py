@@ -205,17 +205,35 @@ class SyntheticWordPiece:
 
 
 class IncrementalDetokenizer:
-    """Turns a growing list of token ids into text deltas without splitting UTF-8 sequences."""
+    """Turns a growing list of token ids into text deltas without splitting characters.
+
+    Byte-level vocabularies (the synthetic one): buffer bytes, emit the longest valid UTF-8
+    prefix.  ``tokenizers`` vocabularies (:class:`HFTokenizer`): decoding a token on its own is
+    wrong twice over -- a character split across byte-level BPE tokens decodes to U+FFFD, and a
+    Metaspace/SentencePiece decoder drops a lone token's leading space.  So keep every id and
+    decode a sliding window ``ids[prefix:]`` against ``ids[prefix:read]`` (the window already
+    emitted); emit the new suffix only once it does not end in an incomplete character."""
 
     def __init__(self, tokenizer: BaseTokenizer, skip_special: bool = True):
         self.tk = tokenizer
         self.skip = tokenizer._special_ids if skip_special else set()
         self.pending = b""
+        self.ids: List[int] = []
+        self.prefix = 0          # window start: context tokens re-decoded for spacing
+        self.read = 0            # tokens whose text has been emitted
+
+    def _push_hf(self, ids: Iterable[int]) -> str:
+        self.ids.extend(i for i in ids if i not in self.skip)
+        done = self.tk.decode(self.ids[self.prefix:self.read], skip_special=True)
+        full = self.tk.decode(self.ids[self.prefix:], skip_special=True)
+        if len(full) > len(done) and not full.endswith("\ufffd"):
+            self.prefix, self.read = self.read, len(self.ids)
+            return full[len(done):]
+        return ""
 
     def push(self, ids: Iterable[int]) -> str:
         if isinstance(self.tk, HFTokenizer):
-            text = self.tk.decode([i for i in ids if i not in self.skip], skip_special=True)
-            return text
+            return self._push_hf(ids)
         self.pending += self.tk.decode_bytes(i for i in ids if i not in self.skip)
         # emit the longest valid UTF-8 prefix
         for cut in range(len(self.pending), max(len(self.pending) - 4, -1), -1):
@@ -230,6 +248,11 @@ class IncrementalDetokenizer:
         return text
 
     def flush(self) -> str:
+        if isinstance(self.tk, HFTokenizer):
+            done = self.tk.decode(self.ids[self.prefix:self.read], skip_special=True)
+            full = self.tk.decode(self.ids[self.prefix:], skip_special=True)
+            self.prefix = self.read = len(self.ids)
+            return full[len(done):]
         text = self.pending.decode("utf-8", errors="replace")
         self.pending = b""
         return text

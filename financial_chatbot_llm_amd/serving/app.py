@@ -3,7 +3,8 @@
 Endpoints:
 * ``GET /health`` -> ``{"status": "healthy"}`` (``main.py:51-53``; Docker HEALTHCHECK target).
 * ``POST /process_message`` -- the reference's commented-out sync endpoint (``main.py:39-49``),
-  re-enabled: ``{conversation_id, message, user_id}`` -> ``{response, retrieved_transactions_count}``.
+  re-enabled: ``{conversation_id, message, user_id}`` -> ``{response, retrieved_transactions_count}``;
+  ``user_id`` must be the conversation's owner (403 otherwise) -- retrieval uses the stored id.
 * ``POST /v1/chat/stream`` -- server-sent events of the agent's updates for one turn (no Kafka);
   used for latency probing.
 * ``GET /metrics`` -- Prometheus text: turns/s, TTFT p50/p99, ITL, KV utilisation, ...
@@ -100,9 +101,13 @@ def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
 
     @app.post("/process_message")
     async def process_message_endpoint(payload: MessagePayload):
-        user_context, _ = await services.db.get_context(payload.conversation_id)
+        user_context, user_id = await services.db.get_context(payload.conversation_id)
+        # retrieval is filtered by this id: it must be the conversation owner's (server-side,
+        # as llm_agent.py:119-120 does for the tool args), never a caller-chosen one
+        if payload.user_id != user_id:
+            return JSONResponse({"detail": "user_id does not own this conversation"}, status_code=403)
         chat_history = await services.db.get_history(payload.conversation_id)
-        res = await services.agent.query(payload.message, payload.user_id, user_context, chat_history)
+        res = await services.agent.query(payload.message, user_id, user_context, chat_history)
         return {"response": res["response"], "retrieved_transactions_count": res["retrieved_transactions_count"]}
 
     @app.post("/v1/chat/stream")

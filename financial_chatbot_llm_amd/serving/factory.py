@@ -11,10 +11,14 @@ from typing import Any, Optional
 
 from .. import config
 from ..adapters import Database, InMemoryBroker, KafkaClient
-from ..agent import LLMAgent, StubLLM
+from ..agent import LLMAgent, LLMService, StubLLM
 from ..retrieval import HashEmbedder, NumpyVectorStore, RetrievalService
 from ..tools import make_plot_tool, make_retrieval_tool
 from .app import Services
+
+
+def retrieval_limit_tokens() -> int:
+    return config.RetrievalConfig.from_env().max_limit_tokens
 
 
 def build_stub_services(broker: Optional[InMemoryBroker] = None, db: Optional[Database] = None,
@@ -26,10 +30,15 @@ def build_stub_services(broker: Optional[InMemoryBroker] = None, db: Optional[Da
     embedder = embedder or HashEmbedder(768)
     store = store or NumpyVectorStore(embedder.dim)
     retrieval = RetrievalService(embedder, store)
-    agent = LLMAgent(llm or StubLLM(), make_retrieval_tool(retrieval),
-                     extra_tools=[make_plot_tool()], temperature=serving.temperature,
-                     max_response_tokens=serving.max_response_tokens, max_tool_steps=max_tool_steps,
-                     today_fn=today_fn)
+    llm = llm or StubLLM()
+    if not serving.tools:
+        agent = LLMService(llm, temperature=serving.temperature, max_response_tokens=serving.max_response_tokens)
+    else:
+        agent = LLMAgent(llm, make_retrieval_tool(retrieval),
+                         extra_tools=[make_plot_tool()], temperature=serving.temperature,
+                         max_response_tokens=serving.max_response_tokens,
+                         max_decide_tokens=serving.max_decide_tokens, max_tool_steps=max_tool_steps,
+                         today_fn=today_fn, max_transaction_tokens=retrieval_limit_tokens())
     return Services(db=db, kafka=kafka, agent=agent, retrieval=retrieval, serving=serving)
 
 
@@ -51,10 +60,15 @@ def build_engine_services(engine_cfg: Optional[config.EngineConfig] = None,
     if retrieval_cfg.corpus_size:
         store.load_synthetic(retrieval_cfg.corpus_size, retrieval_cfg.num_users)
     retrieval = RetrievalService(embedder, store)
-    llm = EngineLLM(engine, max_model_len=engine_cfg.max_model_len)
-    agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
-                     temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
-                     max_tool_steps=max_tool_steps)
+    llm = EngineLLM(engine, max_model_len=engine_cfg.max_model_len,
+                    history_token_budget=serving.history_token_budget)
+    if not serving.tools:
+        agent = LLMService(llm, temperature=serving.temperature, max_response_tokens=serving.max_response_tokens)
+    else:
+        agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
+                         temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
+                         max_decide_tokens=serving.max_decide_tokens, max_tool_steps=max_tool_steps,
+                         max_transaction_tokens=retrieval_cfg.max_limit_tokens)
     return Services(db=db or Database(), kafka=KafkaClient(broker=broker), agent=agent,
                     engine=engine, retrieval=retrieval, serving=serving)
 

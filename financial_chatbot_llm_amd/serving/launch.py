@@ -10,8 +10,10 @@ The reference scales by running N gunicorn worker processes that each consume Ka
 (``gunicorn.conf.py:8-9``, ``main.py:131-138``).  Here each TP-group LEADER owns one engine
 replica and one Kafka consumer in the same group (Kafka spreads partitions across replicas, per
 key ordering preserved); its event loop runs hundreds of concurrent turns that batch inside the
-engine.  Non-leader TP ranks replay the leader's steps (``LLMEngine.follower_loop``).  The global
-rank 0 additionally serves the FastAPI surface (``/health``, ``/metrics``, ...) on ``--port``.
+engine.  Non-leader TP ranks replay the leader's steps (``LLMEngine.follower_loop``).  EVERY
+replica leader also serves the FastAPI surface (``/health``, ``/process_message``,
+``/v1/chat/stream``, ``/metrics``, ...) on ``--port + dp_rank`` -- as every reference gunicorn
+worker serves HTTP (``gunicorn.conf.py:8-9``); a load balancer spreads requests over the ports.
 """
 from __future__ import annotations
 
@@ -35,6 +37,8 @@ def parse(argv=None):
     ap.add_argument("--users", type=int, default=int(os.environ.get("PENNY_CORPUS_USERS", "10000")))
     ap.add_argument("--port", type=int, default=int(os.environ.get("PORT", "8000")))
     ap.add_argument("--tool-steps", type=int, default=1, help=">1 enables the multi-step agent (retrieval + plot)")
+    ap.add_argument("--no-tools", action="store_true",
+                    help="legacy single-chain chat (llm_service.py): no decide step, no retrieval")
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--device", default=None)
     ap.add_argument("--no-http", action="store_true")
@@ -44,7 +48,7 @@ def parse(argv=None):
 
 def build_leader_services(args, engine, device):
     from ..adapters import Database, InMemoryBroker, KafkaClient
-    from ..agent import LLMAgent
+    from ..agent import LLMAgent, LLMService
     from ..engine.backend import EngineLLM
     from ..retrieval import BgeEmbedder, DeviceVectorStore, HashEmbedder, NumpyVectorStore, RetrievalService
     from ..tools import make_plot_tool, make_retrieval_tool
@@ -59,11 +63,14 @@ def build_leader_services(args, engine, device):
         embedder = HashEmbedder(768)
         store = NumpyVectorStore(768)
     retrieval = RetrievalService(embedder, store)
-    llm = EngineLLM(engine, max_model_len=args.max_model_len)
     serving = config.ServingConfig.from_env()
-    agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
-                     temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
-                     max_tool_steps=args.tool_steps)
+    llm = EngineLLM(engine, max_model_len=args.max_model_len, history_token_budget=serving.history_token_budget)
+    if args.no_tools or not serving.tools:
+        agent = LLMService(llm, temperature=serving.temperature, max_response_tokens=serving.max_response_tokens)
+    else:
+        agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
+                         temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
+                         max_decide_tokens=serving.max_decide_tokens, max_tool_steps=args.tool_steps)
     broker = InMemoryBroker() if args.smoke else None
     return Services(db=Database(uri="" if args.smoke else None), kafka=KafkaClient(broker=broker), agent=agent,
                     engine=engine, retrieval=retrieval, serving=serving)
@@ -120,10 +127,12 @@ def main(argv=None) -> int:
         return 0 if last.get("type") == "complete" else 1
     from .app import create_app
     app = create_app(services)
-    if ps.rank == 0 and not args.no_http:
+    if not args.no_http:
         import uvicorn
-        uvicorn.run(app, host="0.0.0.0", port=args.port, log_level="warning")
-    else:  # other DP replicas: Kafka consumer only (lifespan without HTTP)
+        port = args.port + ps.dp_rank
+        logger.info(f"replica {ps.dp_rank} serving HTTP on :{port}")
+        uvicorn.run(app, host="0.0.0.0", port=port, log_level="warning")
+    else:  # Kafka consumer only (lifespan without HTTP)
         async def run_headless():
             async with app.router.lifespan_context(app):
                 await asyncio.Event().wait()

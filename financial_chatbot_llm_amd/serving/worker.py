@@ -35,7 +35,7 @@ class ChatWorker:
         self.message_timeout_s = message_timeout_s
         self.metrics = metrics
         self._sem = asyncio.Semaphore(max_concurrent_turns)
-        self._conv_locks: Dict[str, asyncio.Lock] = {}
+        self._conv_locks: Dict[str, list] = {}   # cid -> [lock, users]
         self._tasks: Set[asyncio.Task] = set()
         self._stop = asyncio.Event()
         self.traces = []
@@ -67,6 +67,9 @@ class ChatWorker:
                     self.kafka.produce_message(config.AI_RESPONSE_TOPIC, conversation_id, complete_event(value))
                     trace.t_complete = now()
                     logger.info(f"Complete message sent to Kafka for conversation {conversation_id}")
+                elif kind == "tool_complete":
+                    trace.tools_ok += int(bool(update.get("ok")))
+                    trace.tools_failed += int(not update.get("ok"))
                 elif kind == "retrieval_complete":
                     trace.retrieved = int(update.get("count", 0))
                     trace.mark("retrieval_done")
@@ -96,29 +99,42 @@ class ChatWorker:
             cid = value.get("conversation_id", "")
         except Exception:  # noqa: BLE001
             value, cid = None, ""
-        lock = self._conv_locks.setdefault(cid, asyncio.Lock())
+        # per-conversation lock, reference-counted: the entry lives while ANY task of the
+        # conversation holds or awaits it (a waiter still queued on the semaphore is not in the
+        # lock's waiter list, so "no waiters" is not "no users")
+        entry = self._conv_locks.get(cid)
+        if entry is None:
+            entry = self._conv_locks[cid] = [asyncio.Lock(), 0]
+        entry[1] += 1
+        lock = entry[0]
         trace = TurnTrace(conversation_id=cid)
-        async with self._sem, lock:
+        try:
+            async with lock, self._sem:
+                await self._handle_locked(message, value, trace)
+        finally:
+            entry[1] -= 1
+            if entry[1] == 0 and self._conv_locks.get(cid) is entry:
+                del self._conv_locks[cid]
+
+    async def _handle_locked(self, message, value, trace: TurnTrace) -> None:
+        try:
+            await asyncio.wait_for(self.process_message(message, trace), timeout=self.message_timeout_s)
+        except asyncio.TimeoutError:
+            logger.error(f"Message processing timed out after {self.message_timeout_s} seconds")
+            trace.error = True
             try:
-                await asyncio.wait_for(self.process_message(message, trace), timeout=self.message_timeout_s)
-            except asyncio.TimeoutError:
-                logger.error(f"Message processing timed out after {self.message_timeout_s} seconds")
-                trace.error = True
-                try:
-                    if value is None:
-                        raise ValueError("undecodable message")
-                    self.kafka.produce_error_message(config.AI_RESPONSE_TOPIC, value["conversation_id"],
-                                                     timeout_event(value))
-                except Exception as e:  # noqa: BLE001
-                    logger.error(f"Failed to send timeout error message: {e}")
+                if value is None:
+                    raise ValueError("undecodable message")
+                self.kafka.produce_error_message(config.AI_RESPONSE_TOPIC, value["conversation_id"],
+                                                 timeout_event(value))
             except Exception as e:  # noqa: BLE001
-                logger.error(f"Error in message consumption: {e}")
-                trace.error = True
-            finally:
-                self.metrics.record_turn(trace)
-                self.traces.append(trace)
-                if not lock.locked() and cid in self._conv_locks and not lock._waiters:  # type: ignore[attr-defined]
-                    self._conv_locks.pop(cid, None)
+                logger.error(f"Failed to send timeout error message: {e}")
+        except Exception as e:  # noqa: BLE001
+            logger.error(f"Error in message consumption: {e}")
+            trace.error = True
+        finally:
+            self.metrics.record_turn(trace)
+            self.traces.append(trace)
 
     async def consume_messages(self) -> None:
         blocking_poll = getattr(self.kafka, "backend", "memory") != "memory"

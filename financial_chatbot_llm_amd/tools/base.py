@@ -7,9 +7,8 @@ validates the arguments the way LangChain's ``args_schema`` does, then calls the
 from __future__ import annotations
 
 import inspect
-import json
 from dataclasses import dataclass, field
-from typing import Any, Awaitable, Callable, Dict, List, Optional, Type
+from typing import Any, Awaitable, Callable, Dict, Optional, Type
 
 from pydantic import BaseModel
 
@@ -60,28 +59,3 @@ class Tool:
         if inspect.isawaitable(res):
             res = await res
         return res
-
-
-class ToolRegistry:
-    def __init__(self, tools: Optional[List[Tool]] = None):
-        self._tools: Dict[str, Tool] = {}
-        for t in tools or []:
-            self.register(t)
-
-    def register(self, tool: Tool) -> None:
-        self._tools[tool.name] = tool
-
-    def get(self, name: str) -> Tool:
-        return self._tools[name]
-
-    def __contains__(self, name: str) -> bool:
-        return name in self._tools
-
-    def __iter__(self):
-        return iter(self._tools.values())
-
-    def declarations(self) -> List[Dict[str, Any]]:
-        return [t.function_declaration() for t in self._tools.values()]
-
-    def declarations_json(self) -> str:
-        return "\n\n".join(json.dumps(d, indent=4) for d in self.declarations())

@@ -97,6 +97,12 @@ def _invoke(transactions_json: str, plot_config: Dict[str, Any]) -> str:
     return create_financial_plot(transactions_json, plot_config)
 
 
+async def _ainvoke(transactions_json: str, plot_config: Dict[str, Any]) -> str:
+    # matplotlib rendering takes tens of ms of CPU: off the serving event loop
+    import asyncio
+    return await asyncio.to_thread(_invoke, transactions_json, plot_config)
+
+
 def make_plot_tool() -> Tool:
     return Tool(name="create_financial_plot", description=PLOT_TOOL_DESCRIPTION,
-                args_schema=PlotArgs, func=_invoke)
+                args_schema=PlotArgs, func=_invoke, coroutine=_ainvoke)

@@ -16,7 +16,7 @@ Semantics preserved:
 from __future__ import annotations
 
 import datetime as _dt
-from typing import List, Optional
+from typing import Any, Dict, List, Optional
 
 from pydantic import BaseModel, ConfigDict, Field
 
@@ -66,15 +66,35 @@ def effective_limit(num_transactions: Optional[int]) -> int:
     return num_transactions if num_transactions is not None else config.RETRIEVAL_DEFAULT_LIMIT
 
 
+class TransactionList(list):
+    """The tool's return value: a plain ``list`` of ``page_content`` strings, exactly as the
+    reference (``qdrant_tool.py:159-172``), carrying the hits' structured metadata alongside in
+    ``records`` (date as ``YYYY-MM-DD``, amount, merchant, category, ...; ``user_id`` dropped) so
+    the plot tool gets real columns (``plot_tool.py:29-63``)."""
+
+    records: List[Dict[str, Any]]
+
+
+def transaction_record(payload: Dict[str, Any]) -> Dict[str, Any]:
+    meta = dict(payload.get("metadata", {}))
+    meta.pop("user_id", None)
+    if isinstance(meta.get("date"), (int, float)):
+        meta["date"] = _dt.datetime.fromtimestamp(int(meta["date"])).strftime("%Y-%m-%d")
+    meta.setdefault("description", payload.get("page_content", ""))
+    return meta
+
+
 def make_retrieval_tool(service) -> Tool:
     """Bind the tool to a RetrievalService (sync ``invoke`` and async ``ainvoke`` paths)."""
 
     def _post(user_id: str, hits) -> List[str]:
-        out, skipped = [], 0
+        out, skipped = TransactionList(), 0
+        out.records = []
         for h in hits:
             meta = (h.payload or {}).get("metadata", {}) if h.payload else {}
             if h.payload and meta.get("user_id") == user_id:
                 out.append(h.payload["page_content"])
+                out.records.append(transaction_record(h.payload))
             else:
                 skipped += 1
         if skipped:

@@ -29,6 +29,8 @@ class TurnTrace:
     n_chunks: int = 0
     chunk_times: List[float] = field(default_factory=list)
     retrieved: int = 0
+    tools_ok: int = 0            # non-retrieval tool calls that succeeded (plots rendered)
+    tools_failed: int = 0
     error: bool = False
 
     def mark(self, stage: str) -> None:

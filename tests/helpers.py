@@ -26,10 +26,11 @@ def seeded_store(now=None):
     emb = HashEmbedder(64)
     store = NumpyVectorStore(64)
     now = int(time.time()) if now is None else now
-    texts = [("u1", "grocery store purchase Whole Foods $54.20", now - 86400),
-             ("u1", "grocery purchase Safeway $12.00", now - 40 * 86400),
-             ("u1", "Netflix subscription $15.99", now - 2 * 86400),
-             ("u2", "grocery purchase Trader Joes $33.00", now - 86400)]
-    store.add(emb.embed([t for _, t, _ in texts]), [u for u, _, _ in texts], [d for _, _, d in texts],
-              [{"page_content": t, "metadata": {"user_id": u, "date": d}} for u, t, d in texts])
+    texts = [("u1", "grocery store purchase Whole Foods $54.20", now - 86400, 54.20, "Groceries"),
+             ("u1", "grocery purchase Safeway $12.00", now - 40 * 86400, 12.00, "Groceries"),
+             ("u1", "Netflix subscription $15.99", now - 2 * 86400, 15.99, "Entertainment"),
+             ("u2", "grocery purchase Trader Joes $33.00", now - 86400, 33.00, "Groceries")]
+    store.add(emb.embed([t[1] for t in texts]), [t[0] for t in texts], [t[2] for t in texts],
+              [{"page_content": t, "metadata": {"user_id": u, "date": d, "amount": a, "category": c}}
+               for u, t, d, a, c in texts])
     return emb, store

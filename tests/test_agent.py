@@ -77,14 +77,35 @@ def test_query_graph_path():
 
 
 def test_multi_step_with_plot():
+    cfg = {"plot_type": "bar", "x_axis": "category", "y_axis": "amount", "group_by": "category", "title": "t"}
     calls = [ToolCall("retrieve_transactions", {"search_query": "grocery"}),
-             ToolCall("create_financial_plot", {"plot_config": {"plot_type": "bar", "x_axis": "text", "title": "t"}}),
-             None]
+             ToolCall("create_financial_plot", {"plot_config": cfg}), None]
     llm = StubLLM(decisions=calls, responses=["done"])
     agent = make_agent(llm, max_tool_steps=3)
     ups = collect(agent.stream_with_status("plot my groceries", "u1", "CTX", []))
-    assert sum(u["type"] == "retrieval_complete" for u in ups) == 2
+    assert sum(u["type"] == "retrieval_complete" for u in ups) == 1
+    plots = [u for u in ups if u["type"] == "tool_complete"]
+    assert len(plots) == 1 and plots[0]["ok"], plots
     assert set(llm.calls[0]["tools"]) == {"retrieve_transactions", "create_financial_plot"}
+    # the plot saw the hits' structured columns (reference plot_tool.py:29-63), not raw text
+    res = asyncio.run(make_agent(StubLLM(decisions=list(calls), responses=["done"]), max_tool_steps=3)
+                      .query("plot my groceries", "u1", "CTX", []))
+    plot = [r for r in res["state"]["tool_results"] if r["name"] == "create_financial_plot"][0]
+    assert plot["result"].startswith("data:image/png;base64,")
+    import json
+    rows = json.loads(plot["args"]["transactions_json"])
+    assert {"date", "amount", "category"} <= set(rows[0]) and "user_id" not in rows[0]
+
+
+def test_transaction_clamp_keeps_best_scoring_rows():
+    calls = [ToolCall("retrieve_transactions", {"search_query": "grocery"})]
+    llm = StubLLM(decisions=calls, responses=["ok"])
+    agent = make_agent(llm, max_transaction_tokens=12)     # ~1 row at len/4 tokens per row
+    res = asyncio.run(agent.query("What did I spend on groceries?", "u1", "CTX", []))
+    assert res["retrieved_transactions_count"] == 3
+    sysmsg = llm.calls[1]["messages"][0].content
+    block = sysmsg.split("Retrieved Transaction Data:\n", 1)[1]
+    assert block == res["state"]["retrieved_transactions"][0]     # only the top hit fits
 
 
 def test_tool_call_parser():

@@ -120,6 +120,78 @@ def test_http_surface():
     asyncio.run(main())
 
 
+def test_process_message_rejects_foreign_user_id():
+    """A caller cannot read another user's transactions by naming their user_id (retrieval is
+    filtered by the conversation owner's id, as the tool's server-side injection intends)."""
+    llm = StubLLM(decisions=[ToolCall("retrieve_transactions", {"search_query": "grocery"})], responses=["x"])
+    svc = services(llm, convs=(("c1", "u1"), ("c2", "u2")))
+    svc.db.put_user_message("c2", "groceries?", "u2", 1)
+    app = create_app(svc, start_consumer=False)
+
+    async def main():
+        async with app.router.lifespan_context(app):
+            transport = httpx.ASGITransport(app=app)
+            async with httpx.AsyncClient(transport=transport, base_url="http://t") as cl:
+                r = await cl.post("/process_message", json={"conversation_id": "c2", "message": "What did I spend on groceries?",
+                                                            "user_id": "u1"})
+                assert r.status_code == 403
+                assert not llm.calls                       # nothing ran, nothing retrieved
+                r = await cl.post("/process_message", json={"conversation_id": "c2", "message": "What did I spend on groceries?",
+                                                            "user_id": "u2"})
+                assert r.status_code == 200 and r.json()["retrieved_transactions_count"] == 1   # u2's one row
+    asyncio.run(main())
+
+
+def test_conversation_lock_survives_saturated_semaphore():
+    """Turns of one conversation never overlap, even when the second turn is still queued on the
+    concurrency semaphore while the first finishes (lock entry dropped too early)."""
+    active, overlaps = {}, []
+
+    class Probe(StubLLM):
+        async def agenerate(self, messages, tools=None, **kw):
+            cid = messages[-1].content.split()[-1]
+            active[cid] = active.get(cid, 0) + 1
+            overlaps.append(active[cid])
+            await asyncio.sleep(0.01)
+            active[cid] -= 1
+            return await super().agenerate(messages, tools, **kw)
+
+    convs = [(f"c{i}", f"u{i}") for i in range(4)]
+    svc = services(Probe(), convs=convs)
+
+    async def main():
+        svc.kafka.setup_consumer()
+        w = ChatWorker(svc.db, svc.kafka, svc.agent, max_concurrent_turns=1)
+        task = asyncio.create_task(w.consume_messages())
+        msgs = [(c, f"hello {c}", u, k) for k in range(3) for c, u in convs]
+        for m in msgs:
+            send(svc, *m)
+        for _ in range(1000):
+            await asyncio.sleep(0.01)
+            if len(w.traces) >= len(msgs) and not w._tasks:
+                break
+        w.stop()
+        await task
+        return w
+    w = asyncio.run(main())
+    assert len(w.traces) == 12 and not any(t.error for t in w.traces)
+    assert max(overlaps) == 1 and not w._conv_locks
+
+
+def test_no_tools_service_single_chain():
+    """Legacy LLMService (llm_service.py:8-33): one respond call, no decide, SYSTEM_PROMPT verbatim."""
+    from financial_chatbot_llm_amd.agent import LLMService
+    llm = StubLLM(responses=["plain answer"])
+    svc = services(llm)
+    svc.agent = LLMService(llm, system_prompt="SYS")
+    drive(svc, [("c1", "What did I spend on groceries?")])
+    ev = out(svc, "c1")
+    assert "".join(e["message"] for e in ev if e.get("type") == "response_chunk") == "plain answer"
+    assert ev[-1]["type"] == "complete"
+    assert [c["kind"] for c in llm.calls] == ["stream"]
+    assert llm.calls[0]["messages"][0].content.startswith("SYS\nMy name is Ada.")
+
+
 # ---- fault injection in the fakes (SURVEY §5.3: drop, delay, raise) ------------------------------
 def test_fault_poll_errors_back_off_and_recover(monkeypatch):
     """Consumer-loop errors are logged and retried after the backoff (main.py:157-159); the turn
