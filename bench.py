@@ -59,6 +59,8 @@ def parse(argv=None):
     ap.add_argument("--no-tools", action="store_true",
                     help="BASELINE config 2: single-turn chat without tools (legacy llm_service.py chain); "
                          "no decide step, no retrieval")
+    ap.add_argument("--no-jump-forward", action="store_true",
+                    help="decode grammar-forced tool-call tokens one step each (A/B of jump-forward decoding)")
     ap.add_argument("--arrival", default="closed", choices=["closed", "wave"],
                     help="closed: each conversation sends its next turn when its last completes (default); "
                          "wave: all conversations send in lock-step waves")
@@ -109,9 +111,11 @@ async def run(args, ps):
         engine = AsyncEngine(ecfg)
     log(f"engine ready in {time.perf_counter() - t0:.1f}s")
     llm = EngineLLM(engine, max_model_len=args.max_model_len, decide_script=decide_script,
-                    respond_ignore_eos=True, respond_tokens=args.respond_tokens)
+                    respond_ignore_eos=True, respond_tokens=args.respond_tokens,
+                    jump_forward=not args.no_jump_forward)
     wl = RagWorkload(llm, retrieval, args.convs, args.users, args.respond_tokens, rank=ps.rank,
                      max_tool_steps=args.tool_steps, tools=not args.no_tools)
+    wl.progress = log
     wl.kafka.setup_consumer()
     consumer = asyncio.create_task(wl.worker.consume_messages())
 
@@ -211,6 +215,7 @@ def main(argv=None) -> int:
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
                        "tool_steps": 0 if args.no_tools else args.tool_steps,
+                       "decide_decoding": "tool-call grammar, jump-forward" if not args.no_jump_forward else "token by token",
                        "agent": "single-chain chat (no tools)" if args.no_tools else "tool-calling RAG agent",
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},

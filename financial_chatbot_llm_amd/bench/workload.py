@@ -84,6 +84,7 @@ class RagWorkload:
                  respond_tokens: int, seed: int = 0, rank: int = 0, max_tool_steps: int = 1,
                  tools: bool = True):
         self.rng = random.Random(seed * 7919 + rank)
+        self.progress = None       # callable(str): heartbeat for long runs
         self.broker = InMemoryBroker(num_partitions=16)
         self.db = Database(uri="")
         self.kafka = KafkaClient(broker=self.broker)
@@ -130,8 +131,12 @@ class RagWorkload:
         for i in range(len(self.convs)):
             self._send(i)
         seen, target = n0, n0 + turns_per_conv * len(self.convs)
+        t_log = t0
         while seen < target:
             await asyncio.sleep(0.002)
+            if self.progress is not None and time.perf_counter() - t_log > 30:
+                t_log = time.perf_counter()
+                self.progress(f"closed loop: {seen - n0}/{target - n0} turns in {t_log - t0:.0f}s")
             new = self.worker.traces[seen:]
             seen += len(new)
             for tr in new:

@@ -7,11 +7,17 @@
 ``decide_script`` (benchmarks / demos with random weights) supplies the decide step's text per
 turn; the engine still runs every forward pass and teacher-forces those tokens (forced decoding),
 so the compute matches a real model producing that output (SURVEY §6 'scripted tool decision').
+
+Decide outputs follow the tool-call grammar (``agent.grammar``): tokens the grammar forces (the
+JSON skeleton, the tool name, unambiguous keys, the closing braces) are appended without
+sampling and computed as one chunk (jump-forward decoding) -- for scripted and sampled outputs
+alike; ``jump_forward=False`` decodes them one step each.
 """
 from __future__ import annotations
 
 from typing import AsyncIterator, Callable, Optional, Sequence
 
+from ..agent.grammar import ToolCallGrammar, jump_mask
 from ..agent.llm import LLMBackend, LLMResult
 from ..agent.toolcall import parse_tool_calls
 from ..tools.base import Tool
@@ -26,12 +32,14 @@ class EngineLLM(LLMBackend):
     def __init__(self, engine: AsyncEngine, max_model_len: int = 8192,
                  decide_script: Optional[Callable[[Sequence[ChatMessage], Sequence[Tool]], str]] = None,
                  respond_ignore_eos: bool = False, respond_tokens: Optional[int] = None,
-                 stream_chunk_tokens: int = 1, history_token_budget: Optional[int] = None):
+                 stream_chunk_tokens: int = 1, history_token_budget: Optional[int] = None,
+                 jump_forward: bool = True):
         self.engine = engine
         self.tok = engine.tokenizer
         self.encoder = ChatEncoder(self.tok)
         self.max_model_len = max_model_len
         self.history_token_budget = history_token_budget
+        self.jump_forward = jump_forward
         self.decide_script = decide_script
         self.respond_ignore_eos = respond_ignore_eos
         self.respond_tokens = respond_tokens
@@ -63,11 +71,15 @@ class EngineLLM(LLMBackend):
     async def agenerate(self, messages, tools=None, temperature=0.5, max_tokens=256, **kw) -> LLMResult:
         tools = list(tools or [])
         ids = self._encode(messages, tools, max_tokens)
-        forced = None
+        forced = jump = None
+        grammar = ToolCallGrammar(tools) if (tools and self.jump_forward) else None
         if self.decide_script is not None:
             text = self.decide_script(messages, tools)
             forced = self.tok.encode(text, allow_special=False)[: max_tokens - 1] + ([self.eot] if self.eot is not None else [])
-        params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced)
+            if grammar is not None:
+                jump = jump_mask(forced, self.tok.decode, grammar, self.eot)
+        params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced,
+                                forced_jump=jump, grammar=grammar)
         out = await self.engine.generate_all(ids, params)
         self._account(kw.get("purpose", "decide"), len(ids), out.seq)
         text = self.tok.decode(out.seq.output_ids)

@@ -119,19 +119,55 @@ class LLMEngine:
         """Rows of a batch that sample a token, in sampled-vector order."""
         return [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
 
-    def _ends_after(self, seq: Sequence, tok: Optional[int]) -> bool:
-        """Will the token about to be sampled certainly finish ``seq``?  (tok: known forced token)"""
-        k = len(seq.output_ids) + 1
+    def _ends_after(self, seq: Sequence, tok: Optional[int], run: int = 1) -> bool:
+        """Will the token(s) about to be appended certainly finish ``seq``?  ``tok``: the known
+        last token of the run (None: sampled), ``run``: tokens appended at once (jump-forward)."""
+        k = len(seq.output_ids) + run
         p = seq.params
-        if k >= p.max_tokens or seq.num_tokens + 1 >= self.cfg.max_model_len:
+        if k >= p.max_tokens or seq.num_tokens + run >= self.cfg.max_model_len:
             return True
         if p.forced_output is not None and k >= len(p.forced_output) and not p.ignore_eos:
             return True
         return tok is not None and not p.ignore_eos and (tok in self.eos_ids or tok in p.stop_token_ids)
 
+    def _known_run(self, seq: Sequence) -> List[int]:
+        """Tokens known at launch time for the sampler row of ``seq``: a teacher-forced token
+        plus the grammar-forced tokens that follow it (jump-forward), or the grammar-forced run
+        staged by the previous resolve.  Empty: the token must be sampled."""
+        p = seq.params
+        k = len(seq.output_ids)
+        room = max(p.max_tokens - k, 1)   # never append past max_tokens
+        if seq.jump_queue:
+            run, seq.jump_queue = seq.jump_queue, []
+            return run[:room]
+        forced = p.forced_output
+        if forced is None or k >= len(forced):
+            return []
+        run = [forced[k]]
+        jump = p.forced_jump
+        if jump is not None:
+            j = k + 1
+            while j < len(forced) and j < len(jump) and jump[j]:
+                run.append(forced[j])
+                j += 1
+        return run[:room]
+
+    def _stage_grammar(self, seq: Sequence) -> None:
+        """After a SAMPLED token: stage the output grammar's forced continuation (if any)."""
+        g = seq.params.grammar
+        if g is None or seq.params.forced_output is not None:
+            return
+        forced, ends = g.forced(self.tokenizer.decode(seq.output_ids))
+        run = self.tokenizer.encode(forced, allow_special=False) if forced else []
+        if ends and self.eos_ids:
+            run.append(self.tokenizer.special.get("<|eot_id|>", next(iter(self.eos_ids))))
+        seq.jump_queue = run
+
     def _advance(self, batch, samplers: List[Sequence]) -> None:
         """Host view of an in-flight step as if it had completed: KV written (num_computed), full
-        blocks committed, one placeholder token per sampler (device-gathered by the next step)."""
+        blocks committed, one placeholder token per sampler (device-gathered by the next step)
+        -- or the known run of tokens (teacher-forced / grammar-forced), appended at once; a
+        run longer than one token is computed as a prefill chunk by the next step."""
         for seq, start, n in batch.prefill:
             if not seq.finished:
                 seq.num_computed = start + n
@@ -141,18 +177,34 @@ class LLMEngine:
         for i, seq in enumerate(samplers):
             if seq.finished:
                 continue
-            forced = seq.params.forced_output
-            k = len(seq.output_ids)
-            tok = forced[k] if forced is not None and k < len(forced) else None
-            if self._ends_after(seq, tok):
+            run = self._known_run(seq)
+            tok = run[-1] if run else None
+            if self._ends_after(seq, tok, max(len(run), 1)):
                 seq.awaiting = True            # sits out the next step; resolved by _resolve
+                seq.jump_tail = run
+            elif run:
+                seq.output_ids.extend(run)
+                seq.pending_src = -1
+                seq.last_run = run
             else:
-                seq.output_ids.append(PENDING if tok is None else tok)
-                seq.pending_src = i if tok is None else -1
+                seq.output_ids.append(PENDING)
+                seq.pending_src = i
             self.bm.commit(seq)
         for seq, start, n in batch.prefill:
             if not seq.finished and start + n < seq.num_tokens:
                 self.bm.commit(seq)
+
+    def _finish_reason(self, seq: Sequence, tok: int) -> Optional[str]:
+        forced = seq.params.forced_output
+        if len(seq.output_ids) >= seq.params.max_tokens:
+            return "length"
+        if forced is not None and len(seq.output_ids) >= len(forced) and not seq.params.ignore_eos:
+            return "stop"
+        if not seq.params.ignore_eos and (tok in self.eos_ids or tok in seq.params.stop_token_ids):
+            return "stop"
+        if seq.num_tokens >= self.cfg.max_model_len:
+            return "length"
+        return None
 
     def _resolve(self, samplers: List[Sequence], sampled: List[int]) -> List[StepOutput]:
         now = time.perf_counter()
@@ -160,35 +212,32 @@ class LLMEngine:
         for seq, tok in zip(samplers, sampled):
             if seq.finished:                   # aborted (or finished) while in flight
                 continue
-            forced = seq.params.forced_output
+            was_sampled = False
             if seq.awaiting:
                 seq.awaiting = False
-                k = len(seq.output_ids)
-                tok = forced[k] if forced is not None and k < len(forced) else int(tok)
-                seq.output_ids.append(tok)
+                new = seq.jump_tail or [int(tok)]
+                seq.jump_tail = []
+                seq.output_ids.extend(new)
             elif seq.pending_src >= 0:
-                tok = int(tok)
-                seq.output_ids[-1] = tok
+                new = [int(tok)]
+                seq.output_ids[-1] = new[0]
                 seq.pending_src = -1
-            else:                              # forced token, appended at launch time
-                tok = seq.output_ids[-1]
+                was_sampled = True
+            else:                              # known run, appended at launch time
+                new = seq.last_run or [seq.output_ids[-1]]
+                seq.last_run = []
+            tok = new[-1]
             if seq.first_token_time is None:
                 seq.first_token_time = now
-            reason = None
-            if len(seq.output_ids) >= seq.params.max_tokens:
-                reason = "length"
-            elif forced is not None and len(seq.output_ids) >= len(forced) and not seq.params.ignore_eos:
-                reason = "stop"
-            elif not seq.params.ignore_eos and (tok in self.eos_ids or tok in seq.params.stop_token_ids):
-                reason = "stop"
-            elif seq.num_tokens >= self.cfg.max_model_len:
-                reason = "length"
+            reason = self._finish_reason(seq, tok)
             if reason is not None:
                 # its speculative row in the step now in flight writes into blocks freed here; any
                 # reuse is by a LATER step, ordered after it on the stream
                 self.scheduler.finish(seq, reason)
                 self.requests.pop(seq.request_id, None)
-            outs.append(StepOutput(seq.request_id, [tok], reason is not None, reason, seq))
+            elif was_sampled:
+                self._stage_grammar(seq)    # used by the next launch (overrides its sample)
+            outs.append(StepOutput(seq.request_id, new, reason is not None, reason, seq))
         return outs
 
     def _step_overlap(self) -> List[StepOutput]:
@@ -240,29 +289,25 @@ class LLMEngine:
         # sampled order: completed prefills (in batch order), then decodes
         samplers = [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
         for seq, tok in zip(samplers, sampled):
-            forced = seq.params.forced_output
-            k = len(seq.output_ids)
-            if forced is not None and k < len(forced):
-                tok = forced[k]
-            seq.output_ids.append(int(tok))
+            known = self._known_run(seq)
+            run = known or [int(tok)]
+            seq.output_ids.extend(run)
             if seq.first_token_time is None:
                 seq.first_token_time = now
-            reason = None
-            if len(seq.output_ids) >= seq.params.max_tokens:
-                reason = "length"
-            elif forced is not None and len(seq.output_ids) >= len(forced) and not seq.params.ignore_eos:
-                reason = "stop"
-            elif not seq.params.ignore_eos and (tok in self.eos_ids or tok in seq.params.stop_token_ids):
-                reason = "stop"
-            elif seq.num_tokens >= self.cfg.max_model_len:
-                reason = "length"
-            if reason is None:
-                self.bm.commit(seq)
-            else:
-                self.bm.commit(seq)
+            reason = self._finish_reason(seq, run[-1])
+            if reason is None and not known:
+                self._stage_grammar(seq)        # nothing in flight: append the forced run now
+                if seq.jump_queue:
+                    extra, seq.jump_queue = seq.jump_queue, []
+                    extra = extra[:max(seq.params.max_tokens - len(seq.output_ids), 0)]
+                    seq.output_ids.extend(extra)
+                    run = run + extra
+                    reason = self._finish_reason(seq, run[-1])
+            self.bm.commit(seq)
+            if reason is not None:
                 self.scheduler.finish(seq, reason)
                 self.requests.pop(seq.request_id, None)
-            outs.append(StepOutput(seq.request_id, [int(tok)], reason is not None, reason, seq))
+            outs.append(StepOutput(seq.request_id, run, reason is not None, reason, seq))
         for seq, start, n in batch.prefill:
             if start + n < seq.num_tokens:
                 self.bm.commit(seq)

@@ -18,6 +18,11 @@ class SamplingParams:
     stop_token_ids: Seq[int] = ()
     seed: Optional[int] = None
     forced_output: Optional[List[int]] = None   # teacher-forced continuation (scripted tool calls)
+    # jump-forward decoding (agent.grammar): forced_jump[k] -- output token k is forced by the
+    # output grammar given tokens[:k], so it is appended with its predecessor instead of being
+    # sampled; grammar -- the same oracle for sampled outputs (``forced(text) -> (str, ends)``)
+    forced_jump: Optional[List[bool]] = None
+    grammar: Optional[object] = None
 
 
 class SeqStatus(enum.Enum):
@@ -55,6 +60,9 @@ class Sequence:
         # ends the sequence (length / forced end), so it sits out N+1.
         self.pending_src = -1
         self.awaiting = False
+        self.jump_queue: List[int] = []    # grammar-forced tokens staged for the next launch
+        self.last_run: List[int] = []      # tokens appended at launch (emitted on resolve)
+        self.jump_tail: List[int] = []     # final run of an awaiting sequence
 
     @property
     def all_ids(self) -> List[int]:
