@@ -203,6 +203,49 @@ class SyntheticWordPiece:
         ids = [self._wid(w) for w in self._WORD.findall(text.lower())][: max_len - 2]
         return [self.CLS] + ids + [self.SEP]
 
+    def encode_batch(self, texts: Sequence[str], max_len: int = 512) -> List[List[int]]:
+        return [self.encode(t, max_len) for t in texts]
+
+
+class WordPieceTokenizer:
+    """Real BERT WordPiece (``tokenizers``, Rust) from a ``vocab.txt`` or a ``tokenizer.json`` --
+    what bge-base-en ships.  ``[CLS] pieces [SEP]``, truncated to ``max_len`` WITH the ``[SEP]``
+    kept (BERT's truncation); ``encode_batch`` tokenises in parallel outside the GIL."""
+
+    def __init__(self, path: str, lowercase: bool = True):
+        from tokenizers import Tokenizer
+        if path.endswith(".json"):
+            self.tk = Tokenizer.from_file(path)
+        else:
+            from tokenizers import BertWordPieceTokenizer
+            self.tk = BertWordPieceTokenizer(path, lowercase=lowercase)
+        vocab = self.tk.get_vocab()
+        self.vocab_size = self.tk.get_vocab_size()
+        self.CLS, self.SEP = vocab.get("[CLS]", 101), vocab.get("[SEP]", 102)
+        self.PAD, self.UNK = vocab.get("[PAD]", 0), vocab.get("[UNK]", 100)
+        self._max = None
+
+    def _truncate(self, max_len: int) -> None:
+        if self._max != max_len:
+            self.tk.enable_truncation(max_len)
+            self._max = max_len
+
+    def encode(self, text: str, max_len: int = 512) -> List[int]:
+        self._truncate(max_len)
+        return self.tk.encode(text).ids
+
+    def encode_batch(self, texts: Sequence[str], max_len: int = 512) -> List[List[int]]:
+        self._truncate(max_len)
+        return [e.ids for e in self.tk.encode_batch(list(texts))]
+
+
+def load_wordpiece(path: Optional[str] = None, vocab_size: int = 30522):
+    """Real WordPiece when a vocab/tokenizer file is given (``PENNY_EMBED_VOCAB``), else hashed ids."""
+    path = path or os.environ.get("PENNY_EMBED_VOCAB")
+    if path and os.path.exists(path):
+        return WordPieceTokenizer(path)
+    return SyntheticWordPiece(vocab_size)
+
 
 class IncrementalDetokenizer:
     """Turns a growing list of token ids into text deltas without splitting characters.

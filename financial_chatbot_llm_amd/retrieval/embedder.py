@@ -45,22 +45,27 @@ class HashEmbedder:
 
 
 class BgeEmbedder:
-    """On-device bge-base-en encoder (random-init unless a safetensors checkpoint is given)."""
+    """On-device bge-base-en encoder.  Random-init unless ``weights`` (an HF safetensors file or
+    directory) is given; real WordPiece ids when ``vocab`` (``vocab.txt`` / ``tokenizer.json``)
+    is given -- real weights need the real vocabulary, hashed ids would make them meaningless."""
 
     def __init__(self, model_name: str = "bge-base-en", device: str = "cuda", weights: str = None,
-                 max_len: int = 64, seed: int = 0):
+                 max_len: int = 64, seed: int = 0, vocab: str = None):
         from ..models.bert import BertEncoder
         from ..models.configs import get_model_config
-        from ..engine.tokenizer import SyntheticWordPiece
+        from ..engine.tokenizer import load_wordpiece
         self.cfg = get_model_config(model_name)
         self.dim = self.cfg.hidden_size
-        self.tokenizer = SyntheticWordPiece(self.cfg.vocab_size)
+        self.tokenizer = load_wordpiece(vocab, self.cfg.vocab_size)
         self.model = BertEncoder.build(self.cfg, device=device, weights=weights, seed=seed)
-        self.max_len = max_len
+        self.max_len = min(max_len, self.cfg.max_position)
 
-    def embed(self, texts: Sequence[str]):
-        ids = [self.tokenizer.encode(t)[: self.max_len] for t in texts]
-        return self.model.encode(ids)
+    def tokenize(self, texts: Sequence[str], max_len: int = None) -> List[List[int]]:
+        # truncation keeps [SEP] (the encoder was trained on [CLS] ... [SEP])
+        return self.tokenizer.encode_batch(list(texts), max_len or self.max_len)
+
+    def embed(self, texts: Sequence[str], max_len: int = None):
+        return self.model.encode(self.tokenize(texts, max_len))
 
     def embed_query(self, text: str) -> List[float]:
         return self.embed([text])[0].float().cpu().tolist()

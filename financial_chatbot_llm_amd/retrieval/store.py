@@ -58,19 +58,41 @@ def synthetic_payload(row: int, user_id: str, date: int) -> Dict[str, Any]:
 
 
 class Corpus:
-    """Host-side mirror of a collection: ids, user codes, dates, payload provider."""
+    """Host-side mirror of a collection: ids, user codes, dates, payload provider.
+
+    Arrays grow by doubling (bulk ingest appends thousands of batches), payloads are stored
+    per row or generated (``payload_fn``) for synthetic corpora."""
 
     def __init__(self, dim: int):
         self.dim = dim
         self.user_to_code: Dict[str, int] = {}
         self.code_to_user: List[str] = []
-        self.user_codes = np.zeros((0,), np.int32)
-        self.dates = np.zeros((0,), np.int64)
+        self._codes = np.zeros((0,), np.int32)
+        self._dates = np.zeros((0,), np.int64)
+        self._n = 0
         self._payloads: List[Optional[Dict[str, Any]]] = []
         self.payload_fn: Optional[Callable[[int], Dict[str, Any]]] = None
+        self.synthetic: Optional[Dict[str, int]] = None   # how payload_fn was built (snapshots)
+
+    @property
+    def user_codes(self) -> np.ndarray:
+        return self._codes[: self._n]
+
+    @user_codes.setter
+    def user_codes(self, v) -> None:
+        self._codes = np.asarray(v, np.int32)
+        self._n = int(self._codes.shape[0])
+
+    @property
+    def dates(self) -> np.ndarray:
+        return self._dates[: self._n]
+
+    @dates.setter
+    def dates(self, v) -> None:
+        self._dates = np.asarray(v, np.int64)
 
     def __len__(self) -> int:
-        return int(self.user_codes.shape[0])
+        return self._n
 
     def code(self, user_id: str, create: bool = False) -> int:
         c = self.user_to_code.get(user_id)
@@ -82,11 +104,19 @@ class Corpus:
 
     def append(self, user_ids: Sequence[str], dates: Sequence[int], payloads: Sequence[Optional[Dict[str, Any]]]) -> np.ndarray:
         codes = np.array([self.code(u, create=True) for u in user_ids], np.int32)
-        start = len(self)
-        self.user_codes = np.concatenate([self.user_codes, codes])
-        self.dates = np.concatenate([self.dates, np.asarray(dates, np.int64)])
+        n, start = len(codes), self._n
+        if start + n > self._codes.shape[0]:
+            cap = max(start + n, 2 * self._codes.shape[0], 1024)
+            c2, d2 = np.zeros(cap, np.int32), np.zeros(cap, np.int64)
+            c2[:start], d2[:start] = self._codes[:start], self._dates[:start]
+            self._codes, self._dates = c2, d2
+        self._codes[start:start + n] = codes
+        self._dates[start:start + n] = np.asarray(dates, np.int64)
+        self._n = start + n
+        if len(self._payloads) < start:
+            self._payloads.extend([None] * (start - len(self._payloads)))
         self._payloads.extend(payloads)
-        return np.arange(start, len(self))
+        return np.arange(start, start + n)
 
     def payload(self, row: int) -> Optional[Dict[str, Any]]:
         if row < len(self._payloads) and self._payloads[row] is not None:
@@ -200,6 +230,7 @@ class DeviceVectorStore(VectorStoreBase):
         self.corpus.dates = dates
         self.corpus._payloads = []
         self.corpus.payload_fn = lambda r: synthetic_payload(r, user_name(int(users[r])), int(dates[r]))
+        self.corpus.synthetic = {"n": int(n), "num_users": int(num_users), "seed": int(seed)}
         self._ensure(n)
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
@@ -210,6 +241,60 @@ class DeviceVectorStore(VectorStoreBase):
         self.user_codes[:n] = torch.as_tensor(users, device=self.device)
         self.dates[:n] = torch.as_tensor(dates, device=self.device)
         self.size = n
+
+    # -- snapshots (safetensors + JSON sidecars; no pickles) -----------------------------
+    def save(self, path: str) -> None:
+        """Write the collection to ``path/``: ``vectors.safetensors`` (bf16 rows, int32 user
+        codes, int64 dates), ``corpus.json`` (user ids, synthetic recipe) and, for ingested
+        rows, ``payloads.jsonl`` (one payload per row)."""
+        import json
+        import os
+
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        n = self.size
+        save_file({"vectors": self.vectors[:n].cpu().contiguous(), "user_codes": self.user_codes[:n].cpu().contiguous(),
+                   "dates": self.dates[:n].cpu().contiguous()}, os.path.join(path, "vectors.safetensors"))
+        meta = {"dim": self.corpus.dim, "size": n, "users": self.corpus.code_to_user,
+                "synthetic": self.corpus.synthetic}
+        with open(os.path.join(path, "corpus.json"), "w") as fh:
+            json.dump(meta, fh)
+        if self.corpus._payloads:
+            with open(os.path.join(path, "payloads.jsonl"), "w") as fh:
+                for r in range(n):
+                    fh.write(json.dumps(self.corpus._payloads[r] if r < len(self.corpus._payloads) else None) + "\n")
+
+    @classmethod
+    def load(cls, path: str, device: str = "cuda") -> "DeviceVectorStore":
+        import json
+        import os
+
+        from safetensors import safe_open
+        with open(os.path.join(path, "corpus.json")) as fh:
+            meta = json.load(fh)
+        st = cls(meta["dim"], device=device)
+        with safe_open(os.path.join(path, "vectors.safetensors"), framework="pt") as fh:
+            vec, codes, dates = fh.get_tensor("vectors"), fh.get_tensor("user_codes"), fh.get_tensor("dates")
+        n = int(meta["size"])
+        st._ensure(n)
+        st.vectors[:n] = vec.to(st.device)
+        st.user_codes[:n] = codes.to(st.device)
+        st.dates[:n] = dates.to(st.device)
+        st.size = n
+        c = st.corpus
+        c.code_to_user = list(meta["users"])
+        c.user_to_code = {u: i for i, u in enumerate(c.code_to_user)}
+        c.user_codes, c.dates = codes.numpy(), dates.numpy()
+        syn = meta.get("synthetic")
+        if syn:
+            users, ds = c.user_codes, c.dates
+            c.payload_fn = lambda r: synthetic_payload(r, user_name(int(users[r])), int(ds[r]))
+            c.synthetic = syn
+        ppath = os.path.join(path, "payloads.jsonl")
+        if os.path.exists(ppath):
+            with open(ppath) as fh:
+                c._payloads = [json.loads(line) for line in fh]
+        return st
 
     def search_batch(self, qvecs, user_ids, date_gte, limits):
         from ..ops.retrieval import filtered_topk

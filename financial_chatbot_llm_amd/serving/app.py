@@ -8,6 +8,10 @@ Endpoints:
 * ``POST /v1/chat/stream`` -- server-sent events of the agent's updates for one turn (no Kafka);
   used for latency probing.
 * ``GET /metrics`` -- Prometheus text: turns/s, TTFT p50/p99, ITL, KV utilisation, ...
+* ``POST /v1/transactions`` -- ingest ``{"documents": [{page_content, metadata{user_id, date,
+  ...}}]}`` into the on-device collection (bge bulk embedding + append; the upstream Qdrant
+  collection was populated outside the reference repo).  An operator endpoint: put it behind
+  the deployment's auth like any write path.
 * ``/docs``, ``/redoc``, ``/openapi.json`` come from FastAPI as in the reference.
 
 The lifespan pings Mongo (raising aborts startup), subscribes the Kafka consumer and starts
@@ -20,7 +24,7 @@ import asyncio
 import json
 from contextlib import asynccontextmanager
 from dataclasses import dataclass
-from typing import Any, Optional
+from typing import Any, Dict, List, Optional
 
 from fastapi import FastAPI
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
@@ -42,6 +46,10 @@ class Services:
     engine: Any = None
     retrieval: Any = None
     serving: Optional[config.ServingConfig] = None
+
+
+class IngestPayload(BaseModel):
+    documents: List[Dict[str, Any]]
 
 
 class MessagePayload(BaseModel):
@@ -109,6 +117,20 @@ def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
         chat_history = await services.db.get_history(payload.conversation_id)
         res = await services.agent.query(payload.message, user_id, user_context, chat_history)
         return {"response": res["response"], "retrieved_transactions_count": res["retrieved_transactions_count"]}
+
+    @app.post("/v1/transactions")
+    async def ingest_transactions(payload: IngestPayload):
+        svc = services.retrieval
+        if svc is None or not hasattr(svc.store, "add"):
+            return JSONResponse({"detail": "no vector store configured"}, status_code=503)
+        from ..retrieval.ingest import CorpusIngestor
+        ing = CorpusIngestor(svc.embedder, svc.store)
+
+        def run():
+            with svc._lock:          # never interleave with a search batch on the store
+                return ing.ingest(payload.documents)
+        stats = await asyncio.to_thread(run)
+        return {**stats, "size": len(svc.store.corpus)}
 
     @app.post("/v1/chat/stream")
     async def chat_stream(payload: MessagePayload):

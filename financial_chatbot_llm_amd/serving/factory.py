@@ -49,15 +49,15 @@ def build_engine_services(engine_cfg: Optional[config.EngineConfig] = None,
                           max_tool_steps: int = 1) -> Services:
     from ..engine.async_engine import AsyncEngine
     from ..engine.backend import EngineLLM
-    from ..retrieval import BgeEmbedder, DeviceVectorStore
 
     engine_cfg = engine_cfg or config.EngineConfig.from_env()
     retrieval_cfg = retrieval_cfg or config.RetrievalConfig.from_env()
     serving = serving or config.ServingConfig.from_env()
+    from ..retrieval.ingest import build_store
     engine = AsyncEngine(engine_cfg)
-    embedder = BgeEmbedder(retrieval_cfg.embed_model, device=retrieval_cfg.device)
-    store = DeviceVectorStore(embedder.dim, device=retrieval_cfg.device)
-    if retrieval_cfg.corpus_size:
+    embedder, store = build_store(retrieval_cfg.embed_model, retrieval_cfg.device, retrieval_cfg.corpus_path,
+                                  weights=retrieval_cfg.weights, vocab=retrieval_cfg.vocab)
+    if retrieval_cfg.corpus_size and not retrieval_cfg.corpus_path:
         store.load_synthetic(retrieval_cfg.corpus_size, retrieval_cfg.num_users)
     retrieval = RetrievalService(embedder, store)
     llm = EngineLLM(engine, max_model_len=engine_cfg.max_model_len,

@@ -34,6 +34,8 @@ def parse(argv=None):
     ap.add_argument("--model", default=os.environ.get("PENNY_MODEL", "llama3-8b"))
     ap.add_argument("--embed-model", default=os.environ.get("PENNY_EMBED_MODEL", "bge-base-en"))
     ap.add_argument("--corpus", type=int, default=int(os.environ.get("PENNY_CORPUS_SIZE", "0")))
+    ap.add_argument("--corpus-path", default=os.environ.get("PENNY_CORPUS_PATH", ""),
+                    help="collection snapshot dir (DeviceVectorStore.save) or jsonl/json/parquet documents to ingest")
     ap.add_argument("--users", type=int, default=int(os.environ.get("PENNY_CORPUS_USERS", "10000")))
     ap.add_argument("--port", type=int, default=int(os.environ.get("PORT", "8000")))
     ap.add_argument("--tool-steps", type=int, default=1, help=">1 enables the multi-step agent (retrieval + plot)")
@@ -50,14 +52,16 @@ def build_leader_services(args, engine, device):
     from ..adapters import Database, InMemoryBroker, KafkaClient
     from ..agent import LLMAgent, LLMService
     from ..engine.backend import EngineLLM
-    from ..retrieval import BgeEmbedder, DeviceVectorStore, HashEmbedder, NumpyVectorStore, RetrievalService
+    from ..retrieval import HashEmbedder, NumpyVectorStore, RetrievalService
     from ..tools import make_plot_tool, make_retrieval_tool
     from .app import Services
 
     if device.type == "cuda":
-        embedder = BgeEmbedder(args.embed_model, device=str(device))
-        store = DeviceVectorStore(embedder.dim, device=str(device))
-        if args.corpus:
+        from ..retrieval.ingest import build_store
+        rcfg = config.RetrievalConfig.from_env()
+        embedder, store = build_store(args.embed_model, str(device), args.corpus_path or rcfg.corpus_path,
+                                      weights=rcfg.weights, vocab=rcfg.vocab)
+        if args.corpus and not (args.corpus_path or rcfg.corpus_path):
             store.load_synthetic(args.corpus, args.users)
     else:
         embedder = HashEmbedder(768)
