@@ -239,11 +239,11 @@ class ModelRunner:
         return self.model.logits(h.index_select(0, idx))
 
     def sample(self, logits: torch.Tensor, si: StepInputs) -> torch.Tensor:
-        if (si.top_k > 0).any() or (si.top_p < 1).any():
-            logits = ops.apply_top_k_top_p(logits, torch.from_numpy(si.top_k).to(logits.device),
-                                           torch.from_numpy(si.top_p).to(logits.device))
         temps = self._to_dev(si.temps)
         seeds = self._to_dev(si.seeds)
+        if (si.top_k > 0).any() or (si.top_p < 1).any():   # device-side top-k/top-p threshold
+            return ops.sample(logits.contiguous(), temps, seeds, top_k=self._to_dev(si.top_k),
+                              top_p=self._to_dev(si.top_p))
         return ops.sample(logits.contiguous(), temps, seeds)
 
     def execute(self, si: StepInputs) -> List[int]:
@@ -266,8 +266,7 @@ class ModelRunner:
             start_ev = torch.cuda.Event(enable_timing=True)
             start_ev.record()
         graph = False
-        if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
-                and not (si.top_k > 0).any() and not (si.top_p < 1).any()):
+        if self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch:
             with marker(f"decode.graph[{si.num_decode}]"):
                 out = self._graph_decode(si)
             graph = True
@@ -301,24 +300,28 @@ class ModelRunner:
         self._src_off = 4 * B + B * W          # pending-token gather rows (-1: host id)
         self._cas_off = self._src_off + B
         n_cas = sum(n for _, n in CascadeInputs.section_sizes(B)) if self.cascade else 0
-        self._dev_i32 = torch.zeros(self._cas_off + n_cas, dtype=torch.int32, device=self.device)
+        self._topk_off = self._cas_off + n_cas    # per-row top-k (0: off), in the same H2D copy
+        self._dev_i32 = torch.zeros(self._topk_off + B, dtype=torch.int32, device=self.device)
         d = self._dev_i32
         self._static = {
             "ids": d[0:B], "pos": d[B:2 * B], "slots": d[2 * B:3 * B], "ctx": d[3 * B:4 * B],
             "bt": d[4 * B:self._src_off].view(B, W),
             "src": d[self._src_off:self._cas_off],
-            "cascade": CascadeInputs.views(d[self._cas_off:], B) if self.cascade else None,
-            "temps": torch.zeros(B, dtype=torch.float32, device=self.device),
+            "cascade": CascadeInputs.views(d[self._cas_off:self._topk_off], B) if self.cascade else None,
+            "top_k": d[self._topk_off:self._topk_off + B],
+            "f32": torch.zeros(2 * B, dtype=torch.float32, device=self.device),     # temps | top_p
             "seeds": torch.zeros(B, dtype=torch.int64, device=self.device),
         }
         self._static["slots"].fill_(-1)
         self._static["ctx"].fill_(1)
         self._static["src"].fill_(-1)
+        self._static["temps"], self._static["top_p"] = self._static["f32"][:B], self._static["f32"][B:]
+        self._static["top_p"].fill_(1.0)
         # two pinned staging sets, alternated per graph step: in overlap mode the host packs step
         # N+1 while step N's H2D copy may still be queued behind step N-1 on the stream, so a
         # single buffer could be overwritten before the DMA reads it
-        self._pinned_sets = [(torch.zeros(self._cas_off + n_cas, dtype=torch.int32).pin_memory(),
-                              torch.zeros(B, dtype=torch.float32).pin_memory(),
+        self._pinned_sets = [(torch.zeros(self._topk_off + B, dtype=torch.int32).pin_memory(),
+                              torch.zeros(2 * B, dtype=torch.float32).pin_memory(),
                               torch.zeros(B, dtype=torch.int64).pin_memory()) for _ in range(2)]
         self._pin_flip = 0
         self._pinned_i32, self._pinned_f, self._pinned_l = self._pinned_sets[0]
@@ -331,7 +334,9 @@ class ModelRunner:
                                  cascade=s["cascade"])
         h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
         logits = self.model.logits(h)
-        return ops.sample(logits, s["temps"][:B], s["seeds"][:B])
+        # the top-k/top-p threshold kernel is always in the graph: unfiltered rows (k=0, p=1) exit
+        # after reading their parameters
+        return ops.sample(logits, s["temps"][:B], s["seeds"][:B], top_k=s["top_k"][:B], top_p=s["top_p"][:B])
 
     def capture_graphs(self) -> None:
         if not self.use_graphs:
@@ -385,11 +390,17 @@ class ModelRunner:
             src[:n] = si.src
         if self.cascade:
             CascadeInputs.pack(self._plan(si), buf[self._cas_off:], S, n)
-        self._pinned_f.numpy()[:n] = si.temps
+        tk = buf[self._topk_off:self._topk_off + S]
+        tk[:B] = 0
+        tk[:n] = si.top_k
+        f = self._pinned_f.numpy()
+        f[:n] = si.temps
+        f[S:S + B] = 1.0
+        f[S:S + n] = si.top_p
         self._pinned_l.numpy()[:n] = si.seeds
         self._dev_i32.copy_(self._pinned_i32, non_blocking=True)
         s = self._static
-        s["temps"].copy_(self._pinned_f, non_blocking=True)
+        s["f32"].copy_(self._pinned_f, non_blocking=True)
         s["seeds"].copy_(self._pinned_l, non_blocking=True)
         G.graph.replay()
         self.stats["graph_steps"] += 1

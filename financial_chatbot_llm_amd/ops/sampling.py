@@ -1,4 +1,5 @@
-"""K12: temperature / Gumbel-max sampling and greedy argmax over full-vocab logits."""
+"""K12: temperature / Gumbel-max sampling and greedy argmax over full-vocab logits, with optional
+per-row top-k / top-p filters (HIP radix-select threshold, graph-capturable; ``sampler.hip``)."""
 from __future__ import annotations
 
 from typing import Optional
@@ -11,21 +12,30 @@ SPLITS = 16  # vocab slices per row in the HIP sampler (SAMPLE_SPLITS)
 
 
 def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """logits [B, V] (bf16 or f32), temperatures [B] f32 (<= 0 -> greedy), seeds [B] int64.
+           out: Optional[torch.Tensor] = None, top_k: Optional[torch.Tensor] = None,
+           top_p: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """logits [B, V] (bf16 or f32), temperatures [B] f32 (<= 0 -> greedy), seeds [B] int64,
+    optional top_k [B] int32 (<= 0: off) and top_p [B] f32 (>= 1: off).
 
     Returns int32 token ids [B].  On the GPU the HIP kernel draws counter-based Gumbel noise
     from (seed, token index); the CPU reference uses torch's generator seeded per row, so the two
-    paths agree exactly for greedy rows and in distribution for sampled rows.
+    paths agree exactly for greedy rows and in distribution for sampled rows.  top-k/top-p become
+    a per-row logit threshold on the device (no sort, no host sync).
     """
     B, V = logits.shape
+    filt = top_k is not None and top_p is not None
     if N.use_native(logits):
         out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
         assert logits.stride(1) == 1 and logits.stride(0) % 8 == 0
-        ws = torch.empty((B * SPLITS * 2,), dtype=torch.float32, device=logits.device)
+        ws = torch.empty((B * SPLITS * 2 + B,), dtype=torch.float32, device=logits.device)
+        tk = top_k.to(torch.int32).contiguous() if filt else None
+        tp = top_p.to(torch.float32).contiguous() if filt else None
         N.call("penny_sample", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
-               N.ptr(temperatures), N.ptr(seeds), N.ptr(out), N.ptr(ws), B, V, N.stream())
+               N.ptr(temperatures), N.ptr(seeds), N.ptr(tk) if filt else None, N.ptr(tp) if filt else None,
+               N.ptr(out), N.ptr(ws), B, V, N.stream())
         return out
+    if filt:
+        logits = apply_top_k_top_p(logits, top_k.to(logits.device), top_p.to(logits.device), temperatures)
     res = torch.empty((B,), dtype=torch.int32)
     lf = logits.float()
     temps = temperatures.tolist()
@@ -43,18 +53,37 @@ def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor
     return res.to(logits.device)
 
 
-def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor) -> torch.Tensor:
-    """Mask logits outside top-k / nucleus top-p (rows with k<=0 / p>=1 untouched)."""
+def topk_topp_threshold(logits: torch.Tensor, temperatures: torch.Tensor, top_k: torch.Tensor,
+                        top_p: torch.Tensor) -> torch.Tensor:
+    """The HIP filter's per-row logit threshold (-inf: keep all) -- diagnostics/tests."""
+    B, V = logits.shape
+    th = torch.empty((B,), dtype=torch.float32, device=logits.device)
+    N.call("penny_topk_topp_threshold", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
+           N.ptr(temperatures), N.ptr(top_k.to(torch.int32).contiguous()),
+           N.ptr(top_p.to(torch.float32).contiguous()), N.ptr(th), B, V, N.stream())
+    return th
+
+
+def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
+                      temperatures: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 reference: mask logits outside top-k, then outside the nucleus top-p of the
+    temperature-scaled distribution renormalised over the top-k survivors (vLLM/HF order).
+    Rows with k <= 0 / p >= 1 (or greedy rows) are untouched."""
     if bool((top_k <= 0).all()) and bool((top_p >= 1).all()):
         return logits
     lf = logits.float()
+    B, V = lf.shape
+    t = temperatures.float().to(lf.device) if temperatures is not None else torch.ones(B, device=lf.device)
     sorted_l, idx = torch.sort(lf, dim=-1, descending=True)
-    V = lf.shape[-1]
     ranks = torch.arange(V, device=lf.device)[None, :]
-    k = torch.where(top_k > 0, top_k, torch.full_like(top_k, V))[:, None]
-    drop = ranks >= k
-    probs = torch.softmax(sorted_l, dim=-1)
-    cum = probs.cumsum(-1) - probs
-    drop |= cum > top_p[:, None].float()
+    k = torch.where(top_k > 0, top_k, torch.full_like(top_k, V)).to(lf.device)[:, None]
+    kth = sorted_l.gather(1, (k - 1).clamp(max=V - 1))
+    drop = sorted_l < kth                          # ties with the k-th value survive
+    scaled = (sorted_l / t.clamp(min=1e-6)[:, None]).masked_fill(drop, float("-inf"))
+    probs = torch.softmax(scaled, dim=-1)
+    cum = probs.cumsum(-1) - probs                 # mass strictly above each token
+    drop |= cum >= top_p.float().to(lf.device)[:, None]
+    drop &= (t > 0)[:, None]
+    drop[:, 0] = False
     sorted_l = sorted_l.masked_fill(drop, float("-inf"))
     return torch.empty_like(lf).scatter_(-1, idx, sorted_l).to(logits.dtype)

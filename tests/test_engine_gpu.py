@@ -71,6 +71,24 @@ def test_sampling_seeded_reproducible_and_batch_invariant():
     assert a == b
 
 
+def test_top_k_top_p_decode_stays_on_graphs():
+    """top-k/top-p requests no longer fall back to eager decode: the HIP threshold kernel is part
+    of every captured graph; top_k=1 equals greedy at any temperature."""
+    cfg = EngineConfig(model="llama-tiny", device="cuda", num_kv_blocks=64, max_model_len=1024, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8))
+    eng = LLMEngine(cfg)
+    eng.warmup()
+    prompts = [list(range(10, 50)), list(range(60, 90))]
+    greedy = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
+    g0 = eng.runner.stats["graph_steps"]
+    k1 = eng.generate(prompts, SamplingParams(temperature=1.5, top_k=1, max_tokens=8, ignore_eos=True))
+    assert k1 == greedy
+    assert eng.runner.stats["graph_steps"] - g0 >= 7
+    nuc = eng.generate(prompts, SamplingParams(temperature=0.8, top_k=40, top_p=0.9, max_tokens=8, ignore_eos=True,
+                                               seed=7))
+    assert all(len(o) == 8 for o in nuc)
+
+
 def test_mixtral_fp8_experts_close_to_bf16():
     cfg = get_model_config("mixtral-tiny")
     m = MixtralModel(cfg, device="cuda", tp_rank=0, tp_size=1).init_random(seed=2)

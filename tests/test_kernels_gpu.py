@@ -432,3 +432,72 @@ def test_cascade_decode_matches_reference(D, Hq, Hkv):
     ops.CascadeInputs.pack(None, buf.numpy(), 64, B)
     out_e = ops.decode(*args, workspace=ws, cascade=ops.CascadeInputs.views(buf.to(DEV), 64))
     close(out_e, out_p, atol=1e-3)
+
+
+def _kept_ref(lg, k, p, t):
+    m = ops.apply_top_k_top_p(lg[None].float(), torch.tensor([k]), torch.tensor([p]), torch.tensor([t]))[0]
+    return torch.isfinite(m)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_topk_topp_threshold_matches_reference(dtype):
+    """HIP radix-select threshold vs the fp32 sort-based reference: same kept sets (up to tokens
+    tied with the threshold logit), nucleus mass >= p, and k/p-off rows keep everything."""
+    from financial_chatbot_llm_amd.ops.sampling import topk_topp_threshold
+    g = torch.Generator().manual_seed(11)
+    V = 128256
+    cases = [(50, 1.0, 1.0), (0, 0.9, 0.7), (40, 0.5, 1.0), (1, 1.0, 0.5), (0, 1.0, 1.0), (1000, 0.95, 1.3),
+             (0, 0.3, 0.5), (5, 0.99, 2.0)]
+    lg = (torch.randn(len(cases), V, generator=g) * 3.0).to(dtype)
+    k = torch.tensor([c[0] for c in cases], dtype=torch.int32)
+    p = torch.tensor([c[1] for c in cases], dtype=torch.float32)
+    t = torch.tensor([c[2] for c in cases], dtype=torch.float32)
+    th = topk_topp_threshold(lg.to(DEV), t.to(DEV), k.to(DEV), p.to(DEV)).cpu()
+    for i, (kk, pp, tt) in enumerate(cases):
+        row = lg[i].float()
+        kept = row >= th[i]
+        ref = _kept_ref(lg[i], kk, pp, tt)
+        if kk <= 0 and pp >= 1:
+            assert th[i] == float("-inf")
+            continue
+        assert bool((kept | ~ref).all()), f"case {i}: kernel dropped a reference token"
+        extra = kept & ~ref
+        assert bool((row[extra] == th[i]).all()), f"case {i}: extra tokens not ties of the threshold"
+        if kk > 0:
+            assert int((row > th[i]).sum()) < kk
+            if pp >= 1:
+                assert int(kept.sum()) >= min(kk, V)
+        if pp < 1:
+            surv = row >= (torch.sort(row, descending=True).values[kk - 1] if kk > 0 else -float("inf"))
+            probs = torch.softmax(torch.where(surv, row / tt, torch.tensor(-float("inf"))), -1)
+            assert float(probs[kept].sum()) >= pp - 1e-3
+            assert float(probs[row > th[i]].sum()) < pp + 1e-3
+
+
+def test_sampler_with_top_k_top_p_stays_in_the_nucleus():
+    V = 32000
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn(V, generator=g) * 2
+    n = 2048
+    lg = base.repeat(n, 1).contiguous()
+    t = torch.full((n,), 1.0)
+    sd = torch.arange(n, dtype=torch.int64) * 7919 + 3
+    k = torch.full((n,), 8, dtype=torch.int32)
+    p = torch.ones(n)
+    draws = ops.sample(lg.to(DEV), t.to(DEV), sd.to(DEV), top_k=k.to(DEV), top_p=p.to(DEV)).cpu().long()
+    top8 = torch.topk(base, 8).indices
+    assert bool(torch.isin(draws, top8).all())
+    emp = torch.bincount(draws, minlength=V)[top8].float() / n
+    want = torch.softmax(base[top8], -1)
+    assert (emp - want).abs().max() < 0.05
+    # top_k = 1 at any temperature == greedy
+    one = ops.sample(lg[:4].to(DEV), torch.full((4,), 5.0, device=DEV), sd[:4].to(DEV),
+                     top_k=torch.ones(4, dtype=torch.int32, device=DEV), top_p=torch.ones(4, device=DEV)).cpu()
+    assert bool((one.long() == int(torch.argmax(base))).all())
+    # nucleus: p=0.5 draws only from the smallest top set holding >= 50 % of the mass
+    probs = torch.softmax(base, -1)
+    sp, si = torch.sort(probs, descending=True)
+    nuc = si[: int((torch.cumsum(sp, 0) < 0.5).sum()) + 1]
+    draws = ops.sample(lg.to(DEV), t.to(DEV), sd.to(DEV), top_k=torch.zeros(n, dtype=torch.int32, device=DEV),
+                       top_p=torch.full((n,), 0.5, device=DEV)).cpu().long()
+    assert bool(torch.isin(draws, nuc).all())
