@@ -128,6 +128,26 @@ __global__ void __launch_bounds__(256) ar_twoshot_kernel(const bf16* __restrict_
           *reinterpret_cast<const uint4*>(peers.data[q] + off + q * chunk + i);
 }
 
+// All-gather (C2: vocab-parallel LM-head logits) on the same buffers, flags and round counter:
+// copy-in, publish, wait, then read every peer's n elements over the direct links into
+// out[q * n ...] (rank-major; the caller permutes to [B, V]).  One flag round trip.
+__global__ void __launch_bounds__(256) ag_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, long n,
+                                                 ArPeers peers, const int* __restrict__ counter,
+                                                 int* __restrict__ err, int rank, int nranks, long half_elems) {
+  const int round = *counter + 1;
+  const long off = (round & 1) * half_elems;
+  const long per = ((n + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
+  const long lo = blockIdx.x * per, hi = min(n, lo + per);
+  bf16* mine = peers.data[rank] + off;
+  for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+    *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
+  ar_publish(peers, 0, rank, nranks, round);
+  ar_wait(peers, 0, rank, nranks, round, err);
+  for (int q = 0; q < nranks; ++q)
+    for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+      *reinterpret_cast<uint4*>(out + q * n + i) = *reinterpret_cast<const uint4*>(peers.data[q] + off + i);
+}
+
 __global__ void ar_bump_kernel(int* counter) { *counter += 1; }
 
 PENNY_API int penny_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
@@ -174,6 +194,25 @@ static int ar_launch(bool twoshot, const void* in, void* out, long n, void* cons
   else
     hipLaunchKernelGGL(ar_oneshot_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
                        (const int*)counter, err, rank, nranks, half_elems);
+  hipLaunchKernelGGL(ar_bump_kernel, dim3(1), dim3(1), 0, stream, counter);
+  PENNY_RETURN_LAUNCH();
+}
+
+// out: [nranks * n] rank-major; n % 8 == 0, n <= half_elems
+PENNY_API int penny_allgather(const void* in, void* out, long n, void* const* data_ptrs, void* const* sig_ptrs,
+                              int* counter, int* err, int rank, int nranks, long half_elems, int nblocks,
+                              hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (nranks < 1 || nranks > AR_MAX_RANKS || rank < 0 || rank >= nranks || n % 8 || n > half_elems ||
+      nblocks < 1 || nblocks > AR_MAX_BLOCKS)
+    return (int)hipErrorInvalidValue;
+  ArPeers peers;
+  for (int q = 0; q < AR_MAX_RANKS; ++q) {
+    peers.data[q] = q < nranks ? (bf16*)data_ptrs[q] : nullptr;
+    peers.sig[q] = q < nranks ? (int*)sig_ptrs[q] : nullptr;
+  }
+  hipLaunchKernelGGL(ag_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)in, (bf16*)out, n, peers,
+                     (const int*)counter, err, rank, nranks, half_elems);
   hipLaunchKernelGGL(ar_bump_kernel, dim3(1), dim3(1), 0, stream, counter);
   PENNY_RETURN_LAUNCH();
 }

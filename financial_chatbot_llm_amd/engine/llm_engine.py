@@ -1,8 +1,10 @@
 """Synchronous engine core: model + paged KV pool + scheduler + runner, stepped by the caller.
 
 One :class:`LLMEngine` serves one TP group (a DP replica).  On TP>1 only the group leader runs
-the scheduler; each step it broadcasts the packed :class:`StepInputs` (C4) and every rank runs
-the identical forward (``follower_loop`` on the other ranks).
+the scheduler; each step it broadcasts the packed :class:`StepInputs` (C4, one flat buffer over
+a gloo twin of the TP group) and every rank runs the identical forward (``follower_loop`` on the
+other ranks).  Decode-size TP all-reduces take the custom one-shot xGMI kernel by default
+(``EngineConfig.custom_all_reduce``), RCCL the rest.
 """
 from __future__ import annotations
 
@@ -77,6 +79,11 @@ class LLMEngine:
         self.async_scheduling = bool(getattr(cfg, "async_scheduling", True))
         self._inflight = None      # (batch, samplers, PendingStep) of the step on the GPU
         self.ps = pstate()
+        if self.ps.tp_size > 1 and device.type == "cuda" and getattr(cfg, "custom_all_reduce", True):
+            try:   # collective over the TP group: every rank constructs its engine together
+                comm.enable_custom_all_reduce()
+            except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
+                logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
         self.profiler = StepProfiler(rank=self.ps.rank)
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
                     f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
@@ -251,7 +258,7 @@ class LLMEngine:
         if not batch.empty():
             si = build_step_inputs(batch)
             if self.ps.tp_size > 1:
-                comm.broadcast_object(si)
+                comm.broadcast_step(si)
             t1 = time.perf_counter()
             launched = (batch, self._samplers(batch), self.runner.launch(si))
         t2 = time.perf_counter()
@@ -274,7 +281,7 @@ class LLMEngine:
             return []
         si = build_step_inputs(batch)
         if self.ps.tp_size > 1:
-            comm.broadcast_object(si)
+            comm.broadcast_step(si)
         t1 = time.perf_counter()
         sampled = self.runner.execute(si)
         now = time.perf_counter()
@@ -317,14 +324,14 @@ class LLMEngine:
     def follower_loop(self) -> None:
         """Non-leader TP ranks: replay the leader's steps until it broadcasts None."""
         while True:
-            si = comm.broadcast_object(None)
+            si = comm.broadcast_step(None)
             if si is None:
                 return
             self.runner.execute(si)
 
     def stop_followers(self) -> None:
         if self.ps.tp_size > 1 and self.ps.is_tp_leader:
-            comm.broadcast_object(None)
+            comm.broadcast_step(None)
 
     # -- convenience --------------------------------------------------------------------
     def generate(self, prompts: Seq[Seq[int]], params: SamplingParams) -> List[List[int]]:

@@ -55,9 +55,50 @@ class StepInputs:
     def num_prefill_tokens(self) -> int:
         return int(self.cu_q[-1]) if len(self.cu_q) else 0
 
+    # -- C4 wire format: one flat byte buffer (no pickling) ------------------------------------
+    _ARRAYS = ("ids", "positions", "slots", "cu_q", "ctx_p", "bt_p", "ctx_d", "bt_d", "logits_idx", "temps",
+               "seeds", "top_k", "top_p", "src")
+
+    def pack(self) -> np.ndarray:
+        """[header int64: max_q_len, then (dtype code, rows, cols) per array] + raw array bytes."""
+        arrs = [getattr(self, n) for n in self._ARRAYS]
+        head = [self.max_q_len]
+        body = []
+        for a in arrs:
+            if a is None:
+                head += [-1, 0, 0]
+                continue
+            a = np.ascontiguousarray(a)
+            head += [_DT_CODE[a.dtype.str], a.shape[0], a.shape[1] if a.ndim == 2 else -1]
+            body.append(a.view(np.uint8).reshape(-1))
+        h = np.asarray(head, np.int64).view(np.uint8)
+        return np.concatenate([h] + body)
+
+    @classmethod
+    def unpack(cls, buf: np.ndarray) -> "StepInputs":
+        n = len(cls._ARRAYS)
+        head = buf[:8 * (1 + 3 * n)].view(np.int64)
+        off = 8 * (1 + 3 * n)
+        vals = {}
+        for i, name in enumerate(cls._ARRAYS):
+            code, rows, cols = (int(x) for x in head[1 + 3 * i: 4 + 3 * i])
+            if code < 0:
+                vals[name] = None
+                continue
+            dt = np.dtype(_DT_NAME[code])
+            count = rows * (cols if cols >= 0 else 1)
+            a = buf[off: off + count * dt.itemsize].view(dt)
+            off += count * dt.itemsize
+            vals[name] = a.reshape(rows, cols) if cols >= 0 else a
+        return cls(max_q_len=int(head[0]), **vals)
+
     @property
     def num_decode(self) -> int:
         return len(self.ctx_d)
+
+
+_DT_NAME = ("<i4", "<i8", "<f4")
+_DT_CODE = {n: i for i, n in enumerate(_DT_NAME)}
 
 
 def _slots(seq: Sequence, start: int, n: int) -> List[int]:

@@ -8,8 +8,10 @@
 * SP ``tp_reduce_scatter_rows`` / ``tp_all_gather_rows``: sequence-parallel prefill (Megatron
   SP) -- the residual stream is sharded by rows between the row-parallel and column-parallel
   GEMMs (reduce-scatter after O/down, all-gather before QKV/gate-up).
-* C4 ``broadcast_object``: the TP leader's scheduler decisions (token ids, positions, block
-  tables) for a step, so non-leader ranks replay the identical forward.
+* C4 ``broadcast_step``: the TP leader's scheduler decisions (token ids, positions, block
+  tables, sampling params) for a step, so non-leader ranks replay the identical forward: ONE flat
+  byte buffer (``StepInputs.pack``), sent over a gloo twin of the TP group -- host memory to host
+  memory, no pickling and no device round trip (a header broadcast carries the length).
 
 xGMI is point-to-point (7 links per GPU): for 8-way TP the bandwidth-optimal ring is per-link
 bound, so large messages (prefill activations) use RCCL's ring/tree; decode messages are
@@ -32,15 +34,23 @@ def tp_size() -> int:
 _CUSTOM_AR = None   # CustomAllReduce for the TP group (enable_custom_all_reduce)
 
 
-def enable_custom_all_reduce(max_bytes: int = 4 << 20):
-    """Route small bf16 TP all-reduces (decode) through the one-shot xGMI P2P kernel
+def enable_custom_all_reduce(max_bytes: int = 4 << 20, buffer_bytes: int = 32 << 20):
+    """Route small bf16 TP all-reduces (decode) through the one-shot xGMI P2P kernel and the
+    vocab-parallel logits gather (up to ``buffer_bytes`` per rank) through its all-gather twin
     (``custom_ar.py``); RCCL keeps everything else.  Call on every TP rank after init."""
     global _CUSTOM_AR
     s = state()
     if s.tp_size > 1 and _CUSTOM_AR is None:
         from .custom_ar import CustomAllReduce
-        _CUSTOM_AR = CustomAllReduce(s.tp_group, max_bytes=max_bytes)
+        _CUSTOM_AR = CustomAllReduce(s.tp_group, max_bytes=max_bytes, buffer_bytes=buffer_bytes)
     return _CUSTOM_AR
+
+
+def disable_custom_all_reduce() -> None:
+    global _CUSTOM_AR
+    if _CUSTOM_AR is not None:
+        _CUSTOM_AR.close()
+    _CUSTOM_AR = None
 
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
@@ -58,8 +68,12 @@ def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     s = state()
     if s.tp_size == 1:
         return x
+    x = x.contiguous()
+    if _CUSTOM_AR is not None and _CUSTOM_AR.gather_eligible(x):
+        g = _CUSTOM_AR.all_gather(x)                       # [tp, ..., V/tp], graph-capturable
+        return g.movedim(0, -2).reshape(tuple(x.shape[:-1]) + (s.tp_size * x.shape[-1],))
     parts = [torch.empty_like(x) for _ in range(s.tp_size)]
-    dist.all_gather(parts, x.contiguous(), group=s.tp_group)
+    dist.all_gather(parts, x, group=s.tp_group)
     return torch.cat(parts, dim=-1)
 
 
@@ -99,6 +113,34 @@ def tp_all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty((x.shape[0] * s.tp_size,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x, group=s.tp_group)
     return out
+
+
+_STOP = -1
+
+
+def broadcast_step(si: Any) -> Any:
+    """Leader: ``si`` (a StepInputs, or None = stop) -> followers; followers pass None and get
+    the leader's value back."""
+    s = state()
+    if s.tp_size == 1:
+        return si
+    import numpy as np
+    group = s.tp_cpu_group if s.tp_cpu_group is not None else s.tp_group
+    head = torch.zeros(1, dtype=torch.int64)
+    if s.is_tp_leader:
+        payload = None if si is None else si.pack()
+        head[0] = _STOP if payload is None else payload.size
+    dist.broadcast(head, src=s.tp_leader_rank, group=group)
+    n = int(head[0])
+    if n == _STOP:
+        return None
+    if s.is_tp_leader:
+        dist.broadcast(torch.from_numpy(payload), src=s.tp_leader_rank, group=group)
+        return si
+    buf = torch.empty(n, dtype=torch.uint8)
+    dist.broadcast(buf, src=s.tp_leader_rank, group=group)
+    from ..engine.model_runner import StepInputs
+    return StepInputs.unpack(buf.numpy())
 
 
 def broadcast_object(obj: Any) -> Any:

@@ -36,6 +36,9 @@ _SIGS = {
     "penny_allreduce_oneshot": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_void_p],
+    "penny_allgather": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_void_p),
+                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                        ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_void_p],
     "penny_allreduce_twoshot": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_void_p],
@@ -57,21 +60,24 @@ def _check(rc: int, what: str) -> None:
 
 
 class CustomAllReduce:
-    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 4 << 20):
+    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 4 << 20,
+                 buffer_bytes: Optional[int] = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if not 1 <= self.world <= AR_MAX_RANKS:
             raise ValueError(f"custom all-reduce supports up to {AR_MAX_RANKS} ranks")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.max_bytes = max_bytes
-        self.half_elems = max_bytes // 2
+        self.max_bytes = max_bytes                       # all-reduce eligibility
+        buffer_bytes = max(buffer_bytes or max_bytes, max_bytes)
+        self.buffer_bytes = buffer_bytes                 # per-round copy-in capacity (all-gather)
+        self.half_elems = buffer_bytes // 2
         lib = self._lib = _lib()
         hs = lib.penny_ar_handle_size()
         own_data, own_sig = ctypes.c_void_p(), ctypes.c_void_p()
         hd, hsg = ctypes.create_string_buffer(hs), ctypes.create_string_buffer(hs)
         with torch.cuda.device(self.device):
-            _check(lib.penny_ar_alloc(2 * max_bytes, ctypes.byref(own_data), hd), "penny_ar_alloc(data)")
+            _check(lib.penny_ar_alloc(2 * buffer_bytes, ctypes.byref(own_data), hd), "penny_ar_alloc(data)")
             _check(lib.penny_ar_alloc(SIG_BYTES, ctypes.byref(own_sig), hsg), "penny_ar_alloc(signal)")
         self._own = [own_data.value, own_sig.value]
         handles: List = [None] * self.world
@@ -122,6 +128,22 @@ class CustomAllReduce:
         _check(fn(x.data_ptr(), out.data_ptr(), n, self._data, self._sig, self.counter.data_ptr(),
                   self.err.data_ptr(), self.rank, self.world, self.half_elems, nblocks, N.stream()),
                f"penny_allreduce_{method}")
+        return out
+
+    def gather_eligible(self, x: torch.Tensor) -> bool:
+        return (x.dtype == torch.bfloat16 and x.is_cuda and x.is_contiguous() and x.numel() % 8 == 0
+                and x.numel() * 2 <= self.buffer_bytes)
+
+    def all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """[*] per rank -> [world, *] (rank-major), one kernel (copy-in, flag round, peer reads)."""
+        if not self.gather_eligible(x):
+            raise ValueError("tensor not eligible for the custom all-gather")
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        n = x.numel()
+        nblocks = max(1, min(AR_MAX_BLOCKS, (n + 2047) // 2048))
+        _check(self._lib.penny_allgather(x.data_ptr(), out.data_ptr(), n, self._data, self._sig,
+                                         self.counter.data_ptr(), self.err.data_ptr(), self.rank, self.world,
+                                         self.half_elems, nblocks, N.stream()), "penny_allgather")
         return out
 
     def check(self) -> None:

@@ -29,6 +29,7 @@ class ParallelState:
     dp_rank: int = 0
     tp_group: Optional[object] = None
     dp_group: Optional[object] = None
+    tp_cpu_group: Optional[object] = None   # gloo twin of tp_group: host control messages (C4)
     backend: str = "none"
 
     @property
@@ -80,8 +81,11 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None, device_typ
         for d in range(dp):
             ranks = list(range(d * tp_size, (d + 1) * tp_size))
             g = dist.new_group(ranks) if tp_size > 1 else None
+            # C4 step metadata is host data: a gloo group moves it CPU->CPU with no device hop
+            gc = (g if backend == "gloo" else dist.new_group(ranks, backend="gloo")) if tp_size > 1 else None
             if rank in ranks:
                 s.tp_group = g
+                s.tp_cpu_group = gc
         for t in range(tp_size):
             ranks = list(range(t, world, tp_size))
             g = dist.new_group(ranks) if dp > 1 else None
@@ -100,6 +104,8 @@ def barrier() -> None:
 
 
 def shutdown() -> None:
+    from .comm import disable_custom_all_reduce
+    disable_custom_all_reduce()          # unmap peer IPC buffers before the group goes away
     if dist.is_initialized():
         dist.destroy_process_group()
     set_state(ParallelState())

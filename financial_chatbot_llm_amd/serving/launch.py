@@ -109,9 +109,6 @@ def main(argv=None) -> int:
 
     ps = init_distributed(tp_size=args.tp)
     dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    if dev_type == "cuda" and args.tp > 1 and os.environ.get("PENNY_CUSTOM_AR") == "1":
-        from ..parallel import comm
-        comm.enable_custom_all_reduce()   # one-shot xGMI P2P all-reduce for decode-size messages
     device = torch.device(dev_type, torch.cuda.current_device()) if dev_type == "cuda" else torch.device("cpu")
     ecfg = config.EngineConfig.from_env(model=args.model, tp_size=args.tp, max_model_len=args.max_model_len,
                                         device=dev_type, use_cuda_graph=dev_type == "cuda")

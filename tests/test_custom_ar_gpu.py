@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         try:
-            ar = CustomAllReduce(None, torch.device("cuda", 0), max_bytes=1 << 20)
+            ar = CustomAllReduce(None, torch.device("cuda", 0), max_bytes=1 << 20, buffer_bytes=1 << 20)
         except RuntimeError as e:
             q.put((rank, "SKIP", str(e)))
             return
@@ -54,6 +54,14 @@ def _worker(rank, world, port, q):
             b = ar.all_reduce(xd, method="twoshot")
             torch.cuda.synchronize()
             results.append((float((a.float() - b.float()).abs().max().item()), 0.0, 0.0))
+        # all-gather (vocab-parallel logits): rank-major, exact
+        for i, n in enumerate([8, 4096 + 8, 300000]):
+            g = torch.Generator().manual_seed(9000 + 100 * i + rank)
+            x = torch.randn(n, generator=g).to(torch.bfloat16)
+            xs = [torch.empty_like(x) for _ in range(world)]
+            dist.all_gather(xs, x)
+            got = ar.all_gather(x.cuda()).cpu()
+            results.append((float((got.float() - torch.stack(xs).float()).abs().max().item()), 0.0, 0.0))
         # hipGraph capture: the round counter advances on the device across replays
         x = torch.full((4096,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
         ar.all_reduce(x)
@@ -65,7 +73,7 @@ def _worker(rank, world, port, q):
             gph.replay()
         torch.cuda.synchronize()
         results.append((float(y.float().mean().item()), float(world * (world + 1) / 2), 0.0))
-        results.append((float(ar.counter.item()), 22.0, 0.0))   # 10 + 6 + 1 eager calls + 5 replays
+        results.append((float(ar.counter.item()), 25.0, 0.0))   # 10 + 6 + 3 + 1 eager calls + 5 replays
         ar.check()
         dist.barrier()
         ar.close()

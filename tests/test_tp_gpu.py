@@ -23,7 +23,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(tp: int, rank: int = 0):
+def _run(tp: int, rank: int = 0, graphs: bool = False):
     from financial_chatbot_llm_amd.config import EngineConfig
     from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
     from financial_chatbot_llm_amd.engine.tokenizer import SyntheticLlamaTokenizer
@@ -32,24 +32,33 @@ def _run(tp: int, rank: int = 0):
     cfg = get_model_config("llama-tiny-tp")
     m = LlamaModel(cfg, device="cuda").init_random(seed=11, std=0.05)
     ecfg = EngineConfig(model="unused", device="cuda", num_kv_blocks=64, max_model_len=1024,
-                        max_num_batched_tokens=256, use_cuda_graph=False, max_num_seqs=8)
+                        max_num_batched_tokens=256, use_cuda_graph=graphs, max_num_seqs=8,
+                        graph_batch_sizes=(1, 2, 4, 8))
     eng = LLMEngine(ecfg, model=m, tokenizer=SyntheticLlamaTokenizer(cfg.vocab_size))
+    if graphs:
+        eng.warmup()           # every TP rank captures the same graphs (custom AR/AG kernels inside)
     if tp > 1 and rank != 0:
         eng.follower_loop()
         return None
     out = eng.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
     if tp > 1:
         eng.stop_followers()
+    if graphs:
+        assert eng.runner.stats["graph_steps"] > 0
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, graphs=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), PENNY_SPLITK="force")
     try:
+        from financial_chatbot_llm_amd.parallel import comm
         from financial_chatbot_llm_amd.parallel.dist import init_distributed, shutdown
         init_distributed(tp_size=world, backend="gloo", device_type="cuda")
-        out = _run(world, rank)
+        out = _run(world, rank, graphs)
+        if graphs:   # the decode graphs ran on the custom one-shot AR + all-gather kernels
+            assert comm._CUSTOM_AR is not None and int(comm._CUSTOM_AR.counter.item()) > 0
+            comm._CUSTOM_AR.check()
         torch.cuda.synchronize()
         q.put((rank, out))
         shutdown()
@@ -59,13 +68,16 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(240)
-def test_tp2_gpu_matches_tp1(monkeypatch):
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tp2_gpu_matches_tp1(monkeypatch, graphs):
+    """graphs=True: hipGraph-captured TP decode whose all-reduces / logits all-gather run on the
+    custom xGMI P2P kernels (on by default under TP), C4 as one packed buffer."""
     monkeypatch.setenv("PENNY_SPLITK", "force")
     ref = _run(1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, graphs)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=200) for _ in range(2))
