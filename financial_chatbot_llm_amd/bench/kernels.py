@@ -339,6 +339,61 @@ def bench_moe(dev) -> List[Dict]:
     return out
 
 
+def bench_moe_prefill(dev) -> List[Dict]:
+    """Mixtral-8x7B MoE layer at prefill sizes: the device-only fp8 pipeline (device routing +
+    grouped fp8 MFMA GEMMs, no host sync) vs per-expert hipBLASLt fp8 x fp8 GEMMs with a host
+    round trip for the bucket sizes (the r1 prefill path)."""
+    from ..ops import moe
+    out = []
+    E, H, F_, K = 8, 4096, 14336, 2
+    g = torch.Generator(device=dev).manual_seed(0)
+    w13 = (torch.randn((E, 2 * F_, H), device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    w13 = torch.stack([interleave16_rows(w13[e]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    del w13
+    w2 = (torch.randn((E, H, F_), device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    del w2
+    t13, t2 = moe.tile_fp8_weight(q13), moe.tile_fp8_weight(q2)
+    router = torch.randn((E, H), device=dev, generator=g).to(torch.bfloat16)
+    for T in (512, 1024, 2048, 4096, 8192, 16384):
+        h = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
+        logits = (h @ router.t()).contiguous()
+        dev_us = timeit(lambda: moe.moe_prefill_fp8(h, logits, t13, s13, t2, s2, K), iters=5)
+
+        def loop():
+            topw, topi = moe.topk_softmax(logits, K)
+            order, offsets, tok_idx, tok_w = moe.route(topi, topw, E)
+            offs = offsets.tolist()
+            xs = h.index_select(0, tok_idx)
+            ys = torch.empty_like(xs)
+            for e in range(E):
+                a, b = offs[e], offs[e + 1]
+                if b > a:
+                    xq, xsc = moe.quant_rows_fp8(xs[a:b])
+                    y13 = torch._scaled_mm(xq, q13[e].t(), scale_a=xsc[:, None], scale_b=s13[e][None, :],
+                                           out_dtype=torch.bfloat16)
+                    aq, asc = moe.silu_quant_rows_fp8(y13)
+                    ys[a:b] = torch._scaled_mm(aq, q2[e].t(), scale_a=asc[:, None], scale_b=s2[e][None, :],
+                                               out_dtype=torch.bfloat16)
+            return moe.combine_weighted(ys, order, tok_w, T, K)
+        loop_us = timeit(loop, iters=5)
+        a = moe.moe_prefill_fp8(h, logits, t13, s13, t2, s2, K).float()
+        b = loop().float()
+        flops = 2 * T * K * 3 * H * F_
+        out.append({"op": "moe_prefill", "T": T, "device_fp8_us": round(dev_us, 1),
+                    "device_TFLOPs": round(flops / dev_us / 1e6, 1), "hipblaslt_fp8_loop_us": round(loop_us, 1),
+                    "loop_TFLOPs": round(flops / loop_us / 1e6, 1),
+                    "rel_diff": round(float((a - b).abs().max() / b.abs().max()), 4)})
+    return out
+
+
+def interleave16_rows(w: torch.Tensor) -> torch.Tensor:
+    from ..ops.gemm import interleave16
+    half = w.shape[0] // 2
+    return interleave16(w[:half], w[half:])
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="decode,prefill,elementwise,topk")
@@ -350,6 +405,7 @@ def main(argv=None) -> int:
         res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
+                "moe_prefill": bench_moe_prefill,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),

@@ -8,9 +8,16 @@ here every in-flight turn of every conversation shares each forward pass.
 Memory: a sequence holds KV blocks for exactly its computed tokens (+ the step's new tokens).
 When the pool runs dry the youngest running sequence is preempted (blocks freed, re-queued at
 the front, recomputed later -- its full blocks usually come back from the prefix cache).
+
+Admission order (TTFT): preempted sequences first, then SHORT-OUTPUT requests -- the agent's
+decide call (``max_tokens <= short_output_tokens``: a tool call or "No tool call") gates the whole
+turn's TTFT and its prompt is mostly prefix-cached, so it should not queue behind long respond
+prefills -- then everything else, each class FCFS.  Aging keeps it starvation-free: a request
+that has waited ``aging_s`` joins the first class.
 """
 from __future__ import annotations
 
+import time
 from collections import deque
 from dataclasses import dataclass, field
 from typing import Deque, List, Tuple
@@ -38,7 +45,8 @@ class ScheduledBatch:
 
 class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
-                 max_model_len: int = 8192, decode_first: bool = True):
+                 max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
+                 aging_s: float = 1.0, clock=time.perf_counter):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -46,6 +54,18 @@ class Scheduler:
         self.waiting: Deque[Sequence] = deque()
         self.running: List[Sequence] = []
         self.num_preemptions = 0
+        self.short_output_tokens = short_output_tokens
+        self.aging_s = aging_s
+        self.clock = clock
+
+    def _priority(self, seq: Sequence, now: float):
+        if seq.num_preemptions:
+            cls = 0
+        elif seq.params.max_tokens <= self.short_output_tokens or now - seq.arrival >= self.aging_s:
+            cls = 1
+        else:
+            cls = 2
+        return (cls, seq.arrival)
 
     def add(self, seq: Sequence) -> None:
         if seq.num_tokens >= self.max_model_len:
@@ -104,7 +124,10 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
-        # 3) admit waiting sequences
+        # 3) admit waiting sequences, by priority class (preempted, short-output/aged, rest)
+        if len(self.waiting) > 1:
+            now = self.clock()
+            self.waiting = deque(sorted(self.waiting, key=lambda q: self._priority(q, now)))
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
             if seq.pending_src >= 0 or seq.awaiting:

@@ -135,8 +135,13 @@ class MixtralModel(DecoderModel):
         T = h.shape[0]
         logits = linear(h, self.w[p + "router"])
         if self.ep:
+            grouped = None
+            if self.fp8 and ops._native.use_native(h):   # one grouped fp8 call, device bucket offsets
+                grouped = lambda rows, ids: moe_ops.moe_grouped_fp8(  # noqa: E731
+                    rows.contiguous(), ids, self.w[p + "w13_t"], self.w[p + "w13_scale"], self.w[p + "w2_t"],
+                    self.w[p + "w2_scale"])
             return ep_moe(h, logits, c.top_k_experts, c.num_experts, lambda rows, e: self._expert(p, rows, e),
-                          group=pstate().tp_group)
+                          group=pstate().tp_group, grouped_fn=grouped)
         # fp8 MFMA pipeline while the step is weight-bandwidth-bound; bigger prefill chunks go to
         # hipBLASLt on the cached bf16 copy of the same quantized experts (compute-bound regime)
         fp8_limit = 1024 if (self.prefill_dequant_cache or self.prefill_fp8) else 4096

@@ -37,6 +37,91 @@ def route(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
     return order, offsets, tok_idx, tok_w
 
 
+def route_device(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
+    """:func:`route` without a host round trip (prefill buckets of any size): expert offsets as an
+    int32 DEVICE tensor for the grouped kernels, plus the sorted token index, routing weight and
+    the inverse map pair -> sorted position.  No ``bincount`` (it syncs to size its output)."""
+    T, k = topi.shape
+    flat_e = topi.reshape(-1).long()
+    order = torch.argsort(flat_e, stable=True)
+    counts = torch.zeros(num_experts, dtype=torch.int32, device=topi.device)
+    counts.scatter_add_(0, flat_e, torch.ones_like(flat_e, dtype=torch.int32))
+    offsets = torch.zeros(num_experts + 1, dtype=torch.int32, device=topi.device)
+    offsets[1:] = counts.cumsum(0)
+    tok_idx = (order // k).to(torch.int32)
+    tok_w = topw.reshape(-1)[order].float().contiguous()
+    inv = torch.empty_like(order)
+    inv[order] = torch.arange(order.numel(), device=order.device, dtype=order.dtype)
+    return offsets, tok_idx, tok_w, inv.to(torch.int32)
+
+
+def moe_prefill_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Tensor, s13: torch.Tensor,
+                    w2t: torch.Tensor, s2: torch.Tensor, top_k: int) -> torch.Tensor:
+    """Prefill-size fp8 MoE entirely on the device, no host sync: torch top-k routing +
+    :func:`route_device`, then the decode pipeline's grouped fp8 x fp8 MFMA GEMMs over the expert
+    buckets (gathered token rows, fused SiLU / routing-weight epilogues) and the combine."""
+    from . import _native as N
+    T, H = h.shape
+    E, F2 = s13.shape
+    F_ = F2 // 2
+    P = T * top_k
+    topw, topi = topk_softmax(router_logits, top_k)
+    offsets, tok_idx, tok_w, inv = route_device(topi, topw, E)
+    st = N.stream()
+    xq = torch.empty((T, H), dtype=torch.uint8, device=h.device)
+    xs = torch.empty(T, dtype=torch.float32, device=h.device)
+    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(xq), N.ptr(xs), st)
+    a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
+    ntf13, ntf2 = MOE_NTF
+    N.call("penny_moe_gemm_fp8", N.ptr(xq), N.ptr(xs), N.ptr(tok_idx), N.ptr(offsets), N.ptr(w13t), N.ptr(s13), None,
+           N.ptr(a), E, F2, H, 1, ntf13, st)
+    aq = torch.empty((P, F_), dtype=torch.uint8, device=h.device)
+    as_ = torch.empty(P, dtype=torch.float32, device=h.device)
+    N.call("penny_quant_rows_fp8", N.ptr(a), F_, P, F_, N.ptr(aq), N.ptr(as_), st)
+    y2 = torch.empty((P, H), dtype=torch.bfloat16, device=h.device)
+    N.call("penny_moe_gemm_fp8", N.ptr(aq), N.ptr(as_), None, N.ptr(offsets), N.ptr(w2t), N.ptr(s2), N.ptr(tok_w),
+           N.ptr(y2), E, H, F_, 2, ntf2, st)
+    out = torch.empty_like(h)
+    N.call("penny_moe_combine", N.ptr(y2), N.ptr(inv), T, top_k, H, N.ptr(out), st)
+    return out
+
+
+def moe_grouped_fp8(x: torch.Tensor, expert_ids: torch.Tensor, w13t: torch.Tensor, s13: torch.Tensor,
+                    w2t: torch.Tensor, s2: torch.Tensor) -> torch.Tensor:
+    """y[i] = expert_{ids[i]}(x[i]) for every row (ids -1 = padding -> 0), one grouped fp8
+    pipeline over the (local) expert bank, no host sync (expert-parallel receive side)."""
+    from . import _native as N
+    M, H = x.shape
+    E, F2 = s13.shape
+    F_ = F2 // 2
+    ids = expert_ids.long()
+    key = torch.where(ids >= 0, ids, torch.full_like(ids, E))
+    order = torch.argsort(key, stable=True)
+    counts = torch.zeros(E + 1, dtype=torch.int32, device=x.device)
+    counts.scatter_add_(0, key, torch.ones_like(key, dtype=torch.int32))
+    offsets = torch.zeros(E + 1, dtype=torch.int32, device=x.device)
+    offsets[1:] = counts[:E].cumsum(0)
+    rows = order.to(torch.int32)
+    st = N.stream()
+    xq = torch.empty((M, H), dtype=torch.uint8, device=x.device)
+    xs = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.call("penny_quant_rows_fp8", N.ptr(x), x.stride(0), M, H, N.ptr(xq), N.ptr(xs), st)
+    a = torch.zeros((M, F_), dtype=torch.bfloat16, device=x.device)
+    ntf13, ntf2 = MOE_NTF
+    N.call("penny_moe_gemm_fp8", N.ptr(xq), N.ptr(xs), N.ptr(rows), N.ptr(offsets), N.ptr(w13t), N.ptr(s13), None,
+           N.ptr(a), E, F2, H, 1, ntf13, st)
+    aq = torch.empty((M, F_), dtype=torch.uint8, device=x.device)
+    as_ = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.call("penny_quant_rows_fp8", N.ptr(a), F_, M, F_, N.ptr(aq), N.ptr(as_), st)
+    ones = torch.ones(M, dtype=torch.float32, device=x.device)
+    y2 = torch.zeros((M, H), dtype=torch.bfloat16, device=x.device)
+    N.call("penny_moe_gemm_fp8", N.ptr(aq), N.ptr(as_), None, N.ptr(offsets), N.ptr(w2t), N.ptr(s2), N.ptr(ones),
+           N.ptr(y2), E, H, F_, 2, ntf2, st)
+    y = torch.empty_like(y2)
+    y.index_copy_(0, order, y2)
+    return torch.where((ids >= 0)[:, None], y, torch.zeros_like(y))
+
+
 def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Dynamic per-row e4m3 quantisation on the device (HIP ``penny_quant_rows_fp8``, the decode
     pipeline's activation quantiser): x [M, K] bf16 -> (fp8 [M, K], f32 scale [M])."""

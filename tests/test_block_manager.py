@@ -114,3 +114,45 @@ def test_scheduler_chunked_prefill_and_preemption():
             s.output_ids.append(1)
     assert b.num_preemptions >= 0
     assert bm.num_free() >= 0
+
+
+def _mk_params(prompt, rid, max_tokens, arrival):
+    from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
+    return Sequence(rid, prompt, SamplingParams(max_tokens=max_tokens), arrival=arrival)
+
+
+def test_scheduler_admits_short_output_requests_first():
+    """A decide call (short output) queued behind a long respond prefill is admitted first."""
+    clock = [100.0]
+    bm = PyBlockManager(64, BS, True)
+    sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=4096, clock=lambda: clock[0])
+    long_ = _mk_params(list(range(1000, 1400)), "respond", 512, arrival=1.0 + 99)
+    short = _mk_params(list(range(2000, 2060)), "decide", 96, arrival=2.0 + 99)
+    sch.add(long_)
+    sch.add(short)
+    batch = sch.schedule()
+    assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("decide", 0, 60), ("respond", 0, 68)]
+
+
+def test_scheduler_aging_is_starvation_free():
+    """A long request keeps losing to fresh short ones only until it has waited aging_s; then,
+    being older, it is admitted ahead of every newer short request."""
+    clock = [0.0]
+    bm = PyBlockManager(512, BS, True)
+    sch = Scheduler(bm, max_num_seqs=64, max_num_batched_tokens=64, max_model_len=4096, aging_s=1.0,
+                    clock=lambda: clock[0])
+    long_ = _mk_params(list(range(5000, 5300)), "long", 512, arrival=0.0)
+    sch.add(long_)
+    admitted_long_at = None
+    for step in range(40):
+        clock[0] = 0.1 * (step + 1)
+        sch.add(_mk_params(list(range(10 * step, 10 * step + 64)), f"short{step}", 64, arrival=clock[0]))
+        batch = sch.schedule()
+        for s, st, n in batch.prefill:
+            s.num_computed = st + n
+            if s is long_ and admitted_long_at is None:
+                admitted_long_at = clock[0]
+        for s in list(sch.running):       # finish whatever completed its prompt (keeps the pool free)
+            if s.num_computed >= s.num_tokens:
+                sch.finish(s, "stop")
+    assert admitted_long_at is not None and 1.0 <= admitted_long_at <= 1.2, admitted_long_at

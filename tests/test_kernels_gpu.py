@@ -501,3 +501,53 @@ def test_sampler_with_top_k_top_p_stays_in_the_nucleus():
     draws = ops.sample(lg.to(DEV), t.to(DEV), sd.to(DEV), top_k=torch.zeros(n, dtype=torch.int32, device=DEV),
                        top_p=torch.full((n,), 0.5, device=DEV)).cpu().long()
     assert bool(torch.isin(draws, nuc).all())
+
+
+def _moe_bank(g, E=8, H=512, F_=384):
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    w13 = rnd(E, 2 * F_, H, scale=0.05, gen=g)
+    w2 = rnd(E, H, F_, scale=0.05, gen=g)
+    w13i = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13i)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    return q13, s13, q2, s2
+
+
+@pytest.mark.parametrize("T", [700, 2500])
+def test_moe_prefill_fp8_device_pipeline(T):
+    """Prefill-size MoE with device-side routing (no host sync): grouped fp8 MFMA GEMMs over the
+    expert buckets == fp32 reference of the same fp8 arithmetic (odd T, > the route kernel's cap)."""
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(21)
+    E, H, K = 8, 512, 2
+    q13, s13, q2, s2 = _moe_bank(g, E, H)
+    h = rnd(T, H, gen=g)
+    router = rnd(E, H, scale=0.2, gen=g)
+    logits = (h.to(DEV) @ router.to(DEV).t()).contiguous()
+    out = moe.moe_prefill_fp8(h.to(DEV), logits, moe.tile_fp8_weight(q13.to(DEV)), s13.to(DEV),
+                              moe.tile_fp8_weight(q2.to(DEV)), s2.to(DEV), K)
+    ref = moe.moe_fp8_reference(h.float(), router.float(), q13, s13, q2, s2, K, quant_act=True)
+    close(out, ref, atol=3e-2)
+
+
+def test_moe_grouped_fp8_with_padding_rows():
+    """EP receive side: rows tagged with their local expert (-1 = capacity padding) in one grouped
+    call == per-row fp32 reference; padding rows come back zero."""
+    from financial_chatbot_llm_amd.ops import activation, moe
+    g = torch.Generator().manual_seed(22)
+    E, H = 4, 512
+    q13, s13, q2, s2 = _moe_bank(g, E, H)
+    M = 301
+    x = rnd(M, H, gen=g)
+    ids = torch.randint(-1, E, (M,), generator=g, dtype=torch.int32)
+    y = moe.moe_grouped_fp8(x.to(DEV), ids.to(DEV), moe.tile_fp8_weight(q13.to(DEV)), s13.to(DEV),
+                            moe.tile_fp8_weight(q2.to(DEV)), s2.to(DEV)).float().cpu()
+    for i in range(M):
+        e = int(ids[i])
+        if e < 0:
+            assert float(y[i].abs().max()) == 0.0
+            continue
+        xi = moe._fake_quant_rows(x[i:i + 1].float())
+        a = activation.silu_mul((xi @ (q13[e].float() * s13[e][:, None]).t()).to(torch.bfloat16), interleave16=True)
+        ref = moe._fake_quant_rows(a.float()) @ (q2[e].float() * s2[e][:, None]).t()
+        assert float((y[i] - ref[0]).abs().max()) <= 3e-2 * float(ref.abs().max()) + 3e-2, i
