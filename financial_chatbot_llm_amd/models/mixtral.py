@@ -14,7 +14,13 @@ Execution forms:
   epilogues, atomics-free combine.  Weights are OCP e4m3 with per-output-row scales, stored in
   MFMA-fragment tiles, halving the expert bytes streamed per decode step vs bf16.
 * otherwise (prefill, CPU, bf16 experts): tokens are bucketed by expert (``ops.moe.route``) and
-  each expert runs one GEMM pair over its bucket (hipBLASLt; fp8 experts dequantised per layer).
+  each expert runs one GEMM pair over its bucket (hipBLASLt fp8 x fp8 with per-row scales; bf16
+  or dequantised experts elsewhere).  This form reads the bucket sizes on the host once per layer.
+  A device-only form exists (``ops.moe.moe_prefill_fp8``: device routing + the grouped fp8 MFMA
+  kernels, no host sync) and is what the hipGraph / EP paths use, but at prefill sizes the
+  per-expert hipBLASLt GEMMs are 2.3-3.4x faster (T=2048-16384: 0.95-1.85 PF/s vs 0.56-0.58,
+  ``profiles/r2_moe_prefill_device_vs_hipblaslt.jsonl``) while the one host read per layer costs
+  well under 1 % of a prefill step, so prefill keeps the library GEMMs by measurement.
 
 Under TP the experts are parallelised one of two ways (``moe_parallel``):
 * ``"tp"`` (default, hipGraph decode path): every expert's intermediate dimension is sharded
