@@ -196,7 +196,8 @@ def decide_script(messages, tools) -> str:
     names = {t.name for t in tools}
     system = messages[0].content if messages else ""
     if "[retrieve_transactions]" in system:
-        if PLOT_CALL.name in names and f"[{PLOT_CALL.name}]" not in system:
+        nothing = "[retrieve_transactions] 0 transactions retrieved" in system   # nothing to plot
+        if PLOT_CALL.name in names and f"[{PLOT_CALL.name}]" not in system and not nothing:
             return format_tool_call(PLOT_CALL)
         return "No tool call"
     call = scripted_decision(messages[-1].content) if messages else None
