@@ -103,6 +103,53 @@ def bench_prefill(dev) -> List[Dict]:
     return out
 
 
+# prefill-attention launches as the 20-turn RAG workload issues them: (q_len, ctx) per sequence of
+# one mixed step -- respond chunks (~1.6-2k new tokens after a cached system prompt) next to decide
+# prompts (~200 new tokens behind ~4.6k cached ones)
+MIXED_STEPS = {
+    "respond+8decides": [(1600, 3400)] + [(220, 4600)] * 8,
+    "2respond": [(1800, 3000), (1900, 3900)],
+    "16decides": [(200, 4800)] * 16,
+    "respond-long": [(2400, 6400), (1600, 5200)],
+    "first-turn": [(4096, 4096)],
+}
+
+
+def _paged_varlen(shape, Hkv, D, dev, gen):
+    """Per-sequence contexts: (block tables [S, W], k/v caches)."""
+    nbs = [(ctx + KV_BS - 1) // KV_BS for _, ctx in shape]
+    W = max(nbs)
+    tables = torch.zeros((len(shape), W), dtype=torch.int32)
+    nxt = 0
+    for i, nb in enumerate(nbs):
+        tables[i, :nb] = torch.arange(nxt, nxt + nb, dtype=torch.int32)
+        nxt += nb
+    kc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=gen, device=dev).to(torch.bfloat16)
+    vc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=gen, device=dev).to(torch.bfloat16)
+    return tables.to(dev), kc, vc
+
+
+def bench_prefill_mixed(dev) -> List[Dict]:
+    """Prefill attention on the workload's real step shapes (varlen, prefix-cached contexts)."""
+    out = []
+    g = torch.Generator(device=dev).manual_seed(2)
+    Hq, Hkv, D = 32, 8, 128
+    for name, shape in MIXED_STEPS.items():
+        tables, kc, vc = _paged_varlen(shape, Hkv, D, dev, g)
+        qlens = [q for q, _ in shape]
+        T = sum(qlens)
+        q = torch.randn((T, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=dev)
+        lens = torch.tensor([c for _, c in shape], dtype=torch.int32, device=dev)
+        o = torch.empty_like(q)
+        us = timeit(lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o), iters=5)
+        keys = sum(ql * (c - ql) + ql * (ql + 1) / 2 for ql, c in shape)
+        flops = 4 * keys * Hq * D
+        out.append({"op": "prefill_attn_mixed", "step": name, "T": T, "us": round(us, 1),
+                    "TFLOPs": round(flops / us / 1e6, 1)})
+    return out
+
+
 def bench_elementwise(dev) -> List[Dict]:
     out = []
     for T, H in [(64, 4096), (8192, 4096)]:
@@ -161,6 +208,73 @@ def bench_gemm(dev) -> List[Dict]:
             out.append({"op": "gemm", "name": name, "M": M, "N": N, "K": K, "us": round(us, 1),
                         "GBps": round(bytes_ / us / 1e3, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)})
     return out
+
+
+def bench_gemm_prefill(dev) -> List[Dict]:
+    """hipBLASLt at the prefill-step M values the 20-turn workload produces (mixed steps of
+    ~500-4200 rows), random operands, default heuristic: where the 47 % GEMM share goes."""
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    ws = {n: torch.randn((N, K), device=dev).to(torch.bfloat16) * 0.02 for n, (N, K) in shapes.items()}
+    for M in (512, 1024, 1536, 2048, 2400, 3000, 3584, 4096, 4224):
+        tot_f, tot_us = 0.0, 0.0
+        row = {"op": "gemm_prefill", "M": M}
+        for name, (N, K) in shapes.items():
+            x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+            us = timeit(lambda: torch.nn.functional.linear(x, ws[name]), iters=10)
+            f = 2 * M * N * K
+            row[name + "_TF"] = round(f / us / 1e6, 1)
+            tot_f += f
+            tot_us += us
+        row["layer_TF"] = round(tot_f / tot_us / 1e6, 1)
+        out.append(row)
+    return out
+
+
+def bench_gemm_tune_sweep(dev) -> List[Dict]:
+    """Prefill GEMMs at every M = 256k: hipBLASLt default heuristic vs a TunableOp-tuned solution
+    (tuned here, written to ``PENNY_TUNE_OUT``): is a padded-M + tuned-solution policy worth it?"""
+    import os
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    ws = {n: torch.randn((N, K), device=dev).to(torch.bfloat16) * 0.02 for n, (N, K) in shapes.items()}
+    Ms = [256 * k for k in range(2, 17)]
+    Ks = sorted({K for _, K in shapes.values()})
+    # contiguous activations per K: TunableOp keys include the leading dimensions
+    xs = {(M, K): torch.randn((M, K), device=dev).to(torch.bfloat16) for M in Ms for K in Ks}
+    base = {}
+    for M in Ms:
+        for name, (N, K) in shapes.items():
+            x = xs[(M, K)]
+            base[(M, name)] = timeit(lambda: torch.nn.functional.linear(x, ws[name]), iters=10, rounds=3)
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(True)
+    tun.set_max_tuning_duration(60)
+    tun.set_max_tuning_iterations(40)
+    tun.set_filename(os.environ.get("PENNY_TUNE_OUT", "tunableop_prefill.csv"))
+    for M in Ms:
+        for name, (N, K) in shapes.items():
+            x = xs[(M, K)]
+            torch.nn.functional.linear(x, ws[name])      # tunes this shape
+    torch.cuda.synchronize()
+    tun.tuning_enable(False)
+    for M in Ms:
+        row = {"op": "gemm_tune", "M": M}
+        fb = ft = 0.0
+        for name, (N, K) in shapes.items():
+            x = xs[(M, K)]
+            t = timeit(lambda: torch.nn.functional.linear(x, ws[name]), iters=10, rounds=3)
+            f = 2 * M * N * K
+            row[name] = [round(f / base[(M, name)] / 1e6), round(f / t / 1e6)]
+            fb += base[(M, name)]
+            ft += t
+        tot = 2 * M * sum(N * K for N, K in shapes.values())
+        row["layer_default_TF"] = round(tot / fb / 1e6, 1)
+        row["layer_tuned_TF"] = round(tot / ft / 1e6, 1)
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    return out      # TunableOp flushes the tuned solutions to the file at exit
 
 
 def bench_skinny(dev) -> List[Dict]:
@@ -402,8 +516,9 @@ def main(argv=None) -> int:
     dev = torch.device("cuda")
     res = []
     for name in args.only.split(","):
-        res += {"decode": bench_decode, "prefill": bench_prefill, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "skinny": bench_skinny, "splitk": bench_splitk,
+        res += {"decode": bench_decode, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
+                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill,
+                "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "moe_prefill": bench_moe_prefill,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),

@@ -46,7 +46,7 @@ class ScheduledBatch:
 class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
-                 aging_s: float = 1.0, clock=time.perf_counter):
+                 aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -57,6 +57,7 @@ class Scheduler:
         self.short_output_tokens = short_output_tokens
         self.aging_s = aging_s
         self.clock = clock
+        self.token_quantum = token_quantum
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
@@ -145,7 +146,27 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
+        self._quantise(batch)
         return batch
+
+    def _quantise(self, batch: ScheduledBatch) -> None:
+        """Round the step's row count DOWN to a multiple of ``token_quantum`` by shortening its last
+        prefill chunk (those tokens run next step; nothing is padded).  The prefill GEMMs' M is the
+        step's row count, and hipBLASLt's speed swings with M between neighbouring values (1139 vs
+        1417 TF/s at M = 2816 / 2560 on the default heuristic; profiles/r2_gemm_prefill_tunableop_sweep.jsonl):
+        multiples of 256 hit tuned solutions (tuning/gemm_*.csv) and no pathological shape."""
+        q = self.token_quantum
+        if q <= 0 or not batch.prefill:
+            return
+        total = batch.num_tokens
+        r = total % q
+        if total <= q or r == 0:
+            return
+        seq, start, n = batch.prefill[-1]
+        if n <= r:
+            return
+        batch.prefill[-1] = (seq, start, n - r)
+        seq.num_prefilled -= r
 
     def finish(self, seq: Sequence, reason: str) -> None:
         seq.status = SeqStatus.FINISHED

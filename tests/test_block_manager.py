@@ -156,3 +156,22 @@ def test_scheduler_aging_is_starvation_free():
             if s.num_computed >= s.num_tokens:
                 sch.finish(s, "stop")
     assert admitted_long_at is not None and 1.0 <= admitted_long_at <= 1.2, admitted_long_at
+
+
+def test_scheduler_quantises_step_rows():
+    """Step rows (decode + prefill) are rounded down to the quantum by shortening the last chunk."""
+    bm = PyBlockManager(256, BS, True)
+    sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=1000, max_model_len=4096, token_quantum=256)
+    a = _mk_params(list(range(1000, 1700)), "a", 64, arrival=1.0)
+    b = _mk_params(list(range(3000, 3500)), "b", 64, arrival=2.0)
+    sch.add(a)
+    sch.add(b)
+    batch = sch.schedule()
+    assert batch.num_tokens == 768                      # 1000 -> 768: b's chunk 300 -> 68
+    assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("a", 0, 700), ("b", 0, 68)]
+    assert b.num_prefilled == 68
+    small = Scheduler(PyBlockManager(64, BS, True), max_num_seqs=8, max_num_batched_tokens=1000,
+                      max_model_len=4096, token_quantum=256)
+    c = _mk_params(list(range(200)), "c", 64, arrival=1.0)
+    small.add(c)
+    assert small.schedule().num_tokens == 200           # below one quantum: untouched
