@@ -83,6 +83,39 @@ def bench_decode(dev) -> List[Dict]:
     return out
 
 
+def bench_decode_mixed(dev) -> List[Dict]:
+    """Decode attention on the workload's decode batches: B rows with contexts spread over
+    1.5k-6.5k tokens, the first 1k tokens (system prompt) shared by every row (prefix cache)."""
+    out = []
+    g = torch.Generator(device=dev).manual_seed(3)
+    Hq, Hkv, D = 32, 8, 128
+    for B in (64, 96, 128):
+        rng = torch.Generator().manual_seed(B)
+        ctxs = torch.randint(1500, 6500, (B,), generator=rng).tolist()
+        shared = 1024
+        nsh = shared // KV_BS
+        W = max((c + KV_BS - 1) // KV_BS for c in ctxs)
+        tables = torch.zeros((B, W), dtype=torch.int32)
+        nxt = nsh
+        for b, c in enumerate(ctxs):
+            nb = (c + KV_BS - 1) // KV_BS
+            tables[b, :nsh] = torch.arange(nsh, dtype=torch.int32)
+            tables[b, nsh:nb] = torch.arange(nxt, nxt + nb - nsh, dtype=torch.int32)
+            nxt += nb - nsh
+        kc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        vc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        tables = tables.to(dev)
+        q = torch.randn((B, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        lens = torch.tensor(ctxs, dtype=torch.int32, device=dev)
+        ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
+        o = torch.empty_like(q)
+        us = timeit(lambda: ops.decode(q, lens, tables, kc, vc, 0.088, workspace=ws, out=o))
+        uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2
+        out.append({"op": "decode_attn_mixed", "B": B, "ctx_mean": round(sum(ctxs) / B), "us": round(us, 1),
+                    "GBps_unique": round(uniq / us / 1e3, 1)})
+    return out
+
+
 def bench_prefill(dev) -> List[Dict]:
     out = []
     g = torch.Generator(device=dev).manual_seed(1)
@@ -516,7 +549,7 @@ def main(argv=None) -> int:
     dev = torch.device("cuda")
     res = []
     for name in args.only.split(","):
-        res += {"decode": bench_decode, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
+        res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
