@@ -219,7 +219,11 @@ class ModelRunner:
         self.graph_pool = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0,
                       "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
-                      "gpu_idle_s": 0.0, "gpu_idle_gaps": 0, "_prev_end_ev": None}
+                      "gpu_idle_s": 0.0, "gpu_idle_gaps": 0, "_prev_end_ev": None, "overlap_steps": 0}
+        # TP prefill steps of >= overlap_min_rows rows run as two micro-batches whose all-reduces
+        # overlap the other half's compute (PENNY_TP_OVERLAP=0 disables)
+        self.tp_overlap = os.environ.get("PENNY_TP_OVERLAP", "1") == "1"
+        self.overlap_min_rows = int(os.environ.get("PENNY_TP_OVERLAP_MIN_ROWS", "1024"))
         self._gpu_timing = self.on_gpu and os.environ.get("PENNY_STEP_GPU_TIMING", "0") == "1"
         # sampled ids of the latest step stay on the device: the next step gathers its decode ids
         # from here when it was launched before this one's ids reached the host (overlap mode)
@@ -268,14 +272,55 @@ class ModelRunner:
         rows = ids[offset:offset + src.shape[0]]
         rows.copy_(torch.where(src >= 0, self.last_sampled[src.clamp(min=0).long()], rows))
 
-    def forward_logits(self, si: StepInputs) -> torch.Tensor:
+    def _overlap_split(self, si: StepInputs) -> Optional[int]:
+        """Row at which a TP prefill step is cut into two micro-batches (None: no overlap)."""
+        m = self.model
+        if (getattr(m, "tp_size", 1) == 1 or not self.tp_overlap or si.num_prefill_tokens < self.overlap_min_rows
+                or (hasattr(m, "uses_sp") and m.uses_sp(len(si.ids))) or not hasattr(m, "forward_overlap")):
+            return None
+        half = len(si.ids) // 2
+        t = half // 128 * 128 if half >= 512 else half       # GEMM-friendly halves on real steps
+        return max(1, min(t, si.num_prefill_tokens))
+
+    def _split_inputs(self, si: StepInputs, t: int):
+        """Two StepInputs for rows [0, t) (prefill only) and [t, T) (rest of the prefill + the
+        decodes); the sequence containing row t appears in both, its first part with the
+        context length it has after those rows."""
+        cu = si.cu_q
+        s = int(np.searchsorted(cu, t, side="right")) - 1          # sequence holding row t
+        cut = t > cu[s]                                              # row t is inside sequence s
+        na = s + (1 if cut else 0)
+        cu_a = np.concatenate([cu[:s + 1], [t]]) if cut else cu[:s + 1]
+        ctx_a = si.ctx_p[:na].copy()
+        if cut:
+            ctx_a[-1] = si.ctx_p[s] - (cu[s + 1] - t)
+        cu_b = np.concatenate([[0], cu[s + 1:] - t]) if cut else cu[s:] - t
+        empty_i = np.zeros(0, np.int32)
+        a = StepInputs(si.ids[:t], si.positions[:t], si.slots[:t], cu_a.astype(np.int32), ctx_a,
+                       si.bt_p[:na], si.max_q_len, empty_i, np.zeros((0, 1), np.int32), si.logits_idx[:0],
+                       si.temps[:0], si.seeds[:0], si.top_k[:0], si.top_p[:0], None)
+        b = StepInputs(si.ids[t:], si.positions[t:], si.slots[t:], cu_b.astype(np.int32), si.ctx_p[s:],
+                       si.bt_p[s:], si.max_q_len, si.ctx_d, si.bt_d, si.logits_idx, si.temps, si.seeds,
+                       si.top_k, si.top_p, None)
+        return a, b
+
+    def _hidden(self, si: StepInputs) -> torch.Tensor:
+        """Final hidden states of every row of the step."""
         ids = self._to_dev(si.ids)
         if si.src is not None:
             self._gather_pending(ids, self._to_dev(si.src), si.num_prefill_tokens)
         pos = self._to_dev(si.positions)
         slots = self._to_dev(si.slots)
-        meta = self._meta(si, slots)
-        h = self.model.forward(ids, pos, meta, self.kv)
+        t = self._overlap_split(si)
+        if t is not None:    # TP prefill: micro-batch pipeline overlapping the all-reduces
+            a, b = self._split_inputs(si, t)
+            metas = (self._meta(a, slots[:t]), self._meta(b, slots[t:]))
+            self.stats["overlap_steps"] += 1
+            return self.model.forward_overlap(ids, pos, metas, t, self.kv)
+        return self.model.forward(ids, pos, self._meta(si, slots), self.kv)
+
+    def forward_logits(self, si: StepInputs) -> torch.Tensor:
+        h = self._hidden(si)
         idx = self._to_dev(si.logits_idx)
         return self.model.logits(h.index_select(0, idx))
 
@@ -326,10 +371,7 @@ class ModelRunner:
         return PendingStep(None, n, host, ev, start_ev, self.stats, "gpu_graph_s" if graph else "gpu_eager_s")
 
     def _forward_only(self, si: StepInputs) -> None:
-        ids = self._to_dev(si.ids)
-        pos = self._to_dev(si.positions)
-        slots = self._to_dev(si.slots)
-        self.model.forward(ids, pos, self._meta(si, slots), self.kv)
+        self._hidden(si)
 
     # ------------------------------------------------------------------------------------
     # hipGraph decode

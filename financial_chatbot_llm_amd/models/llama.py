@@ -210,6 +210,45 @@ class DecoderModel:
         h = ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
         return comm.tp_all_gather_rows(h)[:T]
 
+    def forward_overlap(self, ids: torch.Tensor, positions: torch.Tensor, metas, split: int,
+                        kv: KVCache) -> torch.Tensor:
+        """TP forward with the row-parallel all-reduces overlapped with compute (C1 overlap).
+
+        The step's rows are cut into two micro-batches at row ``split`` (``metas`` holds each
+        one's attention metadata; a sequence cut in two appears in both, its second part seeing
+        the first part's KV, which is written earlier on the same stream).  Per layer::
+
+            attn(A) -> AR(A) starts | attn(B) -> AR(B) starts | wait A: norm, mlp(A) -> AR(A) ...
+
+        so each half's all-reduce is on the wire (RCCL's stream) while the other half computes,
+        instead of every all-reduce stalling the whole batch.  Same arithmetic as ``forward``."""
+        c = self.cfg
+        x = self.embed(ids)
+        xs = [x[:split], x[split:]]
+        pos = [positions[:split], positions[split:]]
+        res = [xs[0], xs[1]]
+        hs = [ops.rms_norm(xs[k], self.w["layers.0.in_norm"], c.norm_eps) for k in (0, 1)]
+        pend = [None, None]
+        for i in range(c.num_layers):
+            p = f"layers.{i}."
+            outs = [None, None]
+            for k in (0, 1):
+                if i > 0:
+                    pend[k].wait()
+                    hs[k] = ops.rms_norm(xs[k], self.w[p + "in_norm"], c.norm_eps, residual=res[k])
+                outs[k] = self.attention(i, hs[k], pos[k], metas[k], kv, reduce=False)
+                pend[k] = comm.tp_all_reduce_async(outs[k])
+            for k in (0, 1):
+                pend[k].wait()
+                hs[k] = ops.rms_norm(outs[k], self.w[p + "post_norm"], c.norm_eps, residual=res[k])
+                xs[k] = self.mlp(i, hs[k], reduce=False)
+                # expert-parallel MoE outputs come back complete (all-gathered): nothing to reduce
+                pend[k] = comm._Done() if getattr(self, "ep", False) else comm.tp_all_reduce_async(xs[k])
+        for k in (0, 1):
+            pend[k].wait()
+        x = torch.cat(xs)
+        return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=torch.cat(res))
+
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         if self.uses_sp(ids.shape[0]):
             return self.forward_sp(ids, positions, meta, kv)

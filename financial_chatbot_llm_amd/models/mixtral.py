@@ -135,7 +135,9 @@ class MixtralModel(DecoderModel):
             return F.linear(act, self._dequant(p, "w2", e))
         return F.linear(ops.silu_mul(F.linear(rows, self.w[p + "w13"][e])), self.w[p + "w2"][e])
 
-    def mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True) -> torch.Tensor:
+        """``reduce=False``: return the TP partial sum (the overlapped forward all-reduces it);
+        expert-parallel outputs are already complete (all-gathered) either way."""
         p = f"layers.{i}."
         c = self.cfg
         T = h.shape[0]
@@ -155,7 +157,7 @@ class MixtralModel(DecoderModel):
             out = moe_ops.moe_decode_fp8(h.contiguous(), logits.contiguous(), self.w[p + "w13_t"],
                                          self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
                                          c.top_k_experts, self._moe_workspace(T))
-            return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+            return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
         topw, topi = moe_ops.topk_softmax(logits, c.top_k_experts)
         order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
         offs = offsets.tolist()
@@ -167,4 +169,4 @@ class MixtralModel(DecoderModel):
                 ys[a:b] = self._expert(p, xs[a:b], e)
         # every sorted row is written above (the buckets tile [0, T*k)); weighted gather-combine
         out = moe_ops.combine_weighted(ys, order, tok_w, T, c.top_k_experts)
-        return comm.tp_all_reduce(out) if self.tp_size > 1 else out
+        return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out

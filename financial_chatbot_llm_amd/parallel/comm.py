@@ -1,7 +1,9 @@
 """Tensor-parallel collectives over RCCL/xGMI.
 
 * C1 ``tp_all_reduce``: the partial sums after the row-parallel O-projection and
-  down-projection (2 per layer).  In-place ``dist.all_reduce`` on the TP group; captured into
+  down-projection (2 per layer).  ``tp_all_reduce_async`` starts one without blocking the host:
+  the prefill micro-batch pipeline (``DecoderModel.forward_overlap``) computes one half of the
+  batch while the other half's all-reduce is on the wire.  In-place ``dist.all_reduce`` on the TP group; captured into
   the decode hipGraph together with the GEMMs.
 * C2 ``tp_all_gather_last``: vocab-parallel LM-head logits ([B, V/tp] -> [B, V]); embedding
   partials are summed with C1.
@@ -61,6 +63,25 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
         return _CUSTOM_AR.all_reduce(x, out=x)   # reads peers' staged copies, so in-place is safe
     dist.all_reduce(x, group=s.tp_group)
     return x
+
+
+class _Done:
+    def wait(self) -> None:
+        return None
+
+
+def tp_all_reduce_async(x: torch.Tensor):
+    """Start the TP all-reduce of ``x`` (in place) and return a handle whose ``wait()`` orders the
+    CURRENT stream after it -- the host is not blocked, so compute queued meanwhile overlaps the
+    transfer (RCCL runs the collective on its own stream).  Decode-size messages that the custom
+    one-shot kernel takes are latency-bound and run inline (nothing to overlap)."""
+    s = state()
+    if s.tp_size == 1:
+        return _Done()
+    if _CUSTOM_AR is not None and _CUSTOM_AR.eligible(x):
+        _CUSTOM_AR.all_reduce(x, out=x)
+        return _Done()
+    return dist.all_reduce(x, group=s.tp_group, async_op=True)
 
 
 def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:

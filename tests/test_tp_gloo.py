@@ -23,8 +23,10 @@ def _free_port() -> int:
 
 
 def _worker(rank, world, port, q):
+    # PENNY_TP_OVERLAP_MIN_ROWS=16: the engine's prefill steps (<= 64 rows here) run the micro-batch
+    # pipeline with the all-reduces overlapped (rows cut inside a sequence and between sequences)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT=str(port), PENNY_TP_OVERLAP_MIN_ROWS="16")
     try:
         from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
         from financial_chatbot_llm_amd.engine.tokenizer import SyntheticLlamaTokenizer
@@ -49,6 +51,7 @@ def _worker(rank, world, port, q):
             out = eng.generate([list(range(10, 90)), list(range(200, 230))],
                                SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
             eng.stop_followers()
+            assert eng.runner.stats["overlap_steps"] >= 2, eng.runner.stats
         else:
             eng.follower_loop()
         q.put((rank, logits_tp, out))

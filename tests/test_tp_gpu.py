@@ -43,6 +43,7 @@ def _run(tp: int, rank: int = 0, graphs: bool = False):
     out = eng.generate(PROMPTS, SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
     if tp > 1:
         eng.stop_followers()
+        assert eng.runner.stats["overlap_steps"] > 0     # prefill ran the overlapped micro-batches
     if graphs:
         assert eng.runner.stats["graph_steps"] > 0
     return out
@@ -50,7 +51,7 @@ def _run(tp: int, rank: int = 0, graphs: bool = False):
 
 def _worker(rank, world, port, q, graphs=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port), PENNY_SPLITK="force")
+                      MASTER_PORT=str(port), PENNY_SPLITK="force", PENNY_TP_OVERLAP_MIN_ROWS="64")
     try:
         from financial_chatbot_llm_amd.parallel import comm
         from financial_chatbot_llm_amd.parallel.dist import init_distributed, shutdown
