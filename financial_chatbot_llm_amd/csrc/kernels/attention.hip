@@ -175,7 +175,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
                                             const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
                                             bf16* __restrict__ out, float scale_log2, int Hq, int Hkv,
                                             int max_blocks, int causal_arg, int s, int h, int tile, int chunk,
-                                            const CascadeArgs& ca) {
+                                            const CascadeArgs& ca, float* __restrict__ lse = nullptr) {
   constexpr int KC = D / 32;                 // k-chunks of the QK^T product
   constexpr int DT = D / 16;                 // 16-row dim tiles of O^T
   constexpr int TILE = KV_BS * D * 2;        // bytes of one K (or V) block tile
@@ -284,6 +284,8 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
       for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
       *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
     }
+    if (lse != nullptr && g == 0)   // natural-log sum-exp of the scaled scores (ring-attention merge)
+      lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
   }
 }
 
@@ -291,10 +293,11 @@ template <int D>
 __global__ void __launch_bounds__(256, 2) prefill_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
+    float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) char smem[prefill_smem_bytes<D>()];  // [buf][K|V]
   attend_tile<D, false>(smem, q, cu_q, ctx_lens, block_tables, k_cache, v_cache, out, scale_log2, Hq, Hkv,
-                        max_blocks, causal, blockIdx.z, blockIdx.y, blockIdx.x, 0, CascadeArgs{});
+                        max_blocks, causal, blockIdx.z, blockIdx.y, blockIdx.x, 0, CascadeArgs{}, lse);
 }
 
 // grid (W, Hkv): a fixed-size grid (hipGraph-capturable) strides over the device-side work list
@@ -498,7 +501,8 @@ template <int D, int NW, int NBUF, bool HEAD_FAST>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal) {
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
+    float* __restrict__ lse) {
   constexpr int KC = D / 32, DT = D / 16;
   constexpr int TILE = KV_BS * D * 2;         // bytes of one K (or V) block tile
   constexpr int PIECES = TILE / 1024 / NW;    // 1-KiB glds pieces per wave per tile
@@ -605,13 +609,15 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
       for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
       *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
     }
+    if (lse != nullptr && g == 0)
+      lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
   }
 }
 
 PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                       const void* k_cache, const void* v_cache, void* out, int num_seqs,
                                       int max_q_len, int Hq, int Hkv, int D, int max_blocks, float scale, int causal,
-                                      hipStream_t stream) {
+                                      float* lse, hipStream_t stream) {
   if (num_seqs <= 0 || max_q_len <= 0) return 0;
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv;
@@ -634,15 +640,15 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   if (big && head_fast)                                                                                          \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), dim3(Hkv, ntiles, num_seqs), dim3(512), 0, stream,     \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal);                                              \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse);                                         \
   else if (big)                                                                                                  \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, false>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q,     \
                        ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,    \
-                       Hkv, max_blocks, causal);                                                                   \
+                       Hkv, max_blocks, causal, lse);                                                              \
   else                                                                                                           \
     hipLaunchKernelGGL(prefill_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens,           \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \
-                       max_blocks, causal);
+                       max_blocks, causal, lse);
   if (D == 128) {
     PREFILL_LAUNCH(128)
   } else if (D == 64) {

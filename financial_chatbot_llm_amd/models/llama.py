@@ -249,6 +249,44 @@ class DecoderModel:
         x = torch.cat(xs)
         return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=torch.cat(res))
 
+    def forward_cp(self, ids: torch.Tensor, total_len: int, group=None, kv_sink=None) -> torch.Tensor:
+        """Context-parallel prefill of ONE long prompt (SURVEY §5.7 stretch path, >128k tokens).
+
+        ``ids`` is this rank's zig-zag shard (``parallel.context.zigzag_shard``) of a
+        ``total_len``-token prompt; every CP rank holds the full weights (TP=1 inside the CP
+        group).  Each layer: QKV on the local rows, RoPE at the rows' GLOBAL positions, ring
+        attention over the CP group (K/V shards travel one xGMI hop per step; blocks on the HIP
+        prefill kernel on the GPU), then O / MLP on the local rows.  Returns the final hidden
+        states of the local rows.  ``kv_sink(layer, k, v)`` receives each layer's local K/V shard
+        (``zigzag_unshard`` of every rank's shards is the full cache for the decode rank)."""
+        from ..ops.attention import _rope_ref
+        from ..parallel import context as cpx
+        import torch.distributed as dist
+        c = self.cfg
+        cp = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        pos = cpx.zigzag_positions(total_len, cp, rank, device=ids.device)
+        block = cpx.hip_block_attention if ops._native.use_native(self.w["embed"]) else cpx.torch_block_attention
+        x = ops.embedding(ids, self.w["embed"])
+        residual = x
+        h = ops.rms_norm(x, self.w["layers.0.in_norm"], c.norm_eps)
+        T = ids.shape[0]
+        for i in range(c.num_layers):
+            p = f"layers.{i}."
+            if i > 0:
+                h = ops.rms_norm(x, self.w[p + "in_norm"], c.norm_eps, residual=residual)
+            qkv = linear(h, self.w[p + "qkv"]).view(T, self.hq + 2 * self.hkv, self.D)
+            q = _rope_ref(qkv[:, :self.hq], pos, self.cos_sin).to(h.dtype).contiguous()
+            k = _rope_ref(qkv[:, self.hq:self.hq + self.hkv], pos, self.cos_sin).to(h.dtype).contiguous()
+            v = qkv[:, self.hq + self.hkv:].contiguous()
+            if kv_sink is not None:
+                kv_sink(i, k, v)
+            a = cpx.ring_attention(q, k, v, total_len, scale=self.scale, causal=True, group=group, block_fn=block)
+            a = linear(a.reshape(T, self.hq * self.D), self.w[p + "o"])
+            h = ops.rms_norm(a, self.w[p + "post_norm"], c.norm_eps, residual=residual)
+            x = self.mlp(i, h)
+        return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
+
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata, kv: KVCache) -> torch.Tensor:
         if self.uses_sp(ids.shape[0]):
             return self.forward_sp(ids, positions, meta, kv)

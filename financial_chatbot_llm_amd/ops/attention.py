@@ -162,9 +162,12 @@ def _attend_ref(q, k, v, scale, causal_offset: Optional[int]):
 
 def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor,
             k_cache: torch.Tensor, v_cache: torch.Tensor, scale: float, causal: bool = True,
-            max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None,
+            lse: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Varlen paged attention for the new tokens of S sequences (chunked prefill / prefix hits:
-    query i of sequence s sits at absolute position ctx_lens[s] - q_len[s] + i)."""
+    query i of sequence s sits at absolute position ctx_lens[s] - q_len[s] + i).  ``lse`` [T, Hq]
+    f32 (optional) receives each row's natural-log sum-exp of the scaled scores (-inf: no key
+    visible) -- what a ring-attention merge needs."""
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     S = block_tables.shape[0]
@@ -175,7 +178,7 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
             max_q_len = int((cu_q[1:] - cu_q[:-1]).max().item())
         N.call("penny_attention_prefill", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),
                N.ptr(k_cache), N.ptr(v_cache), N.ptr(out), S, int(max_q_len), Hq, Hkv, D, block_tables.shape[1],
-               float(scale), int(causal), N.stream())
+               float(scale), int(causal), N.ptr(lse) if lse is not None else None, N.stream())
         return out
     out = torch.empty_like(q) if out is None else out
     cu = cu_q.tolist()
@@ -186,7 +189,20 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
             continue
         k, v = gather_kv_ref(k_cache, v_cache, block_tables[s], ctx[s])
         out[a:b] = _attend_ref(q[a:b], k, v, scale, ctx[s] - (b - a) if causal else None).to(q.dtype)
+        if lse is not None:
+            lse[a:b] = _lse_ref(q[a:b], k, scale, ctx[s] - (b - a) if causal else None)
     return out
+
+
+def _lse_ref(q: torch.Tensor, k: torch.Tensor, scale: float, q_offset: Optional[int]) -> torch.Tensor:
+    """[Tq, Hq] natural-log sum-exp of the scaled (masked) scores, fp32."""
+    G = q.shape[1] // k.shape[1]
+    kk = k.float().repeat_interleave(G, dim=1)
+    s = torch.einsum("qhd,khd->hqk", q.float(), kk) * scale
+    if q_offset is not None:
+        qi = torch.arange(q.shape[0])[:, None] + q_offset
+        s = s.masked_fill((torch.arange(k.shape[0])[None, :] > qi)[None], float("-inf"))
+    return torch.logsumexp(s, dim=-1).transpose(0, 1)
 
 
 @dataclass

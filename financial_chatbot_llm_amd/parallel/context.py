@@ -19,8 +19,17 @@ Design, for xGMI's point-to-point links:
 * **Merge.** Each block yields ``(o, lse)`` in fp32; blocks combine with the log-sum-exp rule,
   so the result equals one softmax over the whole key range.
 
-``block_fn`` computes one ``(q-shard × kv-shard)`` block and returns ``(o, lse)``; the default is
-an fp32 torch implementation (GQA, position mask) that runs on CPU (gloo tests) and GPU alike.
+``block_fn`` computes one ``(q-shard × kv-shard)`` block and returns ``(o, lse)``:
+
+* :func:`hip_block_attention` (GPU): the shard pair is cut into its contiguous position chunks;
+  each (q chunk, kv chunk) pair is fully visible, causal-diagonal or fully masked under the
+  zig-zag layout, so it runs on the paged MFMA prefill kernel (K6) -- non-causal or causal, the
+  kv chunk staged into a scratch paged cache by the KV writer -- which also emits each row's
+  log-sum-exp;
+* :func:`torch_block_attention`: fp32 torch (GQA, any position mask), CPU tests and fallback.
+
+:meth:`~..models.llama.DecoderModel.forward_cp` runs a whole decoder over one long prompt this
+way (each rank: its zig-zag rows through every layer; ring attention per layer).
 """
 from __future__ import annotations
 
@@ -78,6 +87,77 @@ def torch_block_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos
     return o, lse
 
 
+def _runs(pos: torch.Tensor):
+    """Contiguous runs of a sorted position vector -> [(row0, n, pos0)]."""
+    p = pos.tolist()
+    out, start = [], 0
+    for i in range(1, len(p) + 1):
+        if i == len(p) or p[i] != p[i - 1] + 1:
+            out.append((start, i - start, p[start]))
+            start = i
+    return out
+
+
+class _Scratch:
+    """Reusable scratch paged KV cache for one kv chunk (fragment-native layout)."""
+
+    def __init__(self):
+        self.kc = self.vc = None
+
+    def get(self, nblocks: int, hkv: int, d: int, dtype, device):
+        from ..ops.attention import KV_BS
+        if self.kc is None or self.kc.shape[0] < nblocks or self.kc.shape[1] != hkv or self.kc.device != device:
+            self.kc = torch.zeros((nblocks, hkv, KV_BS * d), dtype=dtype, device=device)
+            self.vc = torch.zeros_like(self.kc)
+        return self.kc, self.vc
+
+
+_SCRATCH = _Scratch()
+
+
+def hip_block_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos_q: torch.Tensor,
+                        pos_k: torch.Tensor, scale: float, causal: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One ring block on the HIP prefill kernel: (o [Tq,Hq,D] f32, lse [Hq,Tq]).
+
+    Each (q run, kv run) pair is fully visible (all keys before every query), the causal diagonal
+    (same positions), or fully masked (skipped); anything else -- never produced by the zig-zag
+    layout -- falls back to :func:`torch_block_attention` for that pair."""
+    from .. import ops
+    from ..ops.attention import KV_BS
+    Tq, Hq, D = q.shape
+    Hkv = k.shape[1]
+    o = torch.zeros((Tq, Hq, D), dtype=torch.float32, device=q.device)
+    lse = torch.full((Hq, Tq), float("-inf"), dtype=torch.float32, device=q.device)
+    q_runs, k_runs = _runs(pos_q), _runs(pos_k)
+    for kr, kn, kp in k_runs:
+        nb = (kn + KV_BS - 1) // KV_BS
+        kc, vc = _SCRATCH.get(nb, Hkv, D, k.dtype, k.device)
+        qkv = torch.cat([k.new_zeros((kn, Hq * D)), k[kr:kr + kn].reshape(kn, Hkv * D),
+                         v[kr:kr + kn].reshape(kn, Hkv * D)], dim=1)
+        slots = torch.arange(kn, dtype=torch.int32, device=k.device)
+        ops.rope_kv_write(qkv, slots, None, slots, kc, vc, Hq, Hkv, D, apply_rope=False)
+        bt = torch.arange(nb, dtype=torch.int32, device=k.device)[None]
+        for qr, qn, qp in q_runs:
+            if causal and kp > qp + qn - 1:
+                continue                                           # every key after every query
+            full = (not causal) or kp + kn - 1 <= qp
+            diag = causal and kp == qp and kn == qn
+            if full or diag:
+                ob = torch.empty((qn, Hq, D), dtype=q.dtype, device=q.device)
+                lb = torch.empty((qn, Hq), dtype=torch.float32, device=q.device)
+                ops.prefill(q[qr:qr + qn].contiguous(), torch.tensor([0, qn], dtype=torch.int32, device=q.device),
+                            torch.tensor([kn], dtype=torch.int32, device=q.device), bt, kc, vc, scale,
+                            causal=diag, max_q_len=qn, out=ob, lse=lb)
+                ob, lb = ob.float(), lb.transpose(0, 1)
+            else:
+                ob, lb = torch_block_attention(q[qr:qr + qn], k[kr:kr + kn], v[kr:kr + kn], pos_q[qr:qr + qn],
+                                               pos_k[kr:kr + kn], scale, causal)
+            mo, ml = merge_blocks(o[qr:qr + qn], lse[:, qr:qr + qn], ob, lb)
+            o[qr:qr + qn] = mo
+            lse[:, qr:qr + qn] = ml
+    return o, lse
+
+
 def merge_blocks(o_a: torch.Tensor, lse_a: torch.Tensor, o_b: torch.Tensor,
                  lse_b: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Log-sum-exp merge of two partial softmax blocks (o [T,H,D] fp32, lse [H,T])."""
@@ -111,12 +191,16 @@ def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, total_len:
     scale = scale if scale is not None else q.shape[-1] ** -0.5
     pos_q = zigzag_positions(total_len, cp, r, device=q.device)
     kv = torch.stack([k, v]).contiguous()                                   # one message per hop
+    # gloo (CPU rehearsals of the GPU path) moves host tensors only: stage the hop through host
+    # memory; RCCL sends the device buffer directly over xGMI
+    host_hop = kv.is_cuda and dist.get_backend(group) == "gloo"
     o = lse = None
     for step in range(cp):
         reqs = []
         if step + 1 < cp:                                                   # post next hop first
-            nxt_kv = torch.empty_like(kv)
-            ops_ = [dist.P2POp(dist.isend, kv, nxt, group), dist.P2POp(dist.irecv, nxt_kv, prv, group)]
+            send = kv.cpu() if host_hop else kv
+            nxt_kv = torch.empty_like(send)
+            ops_ = [dist.P2POp(dist.isend, send, nxt, group), dist.P2POp(dist.irecv, nxt_kv, prv, group)]
             reqs = dist.batch_isend_irecv(ops_)
         src = (r - step) % cp
         pos_k = zigzag_positions(total_len, cp, src, device=q.device)
@@ -125,5 +209,5 @@ def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, total_len:
         for req in reqs:
             req.wait()
         if step + 1 < cp:
-            kv = nxt_kv
+            kv = nxt_kv.to(q.device) if host_hop else nxt_kv
     return o.to(q.dtype)

@@ -95,3 +95,60 @@ def test_ring_attention_matches_single_process(world):
     for causal in (True, False):
         got = cpx.zigzag_unshard([res[r][causal] for r in range(world)])
         assert torch.allclose(got, _full(q, k, v, causal), atol=1e-5), causal
+
+
+def _cp_model_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import torch.distributed as dist
+
+        from financial_chatbot_llm_amd.models.configs import get_model_config
+        from financial_chatbot_llm_amd.models.llama import LlamaModel
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        cfg = get_model_config("llama-tiny")
+        m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=9, std=0.05)
+        total = 24 * world
+        ids = torch.arange(7, 7 + total, dtype=torch.int32)
+        local = cpx.zigzag_shard(ids, world, rank)
+        shards = {}
+        h = m.forward_cp(local, total, kv_sink=lambda i, k, v: shards.setdefault(i, (k, v)))
+        parts = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(parts, h.contiguous())
+        full_h = cpx.zigzag_unshard(parts)
+        q.put((rank, m.logits(full_h).detach().numpy(), tuple(tuple(t.shape) for t in shards[0])))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 3])
+def test_model_forward_cp_matches_single_process_prefill(world):
+    """A whole Llama decoder prefilled context-parallel (zig-zag shards, ring attention per layer,
+    RoPE at global positions) reproduces the single-process prefill logits of every token."""
+    from financial_chatbot_llm_amd.models.configs import get_model_config
+    from financial_chatbot_llm_amd.models.llama import LlamaModel
+    from test_model_parity import _prefill_logits
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cp_model_worker, args=(r, world, port, qq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = qq.get(timeout=200)
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert not (isinstance(v[0], str) and v[0] == "ERR"), v[1]
+    cfg = get_model_config("llama-tiny")
+    ref = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=9, std=0.05)
+    want = _prefill_logits(ref, list(range(7, 7 + 24 * world)))
+    for r in range(world):
+        got = torch.from_numpy(res[r][0])
+        assert torch.allclose(got, want, atol=1e-4, rtol=1e-4), (got - want).abs().max()
+        assert res[r][1][0] == (24, cfg.num_kv_heads, cfg.head_dim)       # local K shard per layer
