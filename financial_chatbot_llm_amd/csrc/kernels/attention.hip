@@ -582,14 +582,23 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  // Waves whose 32 rows are all padding (the last tile of a short chunk, e.g. a decide prompt's
+  // 200 new tokens behind 4.6k cached ones) and, under the causal mask, blocks entirely after a
+  // wave's last row: the wave still stages its K/V pieces and meets every barrier, but skips the
+  // MFMAs and the softmax, leaving its SIMD's issue slots to the live wave sharing it.
+  const int wave_tok0 = tok0 + (w * 32) / G;
+  const bool wave_live = wave_tok0 < qlen;
+  const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
+  const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
   for (int j = 0; j < nblk; ++j) {
     // my pieces of block j landed (younger blocks j+1.. may stay in flight), then publish
     if (j + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
     else wait_vmcnt_barrier<0>();
     if (j + NBUF - 1 < nblk) stage(j + NBUF - 1);   // refills the buffer everyone finished at j-1
+    if (!wave_live || j * KV_BS >= wave_kv_end) continue;
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
-    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0);
+    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
     if (full) attend_block<D, false>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
     else attend_block<D, true>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
   }
