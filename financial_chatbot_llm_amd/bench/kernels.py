@@ -264,6 +264,17 @@ def bench_gemm_prefill(dev) -> List[Dict]:
     return out
 
 
+def bench_lm_head(dev) -> List[Dict]:
+    """LM head (vocab 128256) at the sampler counts of real steps: weight-streaming bound."""
+    out = []
+    w = torch.randn((128256, 4096), device=dev).to(torch.bfloat16) * 0.02
+    for M in (1, 16, 48, 64, 96, 128, 160, 192, 256):
+        x = torch.randn((M, 4096), device=dev).to(torch.bfloat16)
+        us = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
+        out.append({"op": "lm_head", "M": M, "us": round(us, 1), "TBps": round(w.numel() * 2 / us / 1e6, 2)})
+    return out
+
+
 def bench_gemm_tune_sweep(dev) -> List[Dict]:
     """Prefill GEMMs at every M = 256k: hipBLASLt default heuristic vs a TunableOp-tuned solution
     (tuned here, written to ``PENNY_TUNE_OUT``): is a padded-M + tuned-solution policy worth it?"""
@@ -550,7 +561,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill,
+                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "moe_prefill": bench_moe_prefill,
