@@ -215,13 +215,18 @@ class DecodeWorkspace:
     part_stride: int = 0    # partition slots per (row, head): nparts suffix + cascade chunk slots
 
     def partitioning(self, B: int):
-        """(pb, nparts) for a decode batch of B rows.  Large batches already fill the chip with
-        (row, head) work, so they take longer partitions: fewer empty workgroups in the fixed
-        hipGraph grid and fewer partials to merge (B=128: pb 16 is 10-16 % faster than 8;
-        profiles/r1_decode_partition.jsonl).  Small batches keep pb=8 for parallelism."""
+        """(pb, nparts) for a decode batch of B rows.  Batches of 32+ rows already fill the chip
+        with (row, head) work, so they take long partitions: fewer empty workgroups in the fixed
+        hipGraph grid, fewer per-workgroup prologues/merges and fewer partials to reduce."""
         if os.environ.get("PENNY_DECODE_FIXED_PB") == "1":
             return self.pb, self.nparts
-        pb = self.pb if B < 96 else (2 * self.pb if B < 192 else 4 * self.pb)
+        # B >= 32: 2048-key partitions (pb 32) -- the workload's batches (B 64-128, contexts
+        # 1.5-6.5k) run 3-10 % faster than with 512/1024-key ones (r2_decode_partition_sweep.txt);
+        # small batches keep 512-key partitions for parallelism (B=16: 18.5 vs 24.4 us).
+        # PENNY_DECODE_PB_SCALE="small,large" overrides the multipliers (A/B knob).
+        scale = os.environ.get("PENNY_DECODE_PB_SCALE")
+        mult = tuple(int(x) for x in scale.split(",")) if scale else (1, 4)
+        pb = self.pb * (mult[0] if B < 32 else mult[-1])
         nblk = self.nparts * self.pb
         return pb, (nblk + pb - 1) // pb
 
