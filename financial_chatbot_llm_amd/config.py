@@ -133,6 +133,7 @@ class EngineConfig:
     def from_env(cls, **overrides) -> "EngineConfig":
         c = cls(
             model=_env("PENNY_MODEL", cls.model),
+            dtype=_env("PENNY_DTYPE", cls.dtype),
             weights=os.getenv("PENNY_WEIGHTS") or None,
             tokenizer=os.getenv("PENNY_TOKENIZER") or None,
             tp_size=_env_int("PENNY_TP", cls.tp_size),
