@@ -136,7 +136,7 @@ class LLMAgent:
         logger.info("Deciding if transaction retrieval is needed")
         result = await self.llm.agenerate(self.decide_messages(state), tools=self.bound_tools,
                                           temperature=self.temperature, max_tokens=self.max_decide_tokens,
-                                          purpose="decide")
+                                          purpose="decide", ephemeral_kv=bool(state["tool_results"]))
         logger.info(f"Decide Retrieval Response: {result.text!r} tool_calls={[t.to_dict() for t in result.tool_calls]}")
         if result.tool_calls:
             tc = result.tool_calls[0]  # only the first call is honoured (llm_agent.py:100)
@@ -177,7 +177,8 @@ class LLMAgent:
         logger.info("Generating final response")
         parts = []
         async for piece in self.llm.astream(self.respond_messages(state), temperature=self.temperature,
-                                            max_tokens=self.max_response_tokens, purpose="respond"):
+                                            max_tokens=self.max_response_tokens, purpose="respond",
+                                            ephemeral_kv=bool(state["tool_results"])):
             parts.append(piece)
         state["final_response"] = "".join(parts)
         logger.info("Final response generated")
@@ -234,7 +235,8 @@ class LLMAgent:
             yield {"type": "status", "message": "No transaction data retrieval needed"}
         yield {"type": "status", "message": "Generating response..."}
         async for piece in self.llm.astream(self.respond_messages(state), temperature=self.temperature,
-                                            max_tokens=self.max_response_tokens, purpose="respond"):
+                                            max_tokens=self.max_response_tokens, purpose="respond",
+                                            ephemeral_kv=bool(state["tool_results"])):
             if piece:
                 yield {"type": "response_chunk", "content": piece}
         yield {"type": "complete", "message": "Query processing completed"}

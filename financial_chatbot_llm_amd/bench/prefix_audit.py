@@ -44,7 +44,7 @@ class AuditEngine:
     manager when requests do not overlap in time; overlap is modelled by ``hold`` (requests keep
     their blocks until ``hold`` later requests finished)."""
 
-    def __init__(self, num_blocks: int, seed: int = 0, hold: int = 0, policy: str = "lru"):
+    def __init__(self, num_blocks: int, seed: int = 0, hold: int = 0, policy: str = "lru", hints: bool = True):
         self.tokenizer = SyntheticLlamaTokenizer()
         self.bm = make_block_manager(num_blocks, 64, True, prefer_native=False)
         if hasattr(self.bm, "set_policy"):
@@ -52,6 +52,7 @@ class AuditEngine:
         self.rng = random.Random(seed)
         self.calls: List[Dict] = []
         self.hold = hold
+        self.hints = hints          # honour the agent's ephemeral_kv retention hint
         self._held: List[Sequence] = []
 
     def _run(self, prompt_ids, params: SamplingParams, purpose: str, conv: str = "") -> Sequence:
@@ -80,12 +81,14 @@ class AuditEngine:
                            "computed": len(prompt_ids) - cached, "out": len(seq.output_ids)})
         self._held.append(seq)
         while len(self._held) > self.hold:
-            self.bm.free(self._held.pop(0))
+            done = self._held.pop(0)
+            self.bm.free(done, evict_first=self.hints and done.params.ephemeral_kv)
         return seq
 
     def _release_all(self):
         while self._held:
-            self.bm.free(self._held.pop(0))
+            done = self._held.pop(0)
+            self.bm.free(done, evict_first=self.hints and done.params.ephemeral_kv)
 
     async def generate_all(self, prompt_ids, params):
         seq = self._run(prompt_ids, params, "decide")
@@ -113,11 +116,11 @@ class _FakeRetrieval:
 
 
 async def _replay(convs: int, turns: int, num_blocks: int, respond_tokens: int, hold: int, policy: str,
-                  warmup: int):
+                  warmup: int, hints: bool = True):
     from ..engine.backend import EngineLLM
     from .workload import RagWorkload, decide_script
 
-    eng = AuditEngine(num_blocks, hold=hold, policy=policy)
+    eng = AuditEngine(num_blocks, hold=hold, policy=policy, hints=hints)
     llm = EngineLLM(eng, max_model_len=8192, decide_script=decide_script, respond_ignore_eos=True,
                     respond_tokens=respond_tokens)
     wl = RagWorkload(llm, _FakeRetrieval(), convs, 10_000, respond_tokens)
@@ -155,12 +158,15 @@ def main(argv=None) -> int:
     ap.add_argument("--pool", type=int, default=0, help="KV blocks (0 = infinite: structural minimum)")
     ap.add_argument("--hold", type=int, default=0, help="requests in flight (blocks pinned)")
     ap.add_argument("--policy", default="lru")
+    ap.add_argument("--no-hints", action="store_true", help="ignore the agent's ephemeral_kv hint (plain LRU)")
     ap.add_argument("--per-turn", action="store_true")
     a = ap.parse_args(argv)
     pool = a.pool or 10_000_000
-    summary, per_turn = asyncio.run(_replay(a.convs, a.turns, pool, a.respond_tokens, a.hold, a.policy, a.warmup))
+    summary, per_turn = asyncio.run(_replay(a.convs, a.turns, pool, a.respond_tokens, a.hold, a.policy, a.warmup,
+                                        not a.no_hints))
     print(json.dumps({"convs": a.convs, "turns": a.turns, "warmup": a.warmup, "pool_blocks": a.pool or "inf",
-                      "policy": a.policy, "per_turn_timed_mean": summary}))
+                      "policy": a.policy, "hold": a.hold, "hints": not a.no_hints,
+                      "per_turn_timed_mean": summary}))
     if a.per_turn:
         for p in per_turn:
             print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in p.items()}))

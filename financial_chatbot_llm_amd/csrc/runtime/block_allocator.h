@@ -148,15 +148,28 @@ class BlockAllocator {
     return it == seqs_.end() ? std::vector<int>{} : it->second.table;
   }
 
-  void free(int seq) {
+  // Release a sequence.  Cached blocks [0, keep_blocks) join the LRU tail (tail block first, so
+  // a chain is evicted leaf-first); blocks [keep_blocks, end) -- KV the caller knows will not be
+  // asked for again, e.g. a prompt around a one-off retrieval context -- join the LRU HEAD and
+  // are recycled before any other cached block.  keep_blocks < 0: keep everything.
+  void free(int seq, int keep_blocks = -1) {
     auto it = seqs_.find(seq);
     if (it == seqs_.end()) return;
     const std::vector<int>& t = it->second.table;
-    for (auto r = t.rbegin(); r != t.rend(); ++r) {  // tail first: later blocks evict first
-      Block& blk = blocks_[*r];
+    const int n = (int)t.size();
+    const int keep = keep_blocks < 0 ? n : std::min(keep_blocks, n);
+    for (int i = keep; i < n; ++i) {  // forward + push-front: the tail ends up first in line
+      Block& blk = blocks_[t[i]];
       if (--blk.ref == 0) {
-        if (blk.hash) lru_push_back(*r);
-        else free_.push_back(*r);
+        if (blk.hash) lru_push_front(t[i]);
+        else free_.push_back(t[i]);
+      }
+    }
+    for (int i = keep - 1; i >= 0; --i) {  // tail first: later blocks evict first
+      Block& blk = blocks_[t[i]];
+      if (--blk.ref == 0) {
+        if (blk.hash) lru_push_back(t[i]);
+        else free_.push_back(t[i]);
       }
     }
     seqs_.erase(it);
@@ -232,6 +245,17 @@ class BlockAllocator {
     if (lru_tail_ >= 0) blocks_[lru_tail_].lru_next = b;
     else lru_head_ = b;
     lru_tail_ = b;
+    blk.in_lru = true;
+    ++lru_size_;
+  }
+
+  void lru_push_front(int b) {
+    Block& blk = blocks_[b];
+    blk.lru_prev = -1;
+    blk.lru_next = lru_head_;
+    if (lru_head_ >= 0) blocks_[lru_head_].lru_prev = b;
+    else lru_tail_ = b;
+    lru_head_ = b;
     blk.in_lru = true;
     ++lru_size_;
   }

@@ -22,7 +22,7 @@ PYBIND11_MODULE(_penny_runtime, m) {
       .def("commit", &BlockAllocator::commit)
       .def("num_committed", &BlockAllocator::num_committed)
       .def("table", &BlockAllocator::table)
-      .def("free", &BlockAllocator::free)
+      .def("free", &BlockAllocator::free, py::arg("seq"), py::arg("keep_blocks") = -1)
       .def("usage", &BlockAllocator::usage)
       .def("check_invariants", &BlockAllocator::check_invariants)
       .def_property_readonly("hits", &BlockAllocator::hits)

@@ -12,6 +12,10 @@ Decide outputs follow the tool-call grammar (``agent.grammar``): tokens the gram
 JSON skeleton, the tool name, unambiguous keys, the closing braces) are appended without
 sampling and computed as one chunk (jump-forward decoding) -- for scripted and sampled outputs
 alike; ``jump_forward=False`` decodes them one step each.
+
+``ephemeral_kv`` (agent hint): the prompt carries this turn's tool results, which the next turn
+will not repeat, so its freshly computed KV blocks are recycled before any other cached prefix
+(``PyBlockManager.free``) -- the conversation prefixes that DO recur survive in HBM.
 """
 from __future__ import annotations
 
@@ -79,7 +83,7 @@ class EngineLLM(LLMBackend):
             if grammar is not None:
                 jump = jump_mask(forced, self.tok.decode, grammar, self.eot)
         params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced,
-                                forced_jump=jump, grammar=grammar)
+                                forced_jump=jump, grammar=grammar, ephemeral_kv=bool(kw.get("ephemeral_kv")))
         out = await self.engine.generate_all(ids, params)
         self._account(kw.get("purpose", "decide"), len(ids), out.seq)
         text = self.tok.decode(out.seq.output_ids)
@@ -89,7 +93,8 @@ class EngineLLM(LLMBackend):
     async def astream(self, messages, temperature=0.5, max_tokens=512, **kw) -> AsyncIterator[str]:
         n = self.respond_tokens or max_tokens
         ids = self._encode(messages, None, n)
-        params = SamplingParams(temperature=temperature, max_tokens=n, ignore_eos=self.respond_ignore_eos)
+        params = SamplingParams(temperature=temperature, max_tokens=n, ignore_eos=self.respond_ignore_eos,
+                                ephemeral_kv=bool(kw.get("ephemeral_kv")))
         detok = IncrementalDetokenizer(self.tok)
         buf, k = [], 0
         async for o in self.engine.generate(ids, params):

@@ -123,8 +123,23 @@ class PyBlockManager:
             hashes.append(h)
             parent = h
 
-    def free(self, seq: Sequence) -> None:
-        for b in reversed(seq.block_table):
+    def free(self, seq: Sequence, evict_first: bool = False) -> None:
+        """Release ``seq``'s blocks.  ``evict_first``: the blocks it computed itself (everything
+        after its prefix-cache hit) are KV nobody will ask for again -- a prompt built around a
+        one-off retrieval context -- so they go to the FRONT of the eviction order (tail first)
+        instead of pushing still-useful prefixes out (an LRU over a cyclic working set slightly
+        larger than HBM would otherwise evict exactly what the next turn needs)."""
+        table = seq.block_table
+        keep = min(seq.num_cached_prompt // self.block_size, len(table)) if evict_first else len(table)
+        for b in table[keep:]:
+            self.ref[b] -= 1
+            if self.ref[b] == 0:
+                if self.hash_of[b] is not None:
+                    self.evictable[b] = None
+                    self.evictable.move_to_end(b, last=False)
+                else:
+                    self.free_list.append(b)
+        for b in reversed(table[:keep]):
             self.ref[b] -= 1
             if self.ref[b] == 0:
                 if self.hash_of[b] is not None:

@@ -68,6 +68,7 @@ class NativeBlockManager:
         if full > done:
             self.core.commit(seq.seq_id, done, seq.all_ids[done * bs:full * bs])
 
-    def free(self, seq: Sequence) -> None:
-        self.core.free(seq.seq_id)
+    def free(self, seq: Sequence, evict_first: bool = False) -> None:
+        keep = seq.num_cached_prompt // self.block_size if evict_first else -1
+        self.core.free(seq.seq_id, keep)
         seq.block_table = []

@@ -175,4 +175,4 @@ class Scheduler:
             self.running.remove(seq)
         elif seq in self.waiting:          # preempted while its last token was in flight
             self.waiting.remove(seq)
-        self.bm.free(seq)
+        self.bm.free(seq, evict_first=seq.params.ephemeral_kv)

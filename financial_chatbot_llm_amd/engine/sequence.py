@@ -23,6 +23,9 @@ class SamplingParams:
     # sampled; grammar -- the same oracle for sampled outputs (``forced(text) -> (str, ends)``)
     forced_jump: Optional[List[bool]] = None
     grammar: Optional[object] = None
+    # KV retention hint: the prompt's uncached part will not recur (e.g. the respond prompt around
+    # a one-off retrieval context), so its blocks are recycled before any other cached block
+    ephemeral_kv: bool = False
 
 
 class SeqStatus(enum.Enum):

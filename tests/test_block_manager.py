@@ -48,6 +48,32 @@ def test_exhaustion_and_eviction(impl):
     assert bm.match_prefix(d) == 128     # head blocks of `a` survived eviction
 
 
+@pytest.mark.parametrize("impl", [PyBlockManager, NativeBlockManager])
+def test_ephemeral_blocks_are_evicted_first(impl):
+    """A sequence freed with ``evict_first`` (its uncached KV will not recur: a prompt around a
+    one-off retrieval context) gives up its own blocks before older, still-useful prefixes; the
+    blocks it got from the prefix cache keep their LRU place."""
+    bm = impl(8, BS, True)
+    keep = mk(list(range(256)), "keep")                       # 4 blocks, freed first (older)
+    assert bm.grow(keep, 256)
+    keep.num_computed = 256
+    bm.commit(keep)
+    bm.free(keep)
+    eph = mk(list(range(128)) + list(range(5000, 5192)), "eph")  # 2 hit blocks + 3 own blocks
+    assert bm.match_prefix(eph) == 128
+    assert bm.grow(eph, 320)
+    eph.num_computed = 320
+    bm.commit(eph)
+    bm.free(eph, evict_first=True)
+    new = mk(list(range(9000, 9192)), "new")                  # needs 3: 1 free + 2 evicted
+    assert bm.grow(new, 192)
+    again = mk(list(range(256)) + [1], "again")
+    assert bm.match_prefix(again) == 256                      # the older prefix survived whole
+    bm.free(again)
+    probe = mk(list(range(128)) + list(range(5000, 5192)) + [1], "probe")
+    assert bm.match_prefix(probe) == 192                      # eph's tail went first: 1 own block left
+
+
 def test_native_matches_python_on_random_workload():
     rnd = random.Random(0)
     py, nat = PyBlockManager(40, BS, True), NativeBlockManager(40, BS, True)
@@ -83,8 +109,9 @@ def test_native_matches_python_on_random_workload():
                 nat.commit(s2)
         else:
             s1, s2 = live.pop(rnd.randrange(len(live)))
-            py.free(s1)
-            nat.free(s2)
+            eph = rnd.random() < 0.5
+            py.free(s1, evict_first=eph)
+            nat.free(s2, evict_first=eph)
         assert py.num_free() == nat.num_free()
         assert nat.core.check_invariants() == ""
     assert py.hits == nat.hits and py.queries == nat.queries
