@@ -112,7 +112,10 @@ class EngineConfig:
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
     kv_block_size: int = 64                 # tokens per KV block (one MFMA KV tile)
-    kv_mem_fraction: float = 0.80           # of free HBM after weights (288 GB per MI355X)
+    # of (free HBM after weights - 6 GiB); 0.92 leaves ~20 GiB of the 288 GiB unused at the end of
+    # the 20/5 bench (engine stats hbm_used_gib: 8B 264.5, Mixtral fp8 267.9; 0.95 measured no
+    # faster: profiles/r2_bench_kv_fraction.txt)
+    kv_mem_fraction: float = 0.92
     num_kv_blocks: Optional[int] = None     # explicit override (tests)
     max_num_seqs: int = 256                 # running-batch cap
     max_num_batched_tokens: int = 4096      # per-step token budget (chunked prefill; measured best: profiles/r1_sweep_max_batched_tokens.txt)

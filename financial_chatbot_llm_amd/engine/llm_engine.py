@@ -360,4 +360,16 @@ class LLMEngine:
                 "gpu_eager_ms_mean": round(1e3 * self.runner.stats["gpu_eager_s"]
                                            / max(1, self.runner.stats["steps"] - self.runner.stats["graph_steps"]), 3),
                 "gpu_idle_between_steps_s": round(self.runner.stats["gpu_idle_s"], 3),
-                "gpu_idle_gaps": self.runner.stats["gpu_idle_gaps"]}
+                "gpu_idle_gaps": self.runner.stats["gpu_idle_gaps"], **self._memory_stats()}
+
+    def _memory_stats(self) -> Dict[str, float]:
+        """HBM in use on the device (all allocators) and the caching allocator's peak: the
+        headroom ``kv_mem_fraction`` leaves is checked against these, not assumed."""
+        if self.device.type != "cuda":
+            return {}
+        free, total = torch.cuda.mem_get_info(self.device)
+        g = float(1 << 30)
+        return {"hbm_used_gib": round((total - free) / g, 1), "hbm_total_gib": round(total / g, 1),
+                "torch_peak_reserved_gib": round(torch.cuda.max_memory_reserved(self.device) / g, 1),
+                "kv_pool_gib": round(self.bm.num_blocks * KVCache.bytes_per_block(
+                    self.model.cfg.num_layers, self.model.hkv, self.model.D) / g, 1)}
