@@ -30,7 +30,7 @@ Under TP the experts are parallelised one of two ways (``moe_parallel``):
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
@@ -117,19 +117,31 @@ class MixtralModel(DecoderModel):
                                                 f_local, self.device)
         return self._moe_ws
 
-    def _expert_fp8(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
-        """One expert on its routed rows with fp8 x fp8 hipBLASLt GEMMs (prefill-size buckets)."""
+    def _expert_fp8(self, p: str, rows: torch.Tensor, e: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One expert on its routed rows with fp8 x fp8 hipBLASLt GEMMs (prefill-size buckets).
+        ``out``: the expert's slice of the sorted-row output, written by the down GEMM directly
+        (no copy kernel per expert and layer)."""
         xq, xs = moe_ops.quant_rows_fp8(rows)
         y13 = torch._scaled_mm(xq, self.w[p + "w13_q"][e].t(), scale_a=xs[:, None],
                                scale_b=self.w[p + "w13_scale"][e][None, :], out_dtype=self.dtype)
         aq, as_ = moe_ops.silu_quant_rows_fp8(y13)
+        if out is not None:
+            return torch._scaled_mm(aq, self.w[p + "w2_q"][e].t(), scale_a=as_[:, None],
+                                    scale_b=self.w[p + "w2_scale"][e][None, :], out_dtype=self.dtype, out=out)
         return torch._scaled_mm(aq, self.w[p + "w2_q"][e].t(), scale_a=as_[:, None],
                                 scale_b=self.w[p + "w2_scale"][e][None, :], out_dtype=self.dtype)
 
-    def _expert(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
-        """One (local) expert on its routed rows (eager path)."""
+    def _expert(self, p: str, rows: torch.Tensor, e: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One (local) expert on its routed rows (eager path); the result lands in ``out`` if given."""
         if self.fp8 and self.prefill_fp8 and (p + "w13_q") in self.w:
-            return self._expert_fp8(p, rows, e)
+            return self._expert_fp8(p, rows, e, out)
+        y = self._expert_bf16(p, rows, e)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def _expert_bf16(self, p: str, rows: torch.Tensor, e: int) -> torch.Tensor:
         if self.fp8:
             act = ops.silu_mul(F.linear(rows, self._dequant(p, "w13", e)), interleave16=True)
             return F.linear(act, self._dequant(p, "w2", e))
@@ -166,7 +178,7 @@ class MixtralModel(DecoderModel):
         for e in range(c.num_experts):
             a, b = offs[e], offs[e + 1]
             if b > a:
-                ys[a:b] = self._expert(p, xs[a:b], e)
+                self._expert(p, xs[a:b], e, out=ys[a:b])
         # every sorted row is written above (the buckets tile [0, T*k)); weighted gather-combine
         out = moe_ops.combine_weighted(ys, order, tok_w, T, c.top_k_experts)
         return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
