@@ -103,7 +103,8 @@ async def run(args, ps):
                         max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
                         graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype,
                         # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
-                        kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)))
+                        kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
+                        sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)))
     if args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
         from financial_chatbot_llm_amd.engine.process_engine import ProcessAsyncEngine
         engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device() if on_gpu else None)

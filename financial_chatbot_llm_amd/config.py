@@ -121,6 +121,7 @@ class EngineConfig:
     max_num_batched_tokens: int = 4096      # per-step token budget (chunked prefill; measured best: profiles/r1_sweep_max_batched_tokens.txt)
     max_model_len: int = 8192
     step_token_quantum: int = 256           # step rows rounded down to a multiple (prefill GEMM M)
+    sched_aging_s: float = 1.0              # a waiting long-output request joins the priority class after this
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
     # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
@@ -146,6 +147,7 @@ class EngineConfig:
             max_num_batched_tokens=_env_int("PENNY_MAX_BATCHED_TOKENS", cls.max_num_batched_tokens),
             max_model_len=_env_int("PENNY_MAX_MODEL_LEN", cls.max_model_len),
             step_token_quantum=_env_int("PENNY_STEP_TOKEN_QUANTUM", cls.step_token_quantum),
+            sched_aging_s=_env_float("PENNY_SCHED_AGING_S", cls.sched_aging_s),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),

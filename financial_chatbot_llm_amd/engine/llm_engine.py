@@ -71,7 +71,8 @@ class LLMEngine:
                           dtype=getattr(self.model, "dtype", torch.bfloat16), device=device)
         self.bm = make_block_manager(nblocks, KV_BS, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
-                                   token_quantum=cfg.step_token_quantum if device.type == "cuda" else 0)
+                                   token_quantum=cfg.step_token_quantum if device.type == "cuda" else 0,
+                                   aging_s=cfg.sched_aging_s)
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)
