@@ -266,12 +266,22 @@ def bench_gemm_prefill(dev) -> List[Dict]:
 
 def bench_lm_head(dev) -> List[Dict]:
     """LM head (vocab 128256) at the sampler counts of real steps: weight-streaming bound."""
+    from ..ops import gemm
+    gemm.load_gemm_tuning("llama3-8b")   # the library baseline runs the curated solutions, as in serving
     out = []
-    w = torch.randn((128256, 4096), device=dev).to(torch.bfloat16) * 0.02
-    for M in (1, 16, 48, 64, 96, 128, 160, 192, 256):
-        x = torch.randn((M, 4096), device=dev).to(torch.bfloat16)
+    V, K = 128256, 4096
+    w = torch.randn((V, K), device=dev).to(torch.bfloat16) * 0.02
+    for M in (1, 16, 37, 48, 64, 96, 100, 128, 160, 192, 217, 256):
+        x = torch.randn((M, K), device=dev).to(torch.bfloat16)
         us = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
-        out.append({"op": "lm_head", "M": M, "us": round(us, 1), "TBps": round(w.numel() * 2 / us / 1e6, 2)})
+        row = {"op": "lm_head", "M": M, "hipblaslt_us": round(us, 1), "hipblaslt_TBps": round(V * K * 2 / us / 1e6, 2)}
+        ref = torch.nn.functional.linear(x.float(), w.float())
+        P = torch.empty((1, M, V), dtype=torch.float32, device=dev)
+        for nf in (2, 4, 8):
+            t = timeit(lambda: gemm.splitk_partials(x, w, V, 1, nf, out=P, rowmajor=True), iters=10)
+            row[f"splitk_nf{nf}_us"] = round(t, 1)
+            row[f"splitk_nf{nf}_err"] = float((P[0] - ref).abs().max())
+        out.append(row)
     return out
 
 

@@ -10,6 +10,7 @@ import socket
 
 import pytest
 import torch
+from mp_util import to_np, to_torch
 import torch.multiprocessing as mp
 
 from financial_chatbot_llm_amd.parallel import context as cpx
@@ -69,7 +70,7 @@ def _worker(rank, world, port, q_out):
             q, k, v = _inputs(T=12 * world)
             shard = lambda t: cpx.zigzag_shard(t, world, rank)  # noqa: E731
             res[causal] = cpx.ring_attention(shard(q), shard(k), shard(v), q.shape[0], causal=causal)
-        q_out.put((rank, res))
+        q_out.put((rank, to_np(res)))
         dist.barrier()
         shutdown()
     except Exception:  # noqa: BLE001
@@ -86,7 +87,7 @@ def test_ring_attention_matches_single_process(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q_out)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q_out.get(timeout=200) for _ in range(world))
+    res = {r: to_torch(v) for r, v in (q_out.get(timeout=200) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
     for r in range(world):

@@ -9,6 +9,7 @@ import socket
 
 import pytest
 import torch
+from mp_util import to_np, to_torch
 import torch.multiprocessing as mp
 
 
@@ -63,7 +64,7 @@ def _worker(rank, world, port, q):
         logits = _prefill_logits(m, ids)
         m.quantize_experts()
         logits_fp8 = _prefill_logits(m, ids)
-        q.put((rank, raw, logits, logits_fp8, m.w["layers.0.w13_t"].shape[0]))
+        q.put((rank, to_np(raw), to_np(logits), to_np(logits_fp8), m.w["layers.0.w13_t"].shape[0]))
         dist.barrier()
         shutdown()
     except Exception:  # noqa: BLE001
@@ -86,7 +87,7 @@ def test_expert_parallel_all_to_all_matches_single_process():
     res = {}
     for _ in range(2):
         item = q.get(timeout=240)
-        res[item[0]] = item[1:]
+        res[item[0]] = to_torch(item[1:])
     for p in procs:
         p.join(timeout=60)
     for r, v in res.items():

@@ -10,6 +10,7 @@ import socket
 
 import pytest
 import torch
+from mp_util import to_np, to_torch
 import torch.multiprocessing as mp
 
 from financial_chatbot_llm_amd.config import EngineConfig
@@ -54,7 +55,7 @@ def _worker(rank, world, port, q):
             assert eng.runner.stats["overlap_steps"] >= 2, eng.runner.stats
         else:
             eng.follower_loop()
-        q.put((rank, logits_tp, out))
+        q.put((rank, to_np(logits_tp), out))
         shutdown()
     except Exception as e:  # noqa: BLE001
         import traceback
@@ -78,7 +79,7 @@ def test_tp_matches_tp1(world):
     res = {}
     for _ in range(world):
         r, a, b = q.get(timeout=240)
-        res[r] = (a, b)
+        res[r] = (to_torch(a), b)
     for p in procs:
         p.join(timeout=60)
     for r in res:
