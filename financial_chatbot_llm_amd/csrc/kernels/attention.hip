@@ -44,6 +44,23 @@ union Frag {
 // below f32 resolution of the running max term), so the flush is harmless.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Reductions over the 4 lanes {l, l^16, l^32, l^48} (the 4 row groups of a 16x16 MFMA tile) on
+// the gfx950 VALU lane swaps.  permlane16_swap(v, v) leaves rows (0,0,2,2) in one result and
+// (1,1,3,3) in the other, so combining the two is the xor-16 step; permlane32_swap the xor-32
+// one.  __shfl_xor compiles to ds_bpermute: an LDS round trip on the softmax's critical path.
+__device__ __forceinline__ float rowgroup_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rowgroup_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -72,13 +89,18 @@ struct CascadeArgs {
 // base-2 online softmax in registers, O^T += V^T.P^T with P straight from the S^T registers.
 // kl / vl: the block's K and V tiles in LDS (fragment-native).  `full`: no key of the block needs
 // masking (all < ctx and, if causal, <= every row's position).
-// MASK is a template parameter so the hot (unmasked) path is straight-line code: a per-element
-// `full || (...)` short-circuit compiles to 32 divergent branches per block on gfx950.
-template <int D, bool MASK>
+// The masking is one wave-uniform branch around a select loop: a per-element `full || (...)`
+// short-circuit compiles to 32 divergent branches per block on gfx950.
+// MASK: 0 never, 1 always, 2 when the wave-uniform runtime flag `need_mask` is set.  Mode 2 keeps
+// ONE copy of the MFMA code in the loop: with two inlined copies (one per mode, behind an if/else)
+// the accumulators meet at a join point and hipcc materialises the merge as v_mov_b64 copies of
+// MFMA results (each one waits for its MFMA to retire), ~64 per block.
+template <int D, int MASK>
 __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
                                              const Frag (&qf)[2][D / 32], f32x4 (&o)[2][D / 16], float (&m)[2],
                                              float (&l)[2], bool causal, int j, int ctx,
-                                             const int (&qpos)[2], float scale_log2, int lane, int g) {
+                                             const int (&qpos)[2], float scale_log2, int lane, int g,
+                                             bool need_mask = false) {
   constexpr int KC = D / 32;
   constexpr int DT = D / 16;
   // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
@@ -98,25 +120,27 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
 
   // ---- online softmax (base-2) -------------------------------------------------------
   Frag pf[2][2];
+  if (MASK == 1 || (MASK == 2 && need_mask)) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = j * KV_BS + 16 * t + 4 * g + r;
+          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));   // non-short-circuit: selects
+          sc[ct][t][r] = ok ? sc[ct][t][r] : -INFINITY;
+        }
+  }
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     float mt = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = j * KV_BS + 16 * t + 4 * g + r;
-        float v = sc[ct][t][r];
-        if constexpr (MASK) {
-          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));   // non-short-circuit: selects
-          v = ok ? v : -INFINITY;
-        }
-        sc[ct][t][r] = v;
-        mt = fmaxf(mt, v);
-      }
+      for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[ct][t][r]);
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = rowgroup_max(mt);
     mt *= scale_log2;   // max of the scaled scores (scale > 0) -- the 32 scores stay unscaled
     // Deferred rescale: the running max m only moves when a block raises it by more than 8
     // (log2 domain), so p <= 2^8 in between -- harmless for f32 l/O and bf16 P -- and the 64
@@ -252,8 +276,8 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
     const uint4* vl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE + TILE);
 
     const bool full = CASCADE || ((j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0));
-    if (full) attend_block<D, false>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
-    else attend_block<D, true>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
+    attend_block<D, 2>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
+                       __builtin_amdgcn_readfirstlane((int)!full) != 0);
     __syncthreads();  // block j+1 landed (vmcnt drained) and everyone is done with buffer `buf`
   }
 
@@ -261,8 +285,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     float lt = l[ct];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = rowgroup_sum(lt);
     if (tok[ct] >= qlen) continue;
     if constexpr (CASCADE) {
       const long pi = ((long)ca.members[q0 + tok[ct]] * Hq + head[ct]) * ca.part_stride + ca.slot0 + chunk;
@@ -389,8 +412,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
         mt = fmaxf(mt, v);
       }
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = rowgroup_max(mt);
     const float mn = fmaxf(m, mt);
     const float alpha = fast_exp2(m - mn);
     float ls = 0.f;
@@ -415,8 +437,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
   }
 
   // merge the 4 waves through LDS
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = rowgroup_sum(l);
   if (g == 0) {
     s_m[w][col] = m;
     s_l[w][col] = l;
@@ -599,15 +620,14 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
     const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    if (full) attend_block<D, false>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
-    else attend_block<D, true>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g);
+    attend_block<D, 2>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
+                       __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     float lt = l[ct];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = rowgroup_sum(lt);
     if (tok[ct] >= qlen) continue;
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
