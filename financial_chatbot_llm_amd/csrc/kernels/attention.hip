@@ -382,8 +382,18 @@ __global__ void __launch_bounds__(256) decode_kernel(
   for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-  for (int j = blk0 + w; j < blk1; j += 4) {
-    const long phys = bt[j];
+  // This wave's block ids are fetched up front, one per lane (64 iterations per fetch), and read
+  // back with v_readlane: a load of bt[j] at the top of every iteration put a dependent
+  // global-memory round trip in front of each block's K/V loads.
+  const int nit = blk1 - blk0 - w > 0 ? (blk1 - blk0 - w + 3) / 4 : 0;
+  int ids = 0;
+  for (int it = 0; it < nit; ++it) {
+    if ((it & 63) == 0) {
+      const int jl = blk0 + w + 4 * (it + lane);
+      ids = jl < blk1 ? bt[jl] : 0;
+    }
+    const int j = blk0 + w + 4 * it;
+    const long phys = __builtin_amdgcn_readlane(ids, it & 63);
     PENNY_DASSERT(phys >= 0);
     const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
@@ -413,24 +423,32 @@ __global__ void __launch_bounds__(256) decode_kernel(
       }
     }
     mt = rowgroup_max(mt);
-    const float mn = fmaxf(m, mt);
-    const float alpha = fast_exp2(m - mn);
+    // deferred rescale as in prefill: m moves only when a block raises it by more than 8 (log2),
+    // so the 32 accumulator multiplies (AGPR read-modify-write) run on the rare growing blocks
+    const bool grow = mt > m + 8.f;
+    if (__any(grow)) {
+      const float mn = grow ? mt : m;
+      const float alpha = grow ? fast_exp2(m - mn) : 1.f;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      m = mn;
+    }
+    const float mref = (m == -INFINITY) ? 0.f : m;
     float ls = 0.f;
     Frag pf[2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = fast_exp2(sc[t][r] - mn);
+        const float pv = fast_exp2(sc[t][r] - mref);
         ls += pv;
         pf[t >> 1].v[4 * (t & 1) + r] = (bf16)pv;
       }
     }
-    l = l * alpha + ls;
-    m = mn;
+    l += ls;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      o[dt] *= alpha;
       o[dt] = mfma16(vf[dt][0].v, pf[0].v, o[dt]);
       o[dt] = mfma16(vf[dt][1].v, pf[1].v, o[dt]);
     }
