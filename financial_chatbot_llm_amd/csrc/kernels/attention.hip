@@ -95,7 +95,7 @@ struct CascadeArgs {
 // ONE copy of the MFMA code in the loop: with two inlined copies (one per mode, behind an if/else)
 // the accumulators meet at a join point and hipcc materialises the merge as v_mov_b64 copies of
 // MFMA results (each one waits for its MFMA to retire), ~64 per block.
-template <int D, int MASK>
+template <int D, int MASK, bool PREF = false>
 __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
                                              const Frag (&qf)[2][D / 32], f32x4 (&o)[2][D / 16], float (&m)[2],
                                              float (&l)[2], bool causal, int j, int ctx,
@@ -105,6 +105,11 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
   constexpr int DT = D / 16;
   // ---- S^T = K . Q^T for 64 keys x 32 query rows -------------------------------------
   f32x4 sc[2][4];
+  Frag kfa[PREF ? 4 * KC : 1], vfa[PREF ? 2 * DT : 1];
+  if constexpr (PREF) {
+#pragma unroll
+    for (int f = 0; f < 4 * KC; ++f) kfa[f].u = kl[f * 64 + lane];
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -112,10 +117,19 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       Frag kf;
-      kf.u = kl[(t * KC + c) * 64 + lane];
+      if constexpr (PREF) kf = kfa[t * KC + c];
+      else kf.u = kl[(t * KC + c) * 64 + lane];
       sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
       sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
     }
+  }
+  // PREF (the 8-wave kernel, 1 workgroup per CU: registers to spare): all 16 K fragments of the
+  // block are read before the QK^T MFMAs and all 16 V fragments right after them, so the V reads
+  // are in flight during the softmax instead of exposed in front of each P.V pair (+2-5 %,
+  // profiles/r2_prefill_attn_kv_prefetch_ab.jsonl)
+  if constexpr (PREF) {   // V fragments in flight while the softmax runs
+#pragma unroll
+    for (int f = 0; f < 2 * DT; ++f) vfa[f].u = vl[f * 64 + lane];
   }
 
   // ---- online softmax (base-2) -------------------------------------------------------
@@ -182,7 +196,8 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       Frag vf;
-      vf.u = vl[(dt * 2 + st) * 64 + lane];
+      if constexpr (PREF) vf = vfa[dt * 2 + st];
+      else vf.u = vl[(dt * 2 + st) * 64 + lane];
       o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
       o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
     }
@@ -536,7 +551,7 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int D, int NW, int NBUF, bool HEAD_FAST>
+template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -638,8 +653,8 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
     const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    attend_block<D, 2>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
-                       __builtin_amdgcn_readfirstlane((int)!full) != 0);
+    attend_block<D, 2, PREF>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
+                             __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
 #pragma unroll
