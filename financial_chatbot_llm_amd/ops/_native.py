@@ -54,7 +54,10 @@ _SIGS = {
 
 
 def lib_path() -> str:
-    """The production kernel library, or its bounds-checked debug build with PENNY_KERNEL_DEBUG=1."""
+    """The production kernel library, or its bounds-checked debug build with PENNY_KERNEL_DEBUG=1.
+    ``PENNY_KERNEL_LIB`` names another build of the same library (whole-library A/B runs)."""
+    if os.environ.get("PENNY_KERNEL_LIB"):
+        return os.environ["PENNY_KERNEL_LIB"]
     from .._build import kernel_lib
     return kernel_lib(os.environ.get("PENNY_KERNEL_DEBUG") == "1")
 
