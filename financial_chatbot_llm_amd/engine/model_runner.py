@@ -232,14 +232,62 @@ class ModelRunner:
         self._pinned_out = ([torch.zeros(self.max_samplers, dtype=torch.int32).pin_memory() for _ in range(2)]
                             if self.on_gpu else None)
         self._out_flip = 0
+        # eager-step inputs: one pinned staging ring slot -> ONE H2D copy per step (see _stage_inputs)
+        self._staged: Optional[Dict[int, torch.Tensor]] = None
+        self._stage_ring: List[Optional[torch.Tensor]] = [None] * 4
+        self._stage_events: List[Optional[torch.cuda.Event]] = [None] * 4
+        self._stage_flip = 0
+        self._stage_enabled = os.environ.get("PENNY_STAGE_INPUTS", "1") == "1"
 
     # ------------------------------------------------------------------------------------
     # eager path
     # ------------------------------------------------------------------------------------
+    _STAGE_DTYPES = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
+                     np.dtype(np.float32): torch.float32}
+
+    def _stage_inputs(self, si: StepInputs) -> None:
+        """Upload every array of an eager step with ONE H2D copy: the arrays are packed (16-B
+        aligned) into a pinned staging slot, copied as one byte buffer and handed out as typed
+        device views by ``_to_dev``.  One copy per array meant ~12 blit kernels and pinned
+        allocations per step on the compute stream."""
+        self._staged = None
+        if not self.on_gpu or not self._stage_enabled:
+            return
+        arrs = []
+        total = 0
+        for name in StepInputs._ARRAYS:
+            a = getattr(si, name)
+            if a is None or a.dtype not in self._STAGE_DTYPES:
+                continue
+            arrs.append((a, np.ascontiguousarray(a), total))
+            total += (a.nbytes + 15) // 16 * 16
+        if total == 0:
+            return
+        k = self._stage_flip
+        self._stage_flip = (k + 1) % len(self._stage_ring)
+        if self._stage_events[k] is not None:
+            self._stage_events[k].synchronize()     # the copy that last read this slot is done
+        buf = self._stage_ring[k]
+        if buf is None or buf.numel() < total:
+            buf = torch.empty(max(total, 1 << 20), dtype=torch.uint8).pin_memory()
+            self._stage_ring[k] = buf
+        host = buf.numpy()
+        for _, c, off in arrs:
+            host[off:off + c.nbytes] = c.reshape(-1).view(np.uint8)
+        dev = torch.empty(total, dtype=torch.uint8, device=self.device)
+        dev.copy_(buf[:total], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._stage_events[k] = ev
+        self._staged = {id(a): dev[off:off + c.nbytes].view(self._STAGE_DTYPES[c.dtype]).view(c.shape)
+                        for a, c, off in arrs}
+
     def _to_dev(self, a: np.ndarray, dtype=None) -> torch.Tensor:
-        t = torch.from_numpy(np.ascontiguousarray(a))
-        if self.on_gpu:
-            t = t.pin_memory().to(self.device, non_blocking=True)
+        t = self._staged.get(id(a)) if self._staged is not None else None
+        if t is None:
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if self.on_gpu:
+                t = t.pin_memory().to(self.device, non_blocking=True)
         return t if dtype is None else t.to(dtype)
 
     def _meta(self, si: StepInputs, slots: torch.Tensor) -> AttentionMetadata:
@@ -345,7 +393,11 @@ class ModelRunner:
             self.stats["prefill_steps"] += 1
             self.stats["prefill_step_tokens"] += len(si.ids)
         if len(si.logits_idx) == 0:
-            self._forward_only(si)
+            self._stage_inputs(si)
+            try:
+                self._forward_only(si)
+            finally:
+                self._staged = None
             return PendingStep(None, 0, None, None)
         start_ev = None
         if self._gpu_timing:
@@ -358,7 +410,11 @@ class ModelRunner:
             graph = True
         else:
             with marker(f"forward.eager[{len(si.ids)}]"):
-                out = self.sample(self.forward_logits(si), si)
+                self._stage_inputs(si)
+                try:
+                    out = self.sample(self.forward_logits(si), si)
+                finally:
+                    self._staged = None
         n = len(si.logits_idx)
         self.last_sampled[:n].copy_(out[:n].to(torch.int32), non_blocking=True)
         if not self.on_gpu:
