@@ -210,15 +210,15 @@ __global__ void __launch_bounds__(NW * 64) moe_gemm_kernel(
 #pragma unroll
       for (int m = 0; m < 4; ++m) xv[m] = *reinterpret_cast<const uint4*>(xr[m] + k);
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      // both k-halves of one accumulator back to back (a dependent MFMA pair): interleaving the
+      // halves across all NTF*4 accumulators made hipcc shuffle them between AGPRs every pair
+      for (int f = 0; f < NTF; ++f) {
+        const long a0 = ((long)wv[f].y << 32 | wv[f].x), a1 = ((long)wv[f].w << 32 | wv[f].z);
 #pragma unroll
-        for (int f = 0; f < NTF; ++f) {
-          const long a = half ? ((long)wv[f].w << 32 | wv[f].z) : ((long)wv[f].y << 32 | wv[f].x);
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const long b = half ? ((long)xv[m].w << 32 | xv[m].z) : ((long)xv[m].y << 32 | xv[m].x);
-            acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, acc[f][m], 0, 0, 0);
-          }
+        for (int m = 0; m < 4; ++m) {
+          const long b0 = ((long)xv[m].y << 32 | xv[m].x), b1 = ((long)xv[m].w << 32 | xv[m].z);
+          acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0, b0, acc[f][m], 0, 0, 0);
+          acc[f][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1, b1, acc[f][m], 0, 0, 0);
         }
       }
     }
