@@ -202,13 +202,24 @@ __global__ void __launch_bounds__(NW * 64) moe_gemm_kernel(
       const int src = rows ? rows[pr] : pr;
       xr[m] = Xq + (long)src * K + kb + 16 * g;
     }
+    // one k-pair of W (NTF fragments) and X (4 token tiles) in flight ahead of the MFMAs using
+    // the previous one (register double buffer)
+    uint4 wn[NTF], xn[4];
+    auto fetch = [&](int k) {
+#pragma unroll
+      for (int f = 0; f < NTF; ++f)
+        wn[f] = *reinterpret_cast<const uint4*>(We + (((long)(n0 / 16 + f) * kpairs + (kb + k) / 64) * 64 + lane) * 16);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) xn[m] = *reinterpret_cast<const uint4*>(xr[m] + k);
+    };
+    fetch(0);
     for (int k = 0; k < kper; k += 64) {
       uint4 wv[NTF], xv[4];
 #pragma unroll
-      for (int f = 0; f < NTF; ++f)
-        wv[f] = *reinterpret_cast<const uint4*>(We + (((long)(n0 / 16 + f) * kpairs + (kb + k) / 64) * 64 + lane) * 16);
+      for (int f = 0; f < NTF; ++f) wv[f] = wn[f];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) xv[m] = *reinterpret_cast<const uint4*>(xr[m] + k);
+      for (int m = 0; m < 4; ++m) xv[m] = xn[m];
+      if (k + 64 < kper) fetch(k + 64);
 #pragma unroll
       // both k-halves of one accumulator back to back (a dependent MFMA pair): interleaving the
       // halves across all NTF*4 accumulators made hipcc shuffle them between AGPRs every pair
