@@ -226,3 +226,35 @@ def test_llama3_8b_engine_end_to_end():
                                                            forced_jump=jump_mask(forced, tok.decode, g, eot), grammar=g))
     assert out[0] == forced
     assert eng.runner.stats["steps"] - steps0 < len(forced) - 10     # grammar-forced runs were chunked
+
+
+def test_staged_step_inputs_match_arrays_and_plain_upload(monkeypatch):
+    """Eager steps upload every StepInputs array with ONE pinned H2D copy (typed views of one
+    device byte buffer); the views equal the host arrays, and an engine run with staging off
+    produces the same greedy tokens."""
+    import numpy as np
+    from financial_chatbot_llm_amd.engine.model_runner import StepInputs
+    base = dict(model="llama-tiny", device="cuda", num_kv_blocks=128, max_model_len=2048, max_num_seqs=8,
+                use_cuda_graph=False)
+    prompts = [list(range(50 + 5 * i, 50 + 5 * i + 40 + 13 * i)) for i in range(4)]
+    sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    e1 = LLMEngine(EngineConfig(**base))
+    staged = e1.generate(prompts, sp)
+    runner = e1.runner
+    i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
+    si = StepInputs(i32([5, 6, 7]), i32([0, 1, 2]), i32([64, 65, 66]), i32([0, 3]), i32([3]),
+                    i32([[1, 2, 3]]), 3, i32([]), np.zeros((0, 3), np.int32), np.asarray([2], np.int64),
+                    np.asarray([0.5], np.float32), np.asarray([12345678901], np.int64), i32([0]),
+                    np.asarray([1.0], np.float32), None)
+    runner._stage_inputs(si)
+    for name in ("ids", "positions", "slots", "cu_q", "ctx_p", "bt_p", "ctx_d", "bt_d", "logits_idx", "temps",
+                 "seeds", "top_k", "top_p"):
+        a = getattr(si, name)
+        t = runner._to_dev(a)
+        assert t.is_cuda and tuple(t.shape) == a.shape and t.dtype == torch.from_numpy(a).dtype, name
+        assert np.array_equal(t.cpu().numpy(), a), name
+    runner._staged = None
+    monkeypatch.setenv("PENNY_STAGE_INPUTS", "0")
+    e2 = LLMEngine(EngineConfig(**base), model=e1.model)
+    assert not e2.runner._stage_enabled
+    assert e2.generate(prompts, sp) == staged

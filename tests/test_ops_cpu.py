@@ -175,3 +175,14 @@ def test_rowmajor_and_tiled_decode_gemm_agree_on_cpu():
     y1 = gemm.gateup_silu(x, gemm.tile_weight(wi), 64, 4)
     y2 = gemm.gateup_silu(x, wi, 64, 4, rowmajor=True)
     assert torch.equal(y1, y2)
+
+
+def test_kernel_lib_override_path(monkeypatch):
+    """PENNY_KERNEL_LIB points the loader at another build of the kernel library (A/B runs)."""
+    from financial_chatbot_llm_amd.ops import _native
+    monkeypatch.delenv("PENNY_KERNEL_LIB", raising=False)
+    assert _native.lib_path().endswith("libpenny_kernels.so")
+    monkeypatch.setenv("PENNY_KERNEL_DEBUG", "1")
+    assert _native.lib_path().endswith("libpenny_kernels_debug.so")
+    monkeypatch.setenv("PENNY_KERNEL_LIB", "/tmp/other/libpenny_kernels_ab.so")
+    assert _native.lib_path() == "/tmp/other/libpenny_kernels_ab.so"
