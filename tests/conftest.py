@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# pyarrow's default (jemalloc) pool segfaulted intermittently in parquet reads inside pytest-xdist
+# workers that had run torch-heavy tests first; the system allocator avoids it (tests only)
+os.environ.setdefault("ARROW_DEFAULT_MEMORY_POOL", "system")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
