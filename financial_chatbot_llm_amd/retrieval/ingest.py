@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import datetime as _dt
 import json
+import os
 import time
 from typing import Any, Dict, Iterable, Iterator, List, Optional, Tuple
 
@@ -72,6 +73,9 @@ def iter_documents(path: str, batch_rows: int = 65536) -> Iterator[Dict[str, Any
             data = json.load(fh)
         yield from (data if isinstance(data, list) else data.get("documents", []))
     elif path.endswith(".parquet"):
+        # system allocator unless the deployment chose one: arrow's jemalloc pool segfaulted
+        # intermittently next to torch in test workers (only applies if pyarrow is not loaded yet)
+        os.environ.setdefault("ARROW_DEFAULT_MEMORY_POOL", "system")
         import pyarrow.parquet as pq
         f = pq.ParquetFile(path)
         for batch in f.iter_batches(batch_size=batch_rows):
