@@ -556,6 +556,206 @@ def bench_moe_prefill(dev) -> List[Dict]:
     return out
 
 
+def bench_gemm_hip(dev, Ms=None) -> List[Dict]:
+    """Hand-written prefill GEMM (gemm_prefill.hip) vs hipBLASLt on the Llama-3-8B projections at
+    the step sizes the scheduler emits, interleaved in one process on the same random operands.
+    gate|up is timed with its SiLU epilogue against hipBLASLt + silu_mul; QKV / O / down also at
+    split-K S = 2, 4 (f32 slabs, the form their RMSNorm / RoPE consumers read)."""
+    from ..ops import gemm
+    from ..ops.activation import silu_mul
+    out = []
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    ws = {n: (torch.rand((N, K), device=dev) * 2 - 1).to(torch.bfloat16) * 0.05 for n, (N, K) in shapes.items()}
+    Ms = Ms or [256 * k for k in range(1, 17)]
+    for M in Ms:
+        row = {"op": "gemm_hip", "M": M}
+        fl, t_lib, t_hip = 0.0, 0.0, 0.0
+        for name, (N, K) in shapes.items():
+            x = (torch.rand((M, K), device=dev) * 2 - 1).to(torch.bfloat16)
+            w = ws[name]
+            f = 2 * M * N * K
+            if name == "gate_up":
+                lib = timeit(lambda: silu_mul(torch.nn.functional.linear(x, w), interleave16=True), iters=10)
+                hip = timeit(lambda: gemm.prefill_gemm(x, w, "silu"), iters=10)
+                best = hip
+            else:
+                lib = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
+                hip = timeit(lambda: gemm.prefill_gemm(x, w), iters=10)
+                best = hip
+                for S in (2, 4):
+                    if K % (64 * S) == 0:
+                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                        t = timeit(lambda: gemm.prefill_gemm(x, w, "slabs", S, out=P), iters=10)
+                        row[f"{name}_S{S}_TF"] = round(f / t / 1e6, 1)
+                        best = min(best, t)
+            row[f"{name}_lib_TF"] = round(f / lib / 1e6, 1)
+            row[f"{name}_hip_TF"] = round(f / hip / 1e6, 1)
+            fl += f
+            t_lib += lib
+            t_hip += best
+        row["layer_lib_TF"] = round(fl / t_lib / 1e6, 1)
+        row["layer_hip_best_TF"] = round(fl / t_hip / 1e6, 1)
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
+def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
+    """Each Llama-3-8B projection WITH its consumer, as the decoder layer runs it at a prefill
+    step of M rows, under every available choice (microseconds; same random operands):
+      qkv:     hipBLASLt + rope_kv_write | fused QKV+RoPE+KV-write tile kernel
+      o, down: hipBLASLt + add&RMSNorm   | tile kernel bf16 + add&RMSNorm | split-K S slabs + slab RMSNorm
+      gate_up: hipBLASLt + silu_mul      | tile kernel with the SiLU epilogue
+    -> the table ops/gemm.py PREFILL_POLICY is written from."""
+    from ..ops import gemm
+    from ..ops.activation import silu_mul
+    from ..ops.attention import rope_cos_sin, rope_kv_write
+    out = []
+    H, F_, Hq, Hkv = 4096, 14336, 32, 8
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    w = {"qkv": rnd(6144, H), "o": rnd(H, H), "gate_up": rnd(2 * F_, H), "down": rnd(H, F_)}
+    nw = torch.ones(H, dtype=torch.bfloat16, device=dev)
+    cs = rope_cos_sin(128, 8192, 500000.0, device=dev)
+    Ms = Ms or [256 * k for k in range(1, 17)]
+    nb = 4096 // 64 + 4
+    kc = torch.zeros((nb, Hkv, 64 * 128), dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    for M in Ms:
+        row = {"op": "prefill_policy", "M": M}
+        x = rnd(M, H)
+        xf = rnd(M, F_)
+        res = rnd(M, H)
+        pos = torch.arange(M, dtype=torch.int32, device=dev)
+        slots = torch.arange(M, dtype=torch.int32, device=dev)
+        fns = {}
+        fns["qkv_lib"] = lambda: rope_kv_write(torch.nn.functional.linear(x, w["qkv"]), pos, cs, slots, kc, vc,
+                                               Hq, Hkv, 128)
+        fns["qkv_fused"] = lambda: gemm.prefill_qkv_rope(x, w["qkv"], pos, cs, slots, kc, vc, Hq, Hkv)
+        for name, a in (("o", x), ("down", xf)):
+            K = a.shape[1]
+            fns[f"{name}_lib"] = (lambda a=a, name=name: ops.rms_norm(torch.nn.functional.linear(a, w[name]), nw,
+                                                                       1e-5, residual=res))
+            fns[f"{name}_hip1"] = (lambda a=a, name=name: ops.rms_norm(gemm.prefill_gemm(a, w[name]), nw, 1e-5,
+                                                                        residual=res))
+            for S in (2, 4):
+                if K % (64 * S) == 0:
+                    P = torch.empty((S, M, H), dtype=torch.float32, device=dev)
+                    fns[f"{name}_hipS{S}"] = (lambda a=a, name=name, S=S, P=P: ops.rms_norm(
+                        gemm.Slabs(gemm.prefill_gemm(a, w[name], "slabs", S, out=P)), nw, 1e-5, residual=res))
+        fns["gate_up_lib"] = lambda: silu_mul(torch.nn.functional.linear(x, w["gate_up"]), interleave16=True)
+        fns["gate_up_hip1"] = lambda: gemm.prefill_gemm(x, w["gate_up"], "silu")
+        t = interleaved(fns, rounds=5, iters=5)
+        row.update({k: round(v, 1) for k, v in t.items()})
+        lib = sum(v for k, v in t.items() if k.endswith("_lib"))
+        best = {}
+        for p in ("qkv", "o", "gate_up", "down"):
+            k = min((k for k in t if k.rsplit("_", 1)[0] == p), key=lambda k: t[k])
+            best[p] = k.rsplit("_", 1)[1]
+        row["best"] = best
+        row["layer_lib_us"] = round(lib, 1)
+        row["layer_best_us"] = round(sum(t[f"{p}_{best[p]}"] for p in best), 1)
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
+def interleaved(fns: Dict[str, Callable[[], None]], rounds: int = 7, iters: int = 10) -> Dict[str, float]:
+    """Median microseconds per call of each variant, timed in interleaved rounds (A B C A B C ...)
+    so clock / thermal drift hits every variant alike (cdna_hip_programming.md §5.4 rule 24)."""
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    res: Dict[str, List[float]] = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(iters):
+                f()
+            b.record()
+            b.synchronize()
+            res[k].append(a.elapsed_time(b) * 1e3 / iters)
+    return {k: statistics.median(v) for k, v in res.items()}
+
+
+def bench_gemm_ablate(dev) -> List[Dict]:
+    """Where the prefill tile kernel's cycles go: full kernel vs no LDS-DMA in the K loop vs no
+    fragment reads, for one tile alone (one CU) and for a full chip (M = 4096, N = 4096)."""
+    from ..ops import _native as Nn
+    out = []
+    for M, N_, K in [(256, 256, 32768), (4096, 4096, 4096), (4096, 28672, 4096), (2048, 6144, 4096),
+                     (4096, 4096, 14336)]:
+        x = ((torch.rand((M, K), device=dev) * 2 - 1) * 0.5).to(torch.bfloat16)
+        w = ((torch.rand((N_, K), device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        y = torch.empty((M, N_), dtype=torch.bfloat16, device=dev)
+        row = {"op": "gemm_ablate", "M": M, "N": N_, "K": K}
+        variants = ((0, "full"), (1, "no_glds"), (2, "no_dsread"), (3, "no_vmwait"), (10, "bal0"))
+
+        def mk(ab):
+            return lambda: Nn.call("penny_gemm_prefill_ablate", Nn.ptr(x), K, Nn.ptr(w), K, Nn.ptr(y), N_, M, N_, ab,
+                                   Nn.stream())
+        ts = interleaved({name: mk(ab) for ab, name in variants})
+        for name, us in ts.items():
+            row[name + "_us"] = round(us, 1)
+            row[name + "_TF"] = round(2 * M * N_ * K / us / 1e6, 1)
+        ref = x.float() @ w.float().t()
+        for ab, name in ((0, "full"), (10, "bal0")):
+            Nn.call("penny_gemm_prefill_ablate", Nn.ptr(x), K, Nn.ptr(w), K, Nn.ptr(y), N_, M, N_, ab, Nn.stream())
+            row[name + "_err"] = round(float((y.float() - ref).abs().max() / ref.abs().max()), 4)
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
+def check_gemm_hip(dev) -> List[Dict]:
+    """Numerics of gemm_prefill.hip against an f32 reference at odd M, every epilogue."""
+    from ..ops import gemm
+    out = []
+    g = torch.Generator(device=dev).manual_seed(0)
+    for M, N, K, epi, S in [(1, 256, 64, None, 1), (300, 512, 256, None, 1), (257, 768, 4096, "silu", 1),
+                            (1000, 1024, 1024, "slabs", 4), (4096, 6144, 4096, None, 1), (513, 4096, 14336, "slabs", 2),
+                            (777, 512, 512, "residual", 1)]:
+        x = torch.randn((M, K), generator=g, device=dev).to(torch.bfloat16)
+        w = (torch.randn((N, K), generator=g, device=dev) * 0.05).to(torch.bfloat16)
+        r = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16) if epi == "residual" else None
+        y = gemm.prefill_gemm(x, w, epi, S, residual=r)
+        ref = x.float() @ w.float().t()
+        if epi == "silu":
+            from ..ops.activation import silu_mul
+            ref = silu_mul(ref.to(torch.bfloat16), interleave16=True).float()
+            got = y.float()
+        elif epi == "slabs":
+            got = y.sum(0)
+        elif epi == "residual":
+            ref = ref + r.float()
+            got = y.float()
+        else:
+            got = y.float()
+        err = float((got - ref).abs().max() / ref.abs().max())
+        out.append({"op": "gemm_hip_check", "M": M, "N": N, "K": K, "epi": epi, "S": S, "rel_err": round(err, 5)})
+        print(json.dumps(out[-1]), flush=True)
+    # fused QKV + RoPE + KV write vs hipBLASLt + rope_kv_write
+    from ..ops.attention import rope_cos_sin, rope_kv_write
+    Hq, Hkv, K = 32, 8, 4096
+    cs = rope_cos_sin(128, 8192, 500000.0, device=dev)
+    for M in (300, 2048):
+        x = torch.randn((M, K), generator=g, device=dev).to(torch.bfloat16)
+        w = (torch.randn(((Hq + 2 * Hkv) * 128, K), generator=g, device=dev) * 0.02).to(torch.bfloat16)
+        pos = torch.randint(0, 8000, (M,), generator=g, device=dev, dtype=torch.int32)
+        nb = (M + 63) // 64 + 2
+        perm = torch.randperm(nb * 64, generator=g, device=dev)[:M].to(torch.int32)
+        slots = torch.where(torch.arange(M, device=dev) % 7 == 3, torch.full_like(perm, -1), perm)
+        kc = [torch.zeros((nb, Hkv, 64 * 128), dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        vc = [torch.zeros((nb, Hkv, 64 * 128), dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        q0 = rope_kv_write(torch.nn.functional.linear(x, w), pos, cs, slots, kc[0], vc[0], Hq, Hkv, 128)
+        q1 = gemm.prefill_qkv_rope(x, w, pos, cs, slots, kc[1], vc[1], Hq, Hkv)
+        errs = [float((a.float() - b.float()).abs().max()) for a, b in ((q0, q1), (kc[0], kc[1]), (vc[0], vc[1]))]
+        out.append({"op": "gemm_hip_check_qkv_rope", "M": M, "max_abs_err_q_k_v": [round(e, 4) for e in errs],
+                    "scale": round(float(q0.float().abs().max()), 3)})
+        print(json.dumps(out[-1]), flush=True)
+    return out
+
+
 def interleave16_rows(w: torch.Tensor) -> torch.Tensor:
     from ..ops.gemm import interleave16
     half = w.shape[0] // 2
@@ -574,7 +774,7 @@ def main(argv=None) -> int:
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
-                "moe_prefill": bench_moe_prefill,
+                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "prefill_policy": bench_prefill_policy, "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),

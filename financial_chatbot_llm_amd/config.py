@@ -200,6 +200,9 @@ class ServingConfig:
     history_token_budget: Optional[int] = None
     backend: str = "engine"                 # "engine" | "stub"
     tools: bool = True                      # False: legacy single-chain chat, no decide step (A9)
+    # POST /v1/transactions is only served when an operator token is configured, and every call
+    # must present it (Authorization: Bearer <token>); unset = the write path does not exist
+    ingest_token: Optional[str] = None
 
     @classmethod
     def from_env(cls, **overrides) -> "ServingConfig":
@@ -211,6 +214,7 @@ class ServingConfig:
             history_token_budget=(_env_int("PENNY_HISTORY_TOKEN_BUDGET", 0) or None),
             backend=_env("PENNY_BACKEND", cls.backend),
             tools=_env_bool("PENNY_TOOLS", True),
+            ingest_token=_env("PENNY_INGEST_TOKEN", "") or None,
         )
         return dataclasses.replace(c, **overrides)
 

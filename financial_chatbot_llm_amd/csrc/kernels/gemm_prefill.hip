@@ -1,0 +1,437 @@
+// Prefill projection GEMM (K3 QKV, K8 O, K9 gate|up, K10 down at M = 256..4096+ token rows):
+//   Y[m, n] = sum_k X[m, k] * W[n, k]          X [M, K] bf16 (row stride ldx), W [N, K] bf16
+// with the epilogue fused into the tile:
+//   EPI_BF16  Y bf16 [M, N] (row stride ldy)
+//   EPI_SILU  W is the 16-row-interleaved gate|up weight (ops/gemm.py interleave16):
+//             Y[m, f] = silu(gate) * up, bf16 [M, N/2] -- no [M, N] gate|up intermediate in HBM
+//   EPI_SLAB  split-K: P[s, m, n] f32 partial sums over K slice s (S slices), reduced by the
+//             consumer's own row pass (residual-add + RMSNorm, RoPE + KV write) -- fills the
+//             256 CUs at small M without an extra reduce launch
+//   EPI_RESID Y bf16 = bf16(acc) + R (residual add fused, rounded like GEMM-then-add)
+//   EPI_ROPE  the fused QKV projection (K3+K4+K5): a wave's 128 output columns are exactly one
+//             head, so the rotate-half RoPE pair (d, d+64) sits in one lane (accumulators f, f+4);
+//             q heads -> rotated q [M, Hq, 128]; k heads -> rotated, v heads -> as is, both
+//             scattered into the paged fragment-native KV cache (kv_layout.h).  Replaces the
+//             [M, (Hq+2Hkv)*128] QKV activation round trip and the rope_kv pass.
+//
+// Why a hand-written kernel: hipBLASLt runs these shapes at 0.59-1.5 PF/s at the M the serving
+// scheduler emits (profiles/r2_gemm_prefill_tunableop_sweep.jsonl), its best case is 256x256
+// tiles launched with no K split (48 of 256 CUs busy for QKV at M = 512), and its epilogues
+// (SiLU, residual) are separate passes over HBM.
+//
+// Structure (gfx950, one 512-thread workgroup per CU, 256 x 256 output tile, BK = 64):
+//   * 8 waves as 2 (W rows) x 4 (tokens); each wave owns a 128 x 64 (n x token) sub-tile as
+//     8 x 4 v_mfma_f32_16x16x32_bf16 accumulators.  MFMA A = W (so a lane's 4 accumulator
+//     registers are 4 CONSECUTIVE output columns n -> vector stores, and a head's 128 dims sit in
+//     one wave), MFMA B = X.
+//   * both operands are staged into LDS by global_load_lds (16 B/lane, 1 KiB lane-linear pieces
+//     of 8 rows x 128 B); the XOR swizzle phys_chunk = chunk ^ ((row >> 1) & 7) is applied on the
+//     per-lane SOURCE address and on the fragment read, which makes every 16-lane phase of the
+//     ds_read_b128 fragment reads bank-conflict free (2 rows share a 256-B bank row).
+//   * LDS = 2 K-tiles x 4 half-tiles of 16 KiB, ordered by the phase that reads them:
+//     W_q0 (W rows of quadrant-row 0 of both wave rows), X_q0, X_q1, W_q1.
+//   * each K-tile runs as 4 phases {fragment ds_reads ; issue one half-tile of prefetch ;
+//     s_barrier ; 16 MFMA ; s_barrier}.  A half-tile is restaged one phase after its last read,
+//     so 3 half-tiles (6 loads per wave) stay in flight across every barrier: the only vmcnt wait
+//     is a COUNTED vmcnt(6) once per K-tile (never 0 in the steady state).
+//   * blockIdx is remapped bijectively so each XCD owns a contiguous range of tiles, grouped
+//     4 token-tiles x N so the XCD's 32 concurrent tiles share X and W panels in its L2.
+#include "common.h"
+#include "kv_layout.h"
+
+#include <type_traits>
+
+namespace {
+
+constexpr int TN = 256;              // W rows (output columns) per tile
+constexpr int TM = 256;              // token rows per tile
+constexpr int BK = 64;               // K per stage
+constexpr int HALF = 128 * 128;      // half-tile: 128 rows x 64 bf16 = 16 KiB
+constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
+constexpr int GM = 4;                // token tiles per L2 group
+enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
+enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4 };
+
+struct RopeArgs {
+  const int* positions;   // [M]
+  const float* cos_sin;   // [max_pos, 128]: cos of the 64 frequencies, then sin
+  const int* slots;       // [M] paged-KV slot (block * 64 + offset), < 0 = do not store
+  bf16* q_out;            // [M, Hq, 128]
+  bf16* k_cache;          // [num_blocks, Hkv, 64 * 128]
+  bf16* v_cache;
+  int Hq, Hkv;
+};
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+union Frag {
+  uint4 u;
+  bf16x8 v;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void bar() { __builtin_amdgcn_s_barrier(); }
+
+// Fragment reads.  Row r of a half-tile is at r*128; this lane's row within a 16-row fragment is
+// (lane & 15), whose swizzle (lane >> 1) & 7 is folded into choff[kk].
+__device__ __forceinline__ void read_w(const char* __restrict__ h, Frag (&a)[4][2], int wa, int rowoff,
+                                       const int (&choff)[2]) {
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      a[f][kk].u = *reinterpret_cast<const uint4*>(h + (wa * 64 + f * 16) * 128 + rowoff + choff[kk]);
+}
+
+__device__ __forceinline__ void read_x(const char* __restrict__ h, Frag (&b)[2][2], int wb, int rowoff,
+                                       const int (&choff)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      b[t][kk].u = *reinterpret_cast<const uint4*>(h + (wb * 32 + t * 16) * 128 + rowoff + choff[kk]);
+}
+
+template <int F0, int T0>
+__device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const Frag (&a)[4][2], const Frag (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc[F0 + f][T0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk].v, b[t][kk].v, acc[F0 + f][T0 + t], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// ABL (diagnostic builds only, penny_gemm_prefill_ablate): 1 = no LDS-DMA inside the K loop,
+// 2 = no fragment ds_reads inside the K loop, 3 = LDS-DMA issued but never waited for in the
+// steady state (wrong results; timing attribution only)
+// BAL: balanced fragment-read schedule (below); 0 = the plain 12/4/8/0 schedule (A/B reference)
+template <int EPI, int ABL = 0, int BAL = 1>
+__global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restrict__ X, int ldx,
+                                                           const bf16* __restrict__ W, int K,
+                                                           void* __restrict__ Y, int ldy,
+                                                           const bf16* __restrict__ R, int ldr,
+                                                           int M, int N, int S, RopeArgs ra) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wa = w >> 2, wb = w & 3;  // wave grid 2 (W rows) x 4 (tokens)
+  const int g = lane >> 4, col = lane & 15;
+
+  // ---- tile of this workgroup: bijective XCD remap, then L2 groups of GM token tiles ----
+  const int Mt = (M + TM - 1) / TM, Nt = N / TN, tiles = Mt * Nt, nwg = tiles * S;
+  int id = blockIdx.x;
+  {
+    const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+  }
+  const int s = id / tiles, tile = id - s * tiles;
+  const int grp = tile / (GM * Nt), first = grp * GM, gm = min(Mt - first, GM);
+  const int within = tile - grp * GM * Nt;
+  const int tm = first + within % gm, tn = within / gm;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kc = K / S, k0 = s * kc, nt = kc / BK;
+  PENNY_DASSERT(N % TN == 0 && kc % BK == 0 && tm < Mt && tn < Nt);
+
+  // ---- per-lane LDS-DMA sources: half h, piece i -> LDS rows 16w + 8i .. +7 of that half ----
+  const char* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr = 16 * w + 8 * i + (lane >> 3);
+      const int c = (lane & 7) ^ swz(lr);                 // logical 16-B chunk held by this slot
+      if (h == H_W0 || h == H_W1) {
+        const int n = n0 + (lr >> 6) * 128 + (h == H_W1 ? 64 : 0) + (lr & 63);
+        src[h][i] = reinterpret_cast<const char*>(W + (long)n * K + k0 + 8 * c);
+      } else {
+        const int m = min(m0 + (lr >> 5) * 64 + (h == H_X1 ? 32 : 0) + (lr & 31), M - 1);
+        src[h][i] = reinterpret_cast<const char*>(X + (long)m * ldx + k0 + 8 * c);
+      }
+    }
+  // The LDS-DMA is issued from inline asm, invisible to hipcc's waitcnt pass: with the builtin,
+  // hipcc cannot prove the fragment ds_reads do not alias the in-flight DMA and drains vmcnt(0)
+  // before every phase.  The counted vmcnt(6) below is then the only wait on these loads (the
+  // loop issues no other vector-memory instruction), and M0 is set and restored in the statement.
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  auto stage = [&](int h, int t, unsigned buf) {
+    if (ABL == 1 && t > 1) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const char* gp = src[h][i] + (long)t * (BK * 2);
+      const unsigned dst = buf + h * HALF + (16 * w + 8 * i) * 128;
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(gp), "s"(dst)
+                   : "memory");
+    }
+  };
+
+  const int rowoff = col * 128;
+  const int choff[2] = {((0 + g) ^ ((col >> 1) & 7)) << 4, ((4 + g) ^ ((col >> 1) & 7)) << 4};
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag a[4][2], b0[2][2], b1[2][2];
+
+  // ---- prologue: K-tile 0 whole, K-tile 1 halves W0, X0, X1 ----
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(h, 0, lds0);
+  if (nt > 1) {
+#pragma unroll
+    for (int h = 0; h < 3; ++h) stage(h, 1, lds0 + BUF);
+    wait_vm<6>();
+  } else {
+    wait_vm<0>();
+  }
+  bar();
+  // Stagger: waves 4-7 (wave row wa = 1; SIMD s hosts waves s and s+4, one of each row) pass one
+  // extra barrier here, so barrier instance i is phase-body i of one row and i-1 of the other:
+  // each SIMD alternates one wave's fragment ds_reads with its partner's 16 MFMAs.  Hazards with
+  // the offset: a W half-tile is restaged only by the wave row that reads it (rows 64*wa..), and
+  // an X half-tile is restaged by the other row >= 1 barrier instance after this row's reads of
+  // it retired (lgkmcnt(0) before the row's next barrier); the vmcnt(6) wait of phase 4 precedes
+  // that row's barrier instance 8t+7 (row 0) / 8t+8 (row 1) and the next tile's first read
+  // follows instance 8t+8 / 8t+9.  Row 0 passes one extra barrier after the loop to balance.
+  if (wa == 1) bar();
+
+  // one phase: [fragment reads + DMA issued by the caller] barrier lgkmcnt(0) 16 MFMAs barrier
+  auto phase = [&](auto F0c, auto T0c, const Frag (&aa)[4][2], const Frag (&bb)[2][2]) {
+    constexpr int F0 = decltype(F0c)::value, T0 = decltype(T0c)::value;
+    bar();
+    wait_lgkm0();
+    mma<F0, T0>(acc, aa, bb);
+    bar();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
+
+  if constexpr (BAL) {
+    // Balanced read schedule: the next K-tile's X_q0 fragments (B0) are read in phase 4, which
+    // reads nothing otherwise, so each phase moves 8 / 4 / 8 / 4 fragments per wave instead of
+    // 12 / 4 / 8 / 0 (phase 1's 48 KB of reads + 16 KB of landing DMA filled its whole MFMA
+    // window on the LDS).  The extra wait: vmcnt(8) in phase 3 retires X_q0 (and W_q0) of t+1
+    // (4 younger half-tiles may stay in flight), a phase before it is read.
+    Frag c0[2][2];
+    auto tile = [&](int t, Frag (&bc)[2][2], Frag (&bn)[2][2]) {
+      const char* cur = smem + (t & 1) * BUF;
+      const char* nx = smem + ((t + 1) & 1) * BUF;
+      const unsigned lcur = lds0 + (t & 1) * BUF, lnxt = lds0 + ((t + 1) & 1) * BUF;
+      const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+      if (ABL != 2 || t == 0) read_w(cur + H_W0 * HALF, a, wa, rowoff, choff);
+      if (more1) stage(H_W1, t + 1, lnxt);
+      phase(I0{}, I0{}, a, bc);
+      if (ABL != 2 || t == 0) read_x(cur + H_X1 * HALF, b1, wb, rowoff, choff);
+      if (more2) stage(H_W0, t + 2, lcur);
+      phase(I0{}, I2{}, a, b1);
+      if (ABL != 2 || t == 0) read_w(cur + H_W1 * HALF, a, wa, rowoff, choff);
+      if (more2) {
+        stage(H_X0, t + 2, lcur);
+        if (ABL != 3) wait_vm<8>();
+      } else {
+        wait_vm<0>();
+      }
+      phase(I4{}, I2{}, a, b1);
+      if (more1 && (ABL != 2 || t == 0)) read_x(nx + H_X0 * HALF, bn, wb, rowoff, choff);
+      if (more2) {
+        stage(H_X1, t + 2, lcur);
+        if (ABL != 3) wait_vm<6>();
+      } else {
+        wait_vm<0>();
+      }
+      phase(I4{}, I0{}, a, bc);
+    };
+    read_x(smem + H_X0 * HALF, b0, wb, rowoff, choff);
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+      tile(t, b0, c0);
+      tile(t + 1, c0, b0);
+    }
+    if (t < nt) tile(t, b0, c0);
+  } else {
+    for (int t = 0; t < nt; ++t) {
+      const char* cur = smem + (t & 1) * BUF;
+      const unsigned lcur = lds0 + (t & 1) * BUF, lnxt = lds0 + ((t + 1) & 1) * BUF;
+      const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+      // phase 1: W_q0 x X_q0          restage: W_q1 of tile t+1 (read last in phase 3 of t-1)
+      if (ABL != 2 || t == 0) {
+        read_w(cur + H_W0 * HALF, a, wa, rowoff, choff);
+        read_x(cur + H_X0 * HALF, b0, wb, rowoff, choff);
+      }
+      if (more1) stage(H_W1, t + 1, lnxt);
+      phase(I0{}, I0{}, a, b0);
+      // phase 2: W_q0 x X_q1          restage: W_q0 of tile t+2 (read in phase 1)
+      if (ABL != 2 || t == 0) read_x(cur + H_X1 * HALF, b1, wb, rowoff, choff);
+      if (more2) stage(H_W0, t + 2, lcur);
+      phase(I0{}, I2{}, a, b1);
+      // phase 3: W_q1 x X_q1          restage: X_q0 of tile t+2 (read in phase 1)
+      if (ABL != 2 || t == 0) read_w(cur + H_W1 * HALF, a, wa, rowoff, choff);
+      if (more2) stage(H_X0, t + 2, lcur);
+      phase(I4{}, I2{}, a, b1);
+      // phase 4: W_q1 x X_q0          restage: X_q1 of tile t+2 (read in phase 2); retire tile t+1
+      // (the 3 younger half-tiles of t+2 may stay in flight)
+      if (more2) {
+        stage(H_X1, t + 2, lcur);
+        if (ABL != 3) wait_vm<6>();
+      } else {
+        wait_vm<0>();
+      }
+      phase(I4{}, I0{}, a, b0);
+    }
+  }
+  if (wa == 0) bar();
+
+  // ---- epilogue: lane holds Y[m0 + wb*64 + 16t + col][n0 + wa*128 + 16f + 4g + r], r = 0..3 ----
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int m = m0 + wb * 64 + t * 16 + col;
+    if (m >= M) continue;
+    if constexpr (EPI == EPI_ROPE) {
+      constexpr int D = 128;
+      const int hd = (n0 + wa * 128) >> 7;     // this wave's head (q heads, then k, then v)
+      const int slot = ra.slots[m];
+      if (hd >= ra.Hq && slot < 0) continue;
+      const long blk = slot >= 0 ? slot / KV_BS : 0;
+      const int off = slot >= 0 ? slot % KV_BS : 0;
+      if (hd < ra.Hq + ra.Hkv) {
+        const float* cs = ra.cos_sin + (long)ra.positions[m] * D;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int d = f * 16 + 4 * g;       // this lane's dims d..d+3 and d+64..d+67
+          const f32x4 co = *reinterpret_cast<const f32x4*>(cs + d), si = *reinterpret_cast<const f32x4*>(cs + 64 + d);
+          bf16x4 o1, o2;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // GEMM output rounded to bf16 first, as the unfused GEMM -> rope_kv path does
+            const float x1 = (float)(bf16)acc[f][t][r], x2 = (float)(bf16)acc[f + 4][t][r];
+            o1[r] = (bf16)(x1 * co[r] - x2 * si[r]);
+            o2[r] = (bf16)(x2 * co[r] + x1 * si[r]);
+          }
+          if (hd < ra.Hq) {
+            bf16* q = ra.q_out + ((long)m * ra.Hq + hd) * D;
+            *reinterpret_cast<bf16x4*>(q + d) = o1;
+            *reinterpret_cast<bf16x4*>(q + 64 + d) = o2;
+          } else {
+            bf16* kb = ra.k_cache + (blk * ra.Hkv + (hd - ra.Hq)) * (long)(KV_BS * D);
+            *reinterpret_cast<bf16x4*>(kb + k_index(off, d, D)) = o1;
+            *reinterpret_cast<bf16x4*>(kb + k_index(off, 64 + d, D)) = o2;
+          }
+        }
+      } else {
+        bf16* vb = ra.v_cache + (blk * ra.Hkv + (hd - ra.Hq - ra.Hkv)) * (long)(KV_BS * D);
+#pragma unroll
+        for (int f = 0; f < 8; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) vb[v_index(off, f * 16 + 4 * g + r, D)] = (bf16)acc[f][t][r];
+      }
+    } else if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+      for (int f = 0; f < 8; f += 2) {
+        // row group G (16 W rows) is gate (G even) / up (G odd) of output columns 16*(G/2)..+15
+        const int G = (n0 + wa * 128 + f * 16) >> 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // same roundings as GEMM -> bf16 gate|up -> silu_mul (HF: silu in the activation dtype)
+          const float gt = (float)(bf16)acc[f][t][r], up = (float)(bf16)acc[f + 1][t][r];
+          o[r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
+        }
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(Y) + (long)m * ldy + (G >> 1) * 16 + 4 * g) = o;
+      }
+    } else if constexpr (EPI == EPI_SLAB) {
+      float* P = static_cast<float*>(Y) + (long)s * M * N + (long)m * N;
+#pragma unroll
+      for (int f = 0; f < 8; ++f) *reinterpret_cast<f32x4*>(P + n0 + wa * 128 + f * 16 + 4 * g) = acc[f][t];
+    } else {
+      bf16* y = static_cast<bf16*>(Y) + (long)m * ldy;
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const int n = n0 + wa * 128 + f * 16 + 4 * g;
+        bf16x4 o;
+        if constexpr (EPI == EPI_RESID) {
+          const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long)m * ldr + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)(bf16)acc[f][t][r] + (float)rr[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[f][t][r];
+        }
+        *reinterpret_cast<bf16x4*>(y + n) = o;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+template <int EPI, int ABL = 0, int BAL = 1>
+static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
+                   const void* R, int ldr, int M, int N, int S, const RopeArgs& ra) {
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, (const bf16*)X, ldx, (const bf16*)W, K, Y,
+                     ldy, (const bf16*)R, ldr, M, N, S, ra);
+}
+
+static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
+
+// Contract (checked): N % 256 == 0, K % (64*S) == 0, ldx % 8 == 0, rows 16-B aligned; EPI_SILU
+// needs S == 1 and ldy % 4 == 0 (Y is [M, N/2]); EPI_SLAB writes P [S, M, N] f32 (ldy unused);
+// EPI_RESID needs R (row stride ldr, ldr % 4 == 0) and S == 1.
+PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, void* Y, int ldy, const void* R,
+                                 int ldr, int M, int N, int S, int epi, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % TN || S < 1 || K % (BK * S) || ldx % 8 || epi < 0 || epi > 3) return (int)hipErrorInvalidValue;
+  if (epi != EPI_SLAB && (S != 1 || ldy % 4)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!R || ldr % 4)) return (int)hipErrorInvalidValue;
+  if ((long)((M + TM - 1) / TM) * (N / TN) * S > (1L << 30)) return (int)hipErrorInvalidValue;
+  const dim3 grid = grid_for(M, N, S);
+  const RopeArgs ra{};
+  switch (epi) {
+    case EPI_BF16: launch<EPI_BF16>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    case EPI_SILU: launch<EPI_SILU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    case EPI_SLAB: launch<EPI_SLAB>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    default: launch<EPI_RESID>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra);
+  }
+  return (int)hipGetLastError();
+}
+
+// Fused QKV projection + RoPE + paged KV write (head dim 128): W [(Hq + 2*Hkv)*128, K] (q heads,
+// k heads, v heads), positions / slots [M] int32, cos_sin [max_pos, 128] f32, q_out [M, Hq, 128].
+// Contract (checked): N == (Hq + 2*Hkv)*128, N % 256 == 0, K % 64 == 0, ldx % 8 == 0.
+PENNY_API int penny_gemm_prefill_qkv_rope(const void* X, int ldx, const void* W, int K, int M, const int* positions,
+                                          const float* cos_sin, const int* slots, void* q_out, void* k_cache,
+                                          void* v_cache, int Hq, int Hkv, hipStream_t stream) {
+  if (M <= 0) return 0;
+  const int N = (Hq + 2 * Hkv) * 128;
+  if (Hq <= 0 || Hkv <= 0 || N % TN || K % BK || ldx % 8 || !positions || !cos_sin || !slots || !q_out)
+    return (int)hipErrorInvalidValue;
+  const RopeArgs ra{positions, cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv};
+  launch<EPI_ROPE>(grid_for(M, N, 1), stream, X, ldx, W, K, nullptr, 0, nullptr, 0, M, N, 1, ra);
+  return (int)hipGetLastError();
+}
+
+// Diagnostic: bf16-epilogue GEMM with part of the K loop removed (ablate 1: LDS-DMA, 2: fragment
+// reads).  Results are WRONG by construction; bench/kernels.py gemm_ablate uses the timings only.
+PENNY_API int penny_gemm_prefill_ablate(const void* X, int ldx, const void* W, int K, void* Y, int ldy, int M, int N,
+                                        int ablate, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % TN || K % BK || ldx % 8 || ldy % 4) return (int)hipErrorInvalidValue;
+  const RopeArgs ra{};
+  if (ablate == 1) launch<EPI_BF16, 1>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  else if (ablate == 10) launch<EPI_BF16, 0, 0>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  else if (ablate == 3) launch<EPI_BF16, 3>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  else if (ablate == 2) launch<EPI_BF16, 2>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  else launch<EPI_BF16, 0>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  return (int)hipGetLastError();
+}

@@ -163,13 +163,18 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
                       np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32), src_a)
 
 
+class CollectiveTimeout(RuntimeError):
+    """A device-side collective (custom xGMI all-reduce) reported a missing peer."""
+
+
 class PendingStep:
     """Sampled ids of a launched step (host copy in flight)."""
 
     def __init__(self, cpu_out: Optional[torch.Tensor], n: int, host: Optional[torch.Tensor], event,
-                 start_event=None, stats: Optional[Dict] = None, key: str = ""):
+                 start_event=None, stats: Optional[Dict] = None, key: str = "", check_err: bool = False):
         self._cpu, self.n, self._host, self._event = cpu_out, n, host, event
         self._start, self._stats, self._key = start_event, stats, key
+        self._check_err = check_err
 
     def result(self) -> List[int]:
         if self.n == 0:
@@ -188,6 +193,9 @@ class PendingStep:
                     st["gpu_idle_s"] += gap
                     st["gpu_idle_gaps"] += 1
             st["_prev_end_ev"] = self._event
+        if self._check_err and int(self._host[self.n]):
+            raise CollectiveTimeout("custom all-reduce: a TP peer missed the bounded wait; this step's "
+                                    "hidden states are stale")
         return self._host[:self.n].tolist()
 
 
@@ -229,7 +237,8 @@ class ModelRunner:
         # from here when it was launched before this one's ids reached the host (overlap mode)
         self.max_samplers = max(self.max_decode_batch, max_decode_batch) + 1024
         self.last_sampled = torch.zeros(self.max_samplers, dtype=torch.int32, device=self.device)
-        self._pinned_out = ([torch.zeros(self.max_samplers, dtype=torch.int32).pin_memory() for _ in range(2)]
+        # one slot past the sampled ids carries the custom all-reduce's timeout flag back with them
+        self._pinned_out = ([torch.zeros(self.max_samplers + 1, dtype=torch.int32).pin_memory() for _ in range(2)]
                             if self.on_gpu else None)
         self._out_flip = 0
         # eager-step inputs: one pinned staging ring slot -> ONE H2D copy per step (see _stage_inputs)
@@ -422,9 +431,15 @@ class ModelRunner:
         host = self._pinned_out[self._out_flip]
         self._out_flip ^= 1
         host[:n].copy_(out[:n], non_blocking=True)
+        ar = comm.custom_all_reduce()
+        if ar is not None:
+            # the xGMI all-reduce never raises from the device: a peer that missed its bounded wait
+            # sets ar.err and the step's sums are stale, so the flag rides the per-step host sync
+            host[n:n + 1].copy_(ar.err, non_blocking=True)
         ev = torch.cuda.Event(enable_timing=start_ev is not None)
         ev.record()
-        return PendingStep(None, n, host, ev, start_ev, self.stats, "gpu_graph_s" if graph else "gpu_eager_s")
+        return PendingStep(None, n, host, ev, start_ev, self.stats, "gpu_graph_s" if graph else "gpu_eager_s",
+                           check_err=ar is not None)
 
     def _forward_only(self, si: StepInputs) -> None:
         self._hidden(si)

@@ -3,9 +3,10 @@
 Replaces the remote Gemini model of the reference (``llm_agent.py:34-45``) with a local
 decoder whose per-layer hot path is (SURVEY §3.6)::
 
-    K2 add+RMSNorm -> K3 QKV GEMM (hipBLASLt) -> K4/K5 RoPE + paged KV write (HIP)
-    -> K6/K7 paged attention (HIP, MFMA) -> K8 O GEMM [-> C1 all-reduce]
-    -> K2 add+RMSNorm -> K9 gate|up GEMM -> SiLU*mul (HIP) -> K10 down GEMM [-> C1]
+    K2 add+RMSNorm -> K3 QKV GEMM -> K4/K5 RoPE + paged KV write (fused into the prefill tile GEMM's
+    epilogue, or a separate HIP pass) -> K6/K7 paged attention (HIP, MFMA) -> K8 O GEMM [-> C1
+    all-reduce] -> K2 add+RMSNorm -> K9 gate|up GEMM + SiLU*mul (fused epilogue) -> K10 down GEMM
+    [-> C1]; the GEMM kernel per shape and step size follows ops/gemm.py (PREFILL_POLICY).
 
 Weights are plain bf16 tensors (``[out, in]``), sharded Megatron-style over the TP group:
 QKV/gate-up column-parallel (whole heads per rank), O/down row-parallel, embedding and LM head
@@ -24,7 +25,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.dist import state as pstate
-from ..ops.gemm import interleave16, linear, tile_weight, uses_tiled_weight
+from ..ops.gemm import interleave16, linear, prefill_qkv_rope, qkv_rope_fused, tile_weight, uses_tiled_weight
 from ..parallel.layers import shard_cols, shard_rows, shard_sections, vocab_range
 from .common import AttentionMetadata, KVCache, random_tensor
 from .configs import ModelConfig
@@ -160,11 +161,16 @@ class DecoderModel:
                   kv: KVCache, reduce: bool = True) -> torch.Tensor:
         p = f"layers.{i}."
         T = h.shape[0]
-        # QKV is column-parallel: even under TP its split-K slabs go straight to the RoPE/KV-write
-        # pass (no all-reduce in between), unlike the row-parallel O / down projections
-        qkv = linear(h, self.w[p + "qkv"], wt=self.wt.get(p + "qkv"), slabs=True)
         kc, vc = kv.k(i), kv.v(i)
-        q = ops.rope_kv_write(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv, self.D)
+        if qkv_rope_fused(h, self.w[p + "qkv"], self.D):
+            # prefill step: QKV GEMM with RoPE + paged KV write in its epilogue (K3+K4+K5, one pass)
+            q = prefill_qkv_rope(h, self.w[p + "qkv"], positions, self.cos_sin, meta.slots, kc, vc, self.hq,
+                                 self.hkv)
+        else:
+            # QKV is column-parallel: even under TP its split-K slabs go straight to the RoPE/KV-write
+            # pass (no all-reduce in between), unlike the row-parallel O / down projections
+            qkv = linear(h, self.w[p + "qkv"], wt=self.wt.get(p + "qkv"), slabs=True)
+            q = ops.rope_kv_write(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv, self.D)
         attn = torch.empty_like(q)
         tp = meta.num_prefill_tokens
         if tp > 0:

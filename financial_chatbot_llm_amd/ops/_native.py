@@ -34,6 +34,9 @@ _SIGS = {
     "penny_splitk_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_reduce": [P, c_int, c_int, c_int, P, c_int, P, c_int, P],
     "penny_gateup_silu_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_gemm_prefill": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_gemm_prefill_qkv_rope": [P, c_int, P, c_int, c_int, P, P, P, P, P, P, c_int, c_int, P],
+    "penny_gemm_prefill_ablate": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P],
     "penny_gelu": [P, c_long, P],
     "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],

@@ -1,4 +1,5 @@
-"""Projection GEMMs: hand-written weight-streaming MFMA kernels for decode, hipBLASLt for prefill.
+"""Projection GEMMs: hand-written MFMA kernels -- weight-streaming ones for decode, the 256x256 tile
+kernel (gemm_prefill.hip) with fused epilogues for prefill -- and hipBLASLt where it measured faster.
 
 ``linear(x, w, epilogue=..., wt=..., slabs=...)`` is the single entry point the models use.  For a
 decode-size M on the GPU, in order:
@@ -10,10 +11,11 @@ decode-size M on the GPU, in order:
 * a ``TUNING`` entry -> ``penny_skinny_gemm`` (M <= 16-32, fused SiLU / residual epilogues).
 
 These kernels stream either the fragment-tiled copy ``wt`` (``tile_weight``; made at load only
-for shapes with an entry, see ``uses_tiled_weight``) or the row-major weight itself.  Everything
-else (prefill-size M, unmeasured shapes) runs hipBLASLt via ``torch.nn.functional.linear``, plus
-the matching HIP epilogue kernel (``silu_mul(interleave16=True)``) or a fused add.  Every table
-entry was measured on MI355X with ``bench/kernels.py`` (profiles named next to each table).
+for shapes with an entry, see ``uses_tiled_weight``) or the row-major weight itself.  Prefill-size
+M (> 256 rows) follows ``PREFILL_POLICY``: the tile kernel with the SiLU / residual epilogue or
+split-K slabs, or hipBLASLt via ``torch.nn.functional.linear`` plus the matching HIP epilogue
+kernel (``silu_mul(interleave16=True)``) or a fused add.  Every table entry was measured on MI355X
+with ``bench/kernels.py`` (profiles named next to each table).
 """
 from __future__ import annotations
 
@@ -78,6 +80,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
     ``ops.rope_kv_write`` -- sums them in its own pass)."""
     M, K = x.shape
     N_ = w.shape[0]
+    if M > 256 and prefill_ok(x, w) and epilogue in (None, "silu", "residual"):
+        c = prefill_choice(M, N_, K, epilogue, slabs and residual is None)
+        if c == "hip":
+            return prefill_gemm(x, w, epilogue, residual=residual)
+        if c.startswith("S"):
+            return Slabs(prefill_gemm(x, w, "slabs", int(c[1:])))
     # the decode kernels stream either the fragment-tiled copy or (DECODE_WEIGHTS == "rowmajor",
     # or no copy was made) the row-major weight itself
     src = wt if wt is not None else (w if w.is_contiguous() else None)
@@ -285,6 +293,126 @@ def splitk_reduce(P: torch.Tensor, residual: Optional[torch.Tensor] = None,
     N.call("penny_splitk_reduce", N.ptr(P), S, M, N_, N.ptr(y), y.stride(0), N.ptr(residual),
            residual.stride(0) if residual is not None else 0, N.stream())
     return y
+
+
+# ----------------------------------------------------------------------------------------------
+# Prefill GEMM (M > 256 token rows): 256x256-tile MFMA kernel with fused epilogues
+# ----------------------------------------------------------------------------------------------
+PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3}
+
+
+# Which path each Llama-3-8B projection takes at a prefill step of M rows (M > 256), measured with
+# its consumer on MI355X, interleaved A/B (bench/kernels.py prefill_policy,
+# profiles/r3_prefill_policy_v2.jsonl): (N, K) -> [(max M, choice), ...], first match wins.
+#   "lib"  hipBLASLt (+ the separate epilogue pass)       "hip"  tile kernel, fused epilogue
+#   "S<n>" tile kernel split-K into n f32 slabs (only where the consumer reads slabs)
+#   "fused" (QKV only) tile kernel with RoPE + paged-KV-write epilogue (prefill_qkv_rope)
+# Shapes without an entry use ``_default_choice``.
+PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
+    (6144, 4096): [(1536, "lib"), (2816, "fused"), (3840, "lib"), (1 << 30, "fused")],     # QKV
+    (4096, 4096): [(1 << 30, "lib")],                                                     # O
+    (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
+    (4096, 14336): [(1024, "S4"), (2048, "S2"), (1 << 30, "lib")],                        # down
+}
+
+
+def _default_choice(M: int, N_: int, K: int, epilogue: Optional[str]) -> str:
+    """Unmeasured shapes: the tile kernel once its 256x256 tiles cover the 256 CUs (one tile
+    alone runs ~80 us at K = 4096, so fewer tiles lose to the library's smaller ones)."""
+    tiles = -(-M // 256) * (N_ // 256)
+    return "hip" if tiles >= 224 or (epilogue == "silu" and tiles >= 112) else "lib"
+
+
+def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slabs: bool = False) -> str:
+    if os.environ.get("PENNY_PREFILL_GEMM", "1") == "0":
+        return "lib"
+    force = os.environ.get("PENNY_PREFILL_GEMM") == "force"
+    rows = PREFILL_POLICY.get((N_, K))
+    choice = None
+    if rows is not None and not force:
+        for max_m, c in rows:
+            if M <= max_m:
+                choice = c
+                break
+    if choice is None:
+        choice = "hip" if force else _default_choice(M, N_, K, epilogue)
+    if choice.startswith("S") and not (slabs and epilogue is None and K % (64 * int(choice[1:])) == 0):
+        choice = "hip" if force else "lib"
+    if choice == "fused":           # only the QKV entry point (qkv_rope_choice) fuses RoPE
+        choice = "hip"
+    return choice
+
+
+def qkv_rope_fused(x: torch.Tensor, w: torch.Tensor, D: int) -> bool:
+    """Does this prefill step run the fused QKV + RoPE + KV-write tile kernel?"""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if D != 128 or M <= 256 or not prefill_ok(x, w):
+        return False
+    mode = os.environ.get("PENNY_PREFILL_GEMM", "1")
+    if mode == "0":
+        return False
+    if mode == "force":
+        return True
+    rows = PREFILL_POLICY.get((N_, K))
+    if rows is None:
+        return _default_choice(M, N_, K, None) == "hip"
+    return next(c for max_m, c in rows if M <= max_m) == "fused"
+
+
+def prefill_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M, K = x.shape
+    N_ = w.shape[0]
+    return (N.use_native(x) and os.environ.get("PENNY_PREFILL_GEMM", "1") != "0" and N_ % 256 == 0
+            and K % 64 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous())
+
+
+def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None, S: int = 1,
+                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ w.T on the hand-written 256x256 MFMA tile kernel (``gemm_prefill.hip``).
+
+    ``epilogue``: None -> bf16 [M, N]; "silu" -> silu(gate)*up bf16 [M, N/2] from the
+    interleave16 gate|up weight; "slabs" -> f32 split-K partials [S, M, N]; "residual" -> bf16
+    x @ w.T + residual.  The torch path (CPU) computes the same math in f32."""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if not N.use_native(x):
+        if epilogue == "slabs":
+            xs = x.float().view(M, S, K // S).transpose(0, 1)
+            return torch.einsum("smk,snk->smn", xs, w.float().view(N_, S, K // S).transpose(0, 1))
+        y = F.linear(x.float(), w.float()).to(x.dtype)
+        if epilogue == "silu":
+            return silu_mul(y, interleave16=True)
+        if epilogue == "residual":
+            return (y.float() + residual.float()).to(x.dtype)
+        return y
+    if epilogue == "slabs":
+        y = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
+        ldy = N_
+    else:
+        S = 1
+        cols = N_ // 2 if epilogue == "silu" else N_
+        y = out if out is not None else torch.empty((M, cols), dtype=x.dtype, device=x.device)
+        ldy = y.stride(0)
+    N.call("penny_gemm_prefill", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), ldy, N.ptr(residual),
+           residual.stride(0) if residual is not None else 0, M, N_, S, PREFILL_EPI[epilogue], N.stream())
+    return y
+
+
+def prefill_qkv_rope(x: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                     slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, Hq: int,
+                     Hkv: int) -> torch.Tensor:
+    """Fused QKV projection + RoPE + paged KV write (head dim 128) on the prefill tile kernel:
+    returns the rotated q [M, Hq, 128]; k / v land in the caches (slots < 0 are skipped)."""
+    from .attention import rope_kv_write
+    M, K = x.shape
+    if not N.use_native(x):
+        return rope_kv_write(F.linear(x.float(), w.float()).to(x.dtype), positions, cos_sin, slots, k_cache,
+                             v_cache, Hq, Hkv, 128)
+    q = torch.empty((M, Hq, 128), dtype=x.dtype, device=x.device)
+    N.call("penny_gemm_prefill_qkv_rope", N.ptr(x), x.stride(0), N.ptr(w), K, M, N.ptr(positions), N.ptr(cos_sin),
+           N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache), Hq, Hkv, N.stream())
+    return q
 
 
 def untile_weight(wt: torch.Tensor) -> torch.Tensor:

@@ -48,6 +48,11 @@ def enable_custom_all_reduce(max_bytes: int = 4 << 20, buffer_bytes: int = 32 <<
     return _CUSTOM_AR
 
 
+def custom_all_reduce():
+    """The enabled CustomAllReduce of the TP group, or None."""
+    return _CUSTOM_AR
+
+
 def disable_custom_all_reduce() -> None:
     global _CUSTOM_AR
     if _CUSTOM_AR is not None:

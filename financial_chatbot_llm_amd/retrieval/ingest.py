@@ -9,7 +9,7 @@ as the queries (``tools/qdrant_tool.py:28,136-137``).  Here:
 * :class:`CorpusIngestor` embeds ``page_content`` in large batches with the on-device bge encoder
   (K14, bulk mode: thousands of rows per forward) and appends vectors + metadata to the store;
 * ``DeviceVectorStore.save`` / ``.load`` snapshot the collection (safetensors + JSON, no pickles);
-* ``POST /v1/transactions`` (serving/app.py) ingests at runtime.
+* ``POST /v1/transactions`` (serving/app.py) ingests at runtime, in batches interleaved with searches.
 
 CLI (bulk build + snapshot, reports docs/s)::
 
@@ -94,14 +94,26 @@ def iter_documents(path: str, batch_rows: int = 65536) -> Iterator[Dict[str, Any
 class CorpusIngestor:
     """Bulk-embed documents on the GPU and append them to a vector store."""
 
-    def __init__(self, embedder, store, batch_size: int = 1024, max_len: int = 128):
+    def __init__(self, embedder, store, batch_size: int = 1024, max_len: int = 128, lock=None):
+        """``lock`` (optional) is held around each batch's embed + append only, so a caller
+        that serialises searches on the same store with it (the serving RetrievalService) can
+        interleave its searches between batches instead of waiting for the whole ingest."""
         self.embedder, self.store = embedder, store
         self.batch_size, self.max_len = batch_size, max_len
+        self.lock = lock
         self.docs = 0
         self.rejected = 0
         self.seconds = 0.0
 
     def _flush(self, batch: List[Dict[str, Any]]) -> None:
+        if self.lock is not None:
+            with self.lock:
+                self._flush_locked(batch)
+                self._sync()
+        else:
+            self._flush_locked(batch)
+
+    def _flush_locked(self, batch: List[Dict[str, Any]]) -> None:
         texts = [d["page_content"] for d in batch]
         if hasattr(self.embedder, "tokenize"):
             vecs = self.embedder.embed(texts, max_len=self.max_len)

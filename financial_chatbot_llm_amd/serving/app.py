@@ -10,8 +10,14 @@ Endpoints:
 * ``GET /metrics`` -- Prometheus text: turns/s, TTFT p50/p99, ITL, KV utilisation, ...
 * ``POST /v1/transactions`` -- ingest ``{"documents": [{page_content, metadata{user_id, date,
   ...}}]}`` into the on-device collection (bge bulk embedding + append; the upstream Qdrant
-  collection was populated outside the reference repo).  An operator endpoint: put it behind
-  the deployment's auth like any write path.
+  collection was populated outside the reference repo).  Operator-only: the route exists only
+  when ``PENNY_INGEST_TOKEN`` is set and every call must send ``Authorization: Bearer <token>``
+  (documents carry their own ``metadata.user_id``, so an open write path would let any caller
+  plant rows in another user's retrieval results).  Batches of 1024 documents are embedded and
+  appended under the retrieval lock one at a time, so concurrent searches interleave.  The write
+  lands in THIS replica's collection only: with several DP replicas (serving/launch.py, one
+  port per replica) the operator sends the same batch to every replica's port, or builds the
+  collection offline (``retrieval.ingest`` CLI snapshot) and starts every replica from it.
 * ``/docs``, ``/redoc``, ``/openapi.json`` come from FastAPI as in the reference.
 
 The lifespan pings Mongo (raising aborts startup), subscribes the Kafka consumer and starts
@@ -21,12 +27,13 @@ reference (``main.py:18-22``), ONE process owns the GPU engine and serves every 
 from __future__ import annotations
 
 import asyncio
+import hmac
 import json
 from contextlib import asynccontextmanager
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional
 
-from fastapi import FastAPI
+from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel
 
@@ -118,19 +125,22 @@ def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
         res = await services.agent.query(payload.message, user_id, user_context, chat_history)
         return {"response": res["response"], "retrieved_transactions_count": res["retrieved_transactions_count"]}
 
-    @app.post("/v1/transactions")
-    async def ingest_transactions(payload: IngestPayload):
-        svc = services.retrieval
-        if svc is None or not hasattr(svc.store, "add"):
-            return JSONResponse({"detail": "no vector store configured"}, status_code=503)
-        from ..retrieval.ingest import CorpusIngestor
-        ing = CorpusIngestor(svc.embedder, svc.store)
+    if serving.ingest_token:
+        expected = f"Bearer {serving.ingest_token}".encode()
 
-        def run():
-            with svc._lock:          # never interleave with a search batch on the store
-                return ing.ingest(payload.documents)
-        stats = await asyncio.to_thread(run)
-        return {**stats, "size": len(svc.store.corpus)}
+        @app.post("/v1/transactions")
+        async def ingest_transactions(payload: IngestPayload, request: Request):
+            got = request.headers.get("authorization", "").encode()
+            if not hmac.compare_digest(got, expected):
+                return JSONResponse({"detail": "operator token required"}, status_code=401)
+            svc = services.retrieval
+            if svc is None or not hasattr(svc.store, "add"):
+                return JSONResponse({"detail": "no vector store configured"}, status_code=503)
+            from ..retrieval.ingest import CorpusIngestor
+            # the service lock is taken per 1024-document batch, never for the whole request
+            ing = CorpusIngestor(svc.embedder, svc.store, lock=svc._lock)
+            stats = await asyncio.to_thread(ing.ingest, payload.documents)
+            return {**stats, "size": len(svc.store.corpus), "scope": "this replica"}
 
     @app.post("/v1/chat/stream")
     async def chat_stream(payload: MessagePayload):

@@ -1,8 +1,9 @@
 """Custom one-shot / two-shot all-reduce (C1 custom path) on the GPU box.
 
-Only one MI355X is available to the test runner, so two processes share cuda:0: each exports
-its IPC buffers, maps the peer's, and runs the real kernel protocol (flags, double-buffered
-rounds, bounded waits).  Cross-GPU xGMI transport is the same code with peers on other devices.
+Only one MI355X is available to the test runner, so 2, 4 or 8 processes share cuda:0: each
+exports its IPC buffers, maps every peer's, and runs the real kernel protocol (flags,
+double-buffered rounds, bounded waits, automatic one-shot / two-shot choice at > 2 ranks).
+Cross-GPU xGMI transport is the same code with peers on other devices.
 """
 import os
 import socket
@@ -18,6 +19,47 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _timeout_worker(rank, world, port, q):
+    """Rank 1 never joins the last all-reduce: rank 0's bounded wait expires, the kernel exits with
+    the error flag set, and the engine's per-step sync (PendingStep) raises CollectiveTimeout."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch.distributed as dist
+
+        from financial_chatbot_llm_amd.engine.model_runner import CollectiveTimeout, PendingStep
+        from financial_chatbot_llm_amd.parallel.custom_ar import CustomAllReduce
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        try:
+            ar = CustomAllReduce(None, torch.device("cuda", 0), max_bytes=1 << 20, buffer_bytes=1 << 20)
+        except RuntimeError as e:
+            q.put((rank, "SKIP", str(e)))
+            return
+        x = torch.ones(4096, dtype=torch.bfloat16, device="cuda")
+        ar.all_reduce(x)                        # a healthy round first
+        torch.cuda.synchronize()
+        ar.check()
+        dist.barrier()
+        raised = None
+        if rank == 0:
+            ar.all_reduce(x)                    # the peer never arrives
+            host = torch.zeros(3, dtype=torch.int32).pin_memory()
+            host[2:3].copy_(ar.err, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            try:
+                PendingStep(None, 2, host, ev, check_err=True).result()
+            except CollectiveTimeout as e:
+                raised = str(e)
+        dist.barrier()
+        ar.close()
+        q.put((rank, "OK", raised))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
 
 
 def _worker(rank, world, port, q):
@@ -84,18 +126,17 @@ def _worker(rank, world, port, q):
         q.put((rank, "ERR", traceback.format_exc()))
 
 
-@pytest.mark.timeout(240)
-def test_custom_oneshot_all_reduce_two_processes():
+def _run(target, world):
     env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
     assert env_keep in (None, "0")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         r, status, payload = q.get(timeout=200)
         res[r] = (status, payload)
     for p in procs:
@@ -104,8 +145,23 @@ def test_custom_oneshot_all_reduce_two_processes():
         pytest.skip(f"IPC mapping unavailable on this box: {[p for s, p in res.values() if s == 'SKIP']}")
     for r, (status, payload) in res.items():
         assert status == "OK", payload
+    return res
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_all_reduce_processes(world):
+    res = _run(_worker, world)
+    for r, (status, payload) in res.items():
         *sizes, graph, rounds = payload
         for err, err_inplace, mag in sizes:
             assert err <= 0.02 * mag + 1e-2 and err_inplace <= 0.02 * mag + 1e-2, (err, err_inplace, mag)
         assert graph[0] == graph[1]
         assert rounds[0] == rounds[1]
+
+
+@pytest.mark.timeout(120)
+def test_custom_all_reduce_missing_peer_fails_the_step():
+    res = _run(_timeout_worker, 2)
+    assert res[0][1] is not None and "missed the bounded wait" in res[0][1]
+    assert res[1][1] is None

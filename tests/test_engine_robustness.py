@@ -175,3 +175,24 @@ def test_overlap_scheduling_matches_synchronous():
         # preemption recomputes KV by prefill (fp32 summation order differs) -> allow a late flip
         assert agree == total if blocks == 64 else agree >= 0.9 * total
     assert outs[(True, 12)][2] > 0
+
+
+def test_pending_step_raises_when_the_collective_flag_is_set():
+    """The custom all-reduce's device timeout flag rides the per-step host copy (model_runner):
+    a set flag fails the step loudly instead of returning tokens sampled from stale sums."""
+    import torch
+
+    from financial_chatbot_llm_amd.engine.model_runner import CollectiveTimeout, PendingStep
+
+    class _Ev:
+        def synchronize(self):
+            pass
+
+    ok = PendingStep(None, 2, torch.tensor([7, 9, 0], dtype=torch.int32), _Ev(), check_err=True)
+    assert ok.result() == [7, 9]
+    bad = PendingStep(None, 2, torch.tensor([7, 9, 1], dtype=torch.int32), _Ev(), check_err=True)
+    import pytest
+    with pytest.raises(CollectiveTimeout):
+        bad.result()
+    # without a custom all-reduce in the group the slot is not consulted
+    assert PendingStep(None, 2, torch.tensor([7, 9, 1], dtype=torch.int32), _Ev()).result() == [7, 9]

@@ -132,7 +132,9 @@ def test_http_ingest_then_retrieve():
     emb = HashEmbedder(64)
     store = NumpyVectorStore(64)
     llm = StubLLM(decisions=[ToolCall("retrieve_transactions", {"search_query": "Groceries purchase"})], responses=["ok"])
-    svc = build_stub_services(db=seeded_db((("c9", "user-9"),)), llm=llm, store=store, embedder=emb, today_fn=lambda: TODAY)
+    from financial_chatbot_llm_amd.config import ServingConfig
+    svc = build_stub_services(db=seeded_db((("c9", "user-9"),)), llm=llm, store=store, embedder=emb, today_fn=lambda: TODAY,
+                              serving=ServingConfig(backend="stub", ingest_token="s3cret"))
     svc.db.put_user_message("c9", "groceries?", "user-9", 1)
     app = create_app(svc, start_consumer=False)
 
@@ -140,11 +142,68 @@ def test_http_ingest_then_retrieve():
         async with app.router.lifespan_context(app):
             async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t") as cl:
                 r = await cl.post("/v1/transactions", json={"documents": _docs(200)})
+                assert r.status_code == 401 and len(store.corpus) == 0                    # no token
+                r = await cl.post("/v1/transactions", json={"documents": _docs(200)},
+                                  headers={"Authorization": "Bearer wrong"})
+                assert r.status_code == 401 and len(store.corpus) == 0
+                r = await cl.post("/v1/transactions", json={"documents": _docs(200)},
+                                  headers={"Authorization": "Bearer s3cret"})
                 assert r.status_code == 200 and r.json()["ingested"] == 200 and r.json()["size"] == 200
                 r = await cl.post("/process_message", json={"conversation_id": "c9", "message": "What did I spend on groceries?",
                                                             "user_id": "user-9"})
                 assert r.json()["retrieved_transactions_count"] == 4      # user-9 owns 4 of the 200
     asyncio.run(main())
+
+
+def test_ingest_endpoint_absent_without_operator_token():
+    from financial_chatbot_llm_amd.serving import create_app
+    from financial_chatbot_llm_amd.serving.factory import build_stub_services
+    app = create_app(build_stub_services(), start_consumer=False)
+
+    async def main():
+        async with app.router.lifespan_context(app):
+            async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://t") as cl:
+                r = await cl.post("/v1/transactions", json={"documents": _docs(5)})
+                assert r.status_code in (404, 405)
+    asyncio.run(main())
+
+
+def test_ingest_takes_the_search_lock_per_batch_only():
+    """A search waiting on the retrieval lock runs between ingest batches, not after the whole
+    ingest (the lock is held per 1024-document batch)."""
+    import threading
+    emb = HashEmbedder(32)
+    store = NumpyVectorStore(32)
+    lock = threading.Lock()
+    events = []
+    orig = store.add
+
+    def add(*a, **k):
+        events.append("add")
+        return orig(*a, **k)
+    store.add = add
+    ing = CorpusIngestor(emb, store, batch_size=50, lock=lock)
+    done = threading.Event()
+
+    def searcher():
+        while not done.is_set():
+            with lock:
+                if events and events[-1] == "add":
+                    events.append("search")
+    t = threading.Thread(target=searcher)
+    t.start()
+    import time as _t
+    orig_flush = ing._flush_locked
+
+    def slow(batch):
+        orig_flush(batch)
+        _t.sleep(0.01)
+    ing._flush_locked = slow
+    ing.ingest(_docs(300))
+    done.set()
+    t.join()
+    assert events.count("add") == 6 and len(store.corpus) == 300
+    assert "search" in events[:-1]           # a search got the lock before the last batch
 
 
 @pytest.mark.gpu

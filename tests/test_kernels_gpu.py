@@ -558,3 +558,76 @@ def test_moe_grouped_fp8_with_padding_rows():
     err = (y[valid] - ref[valid]).abs()
     # e4m3 rounding-boundary flips move single rows by a few %; the aggregate matches tightly
     assert err.mean() < 0.01 * ref[valid].abs().mean() + 1e-4, (err.mean(), ref[valid].abs().mean())
+
+
+# ------------------------------------------------------------------------------------------------
+# prefill tile GEMM (gemm_prefill.hip): every epilogue vs an f32 reference of the same math
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M,N_,K", [(1, 256, 64), (255, 512, 128), (257, 768, 4096), (1000, 256, 1088),
+                                    (2304, 1024, 4096)])
+def test_prefill_gemm_bf16(M, N_, K):
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + N_)
+    x, w = rnd(M, K, gen=g), rnd(N_, K, scale=0.05, gen=g)
+    y = gemm.prefill_gemm(x.to(DEV), w.to(DEV))
+    ref = x.float() @ w.float().t()
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+    assert y.shape == (M, N_) and y.dtype == torch.bfloat16
+
+
+@pytest.mark.parametrize("M,S", [(37, 2), (600, 4), (513, 8)])
+def test_prefill_gemm_split_k_slabs(M, S):
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(S)
+    N_, K = 512, 2048
+    x, w = rnd(M, K, gen=g), rnd(N_, K, scale=0.05, gen=g)
+    P = gemm.prefill_gemm(x.to(DEV), w.to(DEV), "slabs", S)
+    assert P.shape == (S, M, N_) and P.dtype == torch.float32
+    ref = torch.einsum("smk,snk->smn", x.float().view(M, S, K // S).transpose(0, 1),
+                       w.float().view(N_, S, K // S).transpose(0, 1))
+    close(P, ref, atol=1e-3 * ref.abs().max().item(), rtol=1e-3)     # f32 slabs: no bf16 rounding
+
+
+def test_prefill_gemm_silu_and_residual_epilogues():
+    from financial_chatbot_llm_amd.ops import gemm
+    from financial_chatbot_llm_amd.ops.activation import silu_mul
+    g = torch.Generator().manual_seed(5)
+    M, F_, K = 300, 512, 1024
+    x = rnd(M, K, gen=g)
+    w = gemm.interleave16(rnd(F_, K, scale=0.05, gen=g), rnd(F_, K, scale=0.05, gen=g))
+    y = gemm.prefill_gemm(x.to(DEV), w.to(DEV), "silu")
+    ref = silu_mul((x.float() @ w.float().t()).to(torch.bfloat16), interleave16=True)
+    close(y, ref, atol=2e-2 * ref.float().abs().max().item())
+    r = rnd(M, 256, gen=g)
+    w2 = rnd(256, K, scale=0.05, gen=g)
+    y2 = gemm.prefill_gemm(x.to(DEV), w2.to(DEV), "residual", residual=r.to(DEV))
+    ref2 = x.float() @ w2.float().t() + r.float()
+    close(y2, ref2, atol=2e-2 * ref2.abs().max().item())
+
+
+@pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (333, 32, 8), (1500, 8, 1)])
+def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
+    """Fused QKV + RoPE + paged KV write == GEMM -> rope_kv_write (the unfused path), including
+    tokens with no KV slot (slot -1) and llama3-scaled RoPE at large positions."""
+    from financial_chatbot_llm_amd.ops import gemm
+    from financial_chatbot_llm_amd.ops.attention import rope_cos_sin, rope_kv_write
+    g = torch.Generator().manual_seed(M)
+    D, K = 128, 1024
+    x = rnd(M, K, gen=g).to(DEV)
+    w = rnd((Hq + 2 * Hkv) * D, K, scale=0.03, gen=g).to(DEV)
+    cs = rope_cos_sin(D, 8192, 500000.0, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192},
+                      device=DEV)
+    pos = torch.randint(0, 8192, (M,), generator=g, dtype=torch.int32).to(DEV)
+    nb = (M + KV_BS - 1) // KV_BS + 1
+    slots = torch.randperm(nb * KV_BS, generator=g)[:M].to(torch.int32)
+    slots[::5] = -1
+    slots = slots.to(DEV)
+    kc = [torch.zeros((nb, Hkv, KV_BS * D), dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    vc = [torch.zeros((nb, Hkv, KV_BS * D), dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    q_ref = rope_kv_write((x.float() @ w.float().t()).to(torch.bfloat16), pos, cs, slots, kc[0], vc[0], Hq, Hkv, D)
+    q = gemm.prefill_qkv_rope(x, w, pos, cs, slots, kc[1], vc[1], Hq, Hkv)
+    scale = q_ref.float().abs().max().item()
+    close(q, q_ref, atol=2e-2 * scale)
+    close(kc[1], kc[0], atol=2e-2 * scale)
+    close(vc[1], vc[0], atol=2e-2 * scale)
