@@ -69,6 +69,22 @@ union Frag {
   bf16x8 v;
 };
 
+// Two 4-column groups of bf16 accumulators, lo = columns 16f + 4g .. +3 and hi = 16(f+1) + 4g .. +3
+// in lane row g (= lane >> 4) -> the 8 CONSECUTIVE columns 16f + 8*(g>>1) + 16*(g&1) .. +7 of this
+// lane, via v_permlane16_swap (odd lane rows of vdst <-> even lane rows of vsrc): one 16-B store
+// instead of two 8-B ones (the epilogue store tail is issue-bound).
+__device__ __forceinline__ uint4 pair16(bf16x4 lo, bf16x4 hi) {
+  union {
+    bf16x4 v;
+    uint2 u;
+  } a, b;
+  a.v = lo;
+  b.v = hi;
+  const auto x = __builtin_amdgcn_permlane16_swap(a.u.x, b.u.x, false, false);
+  const auto y = __builtin_amdgcn_permlane16_swap(a.u.y, b.u.y, false, false);
+  return make_uint4(x[0], y[0], x[1], y[1]);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -294,6 +310,10 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
   if (wa == 0) bar();
 
   // ---- epilogue: lane holds Y[m0 + wb*64 + 16t + col][n0 + wa*128 + 16f + 4g + r], r = 0..3 ----
+  // bf16 outputs leave as 16-B stores: pair16 swaps 8-B halves between lane rows g and g^1 (same
+  // token row m, so a lane masked off by m >= M always has a masked swap partner), after which a
+  // lane holds 8 consecutive columns at lane_off + 16*(group pair index)
+  const int lane_off = 8 * (g >> 1) + 16 * (g & 1);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int m = m0 + wb * 64 + t * 16 + col;
@@ -337,38 +357,41 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
           for (int r = 0; r < 4; ++r) vb[v_index(off, f * 16 + 4 * g + r, D)] = (bf16)acc[f][t][r];
       }
     } else if constexpr (EPI == EPI_SILU) {
+      // row group G (16 W rows) is gate (G even) / up (G odd) of output columns 16*(G/2)..+15: the
+      // wave's 8 groups give 4 output groups of 16 columns, col0 + 16p
+      const int col0 = ((n0 + wa * 128) >> 5) * 16;
+      bf16x4 o[4];
 #pragma unroll
-      for (int f = 0; f < 8; f += 2) {
-        // row group G (16 W rows) is gate (G even) / up (G odd) of output columns 16*(G/2)..+15
-        const int G = (n0 + wa * 128 + f * 16) >> 4;
-        bf16x4 o;
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           // same roundings as GEMM -> bf16 gate|up -> silu_mul (HF: silu in the activation dtype)
-          const float gt = (float)(bf16)acc[f][t][r], up = (float)(bf16)acc[f + 1][t][r];
-          o[r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
+          const float gt = (float)(bf16)acc[2 * q][t][r], up = (float)(bf16)acc[2 * q + 1][t][r];
+          o[q][r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
         }
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(Y) + (long)m * ldy + (G >> 1) * 16 + 4 * g) = o;
-      }
+      bf16* y = static_cast<bf16*>(Y) + (long)m * ldy + col0 + lane_off;
+#pragma unroll
+      for (int q = 0; q < 4; q += 2) *reinterpret_cast<uint4*>(y + 16 * q) = pair16(o[q], o[q + 1]);
     } else if constexpr (EPI == EPI_SLAB) {
       float* P = static_cast<float*>(Y) + (long)s * M * N + (long)m * N;
 #pragma unroll
       for (int f = 0; f < 8; ++f) *reinterpret_cast<f32x4*>(P + n0 + wa * 128 + f * 16 + 4 * g) = acc[f][t];
     } else {
-      bf16* y = static_cast<bf16*>(Y) + (long)m * ldy;
+      bf16* y = static_cast<bf16*>(Y) + (long)m * ldy + n0 + wa * 128 + lane_off;
 #pragma unroll
-      for (int f = 0; f < 8; ++f) {
-        const int n = n0 + wa * 128 + f * 16 + 4 * g;
-        bf16x4 o;
+      for (int f = 0; f < 8; f += 2) {
+        bf16x4 lo, hi;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lo[r] = (bf16)acc[f][t][r], hi[r] = (bf16)acc[f + 1][t][r];
+        Pack8 v;
+        v.u = pair16(lo, hi);
         if constexpr (EPI == EPI_RESID) {
-          const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long)m * ldr + n);
+          Pack8 rr;
+          rr.u = *reinterpret_cast<const uint4*>(R + (long)m * ldr + n0 + wa * 128 + lane_off + 16 * f);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)(bf16)acc[f][t][r] + (float)rr[r]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[f][t][r];
+          for (int j = 0; j < 8; ++j) v.e[j] = (bf16)((float)v.e[j] + (float)rr.e[j]);
         }
-        *reinterpret_cast<bf16x4*>(y + n) = o;
+        *reinterpret_cast<uint4*>(y + 16 * f) = v.u;
       }
     }
   }
