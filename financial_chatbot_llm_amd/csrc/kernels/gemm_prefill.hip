@@ -8,6 +8,8 @@
 //             consumer's own row pass (residual-add + RMSNorm, RoPE + KV write) -- fills the
 //             256 CUs at small M without an extra reduce launch
 //   EPI_RESID Y bf16 = bf16(acc) + R (residual add fused, rounded like GEMM-then-add)
+//   EPI_BIAS / EPI_BIAS_GELU  Y bf16 = bf16(acc + bias[n]) [-> exact-erf GELU], R = the bias: the
+//             bge encoder's QKV / O / fc2 and its GELU-MLP fc1 (no separate GELU pass)
 //   EPI_ROPE  the fused QKV projection (K3+K4+K5): a wave's 128 output columns are exactly one
 //             head, so the rotate-half RoPE pair (d, d+64) sits in one lane (accumulators f, f+4);
 //             q heads -> rotated q [M, Hq, 128]; k heads -> rotated, v heads -> as is, both
@@ -50,7 +52,7 @@ constexpr int HALF = 128 * 128;      // half-tile: 128 rows x 64 bf16 = 16 KiB
 constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
 constexpr int GM = 4;                // token tiles per L2 group
 enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
-enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4 };
+enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6 };
 
 struct RopeArgs {
   const int* positions;   // [M]
@@ -381,8 +383,23 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
 #pragma unroll
       for (int f = 0; f < 8; f += 2) {
         bf16x4 lo, hi;
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+          const int n = n0 + wa * 128 + f * 16 + 4 * g;
+          const bf16x4 b0 = *reinterpret_cast<const bf16x4*>(R + n), b1 = *reinterpret_cast<const bf16x4*>(R + n + 16);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) lo[r] = (bf16)acc[f][t][r], hi[r] = (bf16)acc[f + 1][t][r];
+          for (int r = 0; r < 4; ++r) {
+            // rounded where GEMM-with-bias -> bf16 -> GELU rounds (F.linear(x, w, b) then gelu)
+            float u0 = (float)(bf16)(acc[f][t][r] + (float)b0[r]), u1 = (float)(bf16)(acc[f + 1][t][r] + (float)b1[r]);
+            if constexpr (EPI == EPI_BIAS_GELU) {
+              u0 = 0.5f * u0 * (1.f + erff(u0 * 0.70710678118654752f));
+              u1 = 0.5f * u1 * (1.f + erff(u1 * 0.70710678118654752f));
+            }
+            lo[r] = (bf16)u0, hi[r] = (bf16)u1;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lo[r] = (bf16)acc[f][t][r], hi[r] = (bf16)acc[f + 1][t][r];
+        }
         Pack8 v;
         v.u = pair16(lo, hi);
         if constexpr (EPI == EPI_RESID) {
@@ -409,14 +426,17 @@ static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
 
 // Contract (checked): N % 256 == 0, K % (64*S) == 0, ldx % 8 == 0, rows 16-B aligned; EPI_SILU
-// needs S == 1 and ldy % 4 == 0 (Y is [M, N/2]); EPI_SLAB writes P [S, M, N] f32 (ldy unused);
-// EPI_RESID needs R (row stride ldr, ldr % 4 == 0) and S == 1.
+// needs S == 1 and ldy % 8 == 0 (Y is [M, N/2]); EPI_SLAB writes P [S, M, N] f32 (ldy unused);
+// EPI_RESID needs R (row stride ldr, ldr % 8 == 0) and S == 1; EPI_BIAS(_GELU) take the bias [N]
+// as R.
 PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, void* Y, int ldy, const void* R,
                                  int ldr, int M, int N, int S, int epi, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (N % TN || S < 1 || K % (BK * S) || ldx % 8 || epi < 0 || epi > 3) return (int)hipErrorInvalidValue;
-  if (epi != EPI_SLAB && (S != 1 || ldy % 4)) return (int)hipErrorInvalidValue;
-  if (epi == EPI_RESID && (!R || ldr % 4)) return (int)hipErrorInvalidValue;
+  if (N % TN || S < 1 || K % (BK * S) || ldx % 8 || epi < 0 || epi > 6 || epi == EPI_ROPE)
+    return (int)hipErrorInvalidValue;
+  if (epi != EPI_SLAB && (S != 1 || ldy % 8)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!R || ldr % 8)) return (int)hipErrorInvalidValue;
+  if ((epi == EPI_BIAS || epi == EPI_BIAS_GELU) && !R) return (int)hipErrorInvalidValue;
   if ((long)((M + TM - 1) / TM) * (N / TN) * S > (1L << 30)) return (int)hipErrorInvalidValue;
   const dim3 grid = grid_for(M, N, S);
   const RopeArgs ra{};
@@ -424,6 +444,8 @@ PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, v
     case EPI_BF16: launch<EPI_BF16>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
     case EPI_SILU: launch<EPI_SILU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
     case EPI_SLAB: launch<EPI_SLAB>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    case EPI_BIAS: launch<EPI_BIAS>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    case EPI_BIAS_GELU: launch<EPI_BIAS_GELU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
     default: launch<EPI_RESID>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra);
   }
   return (int)hipGetLastError();

@@ -164,6 +164,57 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(const bf16* __restrict_
   }
 }
 
+// One WAVE per row for the encoder's H = 768 (bge-base) and other H % 256 == 0 up to 4096: each
+// lane holds H/64 values as C4 8-byte chunks (4 bf16, at chunk lane + 64c), two wave reductions
+// (mean, variance) and no LDS or block barrier.  The block-per-row kernel above spends most of
+// a 128-thread block on two __syncthreads reductions at this width.
+template <int C4, bool ADD_RES>
+__global__ void __launch_bounds__(256) layernorm_wave_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                             const bf16* __restrict__ g, const bf16* __restrict__ b,
+                                                             bf16* __restrict__ y, int T, int H, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const bf16x4* xr = reinterpret_cast<const bf16x4*>(x + (size_t)row * H);
+  const bf16x4* rr = reinterpret_cast<const bf16x4*>(res + (size_t)row * H);
+  bf16x4 xv[C4], rv[C4];
+#pragma unroll
+  for (int c = 0; c < C4; ++c) {
+    xv[c] = xr[lane + 64 * c];
+    if (ADD_RES) rv[c] = rr[lane + 64 * c];
+  }
+  float v[C4][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < C4; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[c][i] = (float)xv[c][i] + (ADD_RES ? (float)rv[c][i] : 0.f);
+      s += v[c][i];
+    }
+  const float mu = wave_sum(s) / (float)H;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < C4; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = v[c][i] - mu;
+      sq += d * d;
+    }
+  const float inv = rsqrtf(wave_sum(sq) / (float)H + eps);
+  const bf16x4* gr = reinterpret_cast<const bf16x4*>(g);
+  const bf16x4* br = reinterpret_cast<const bf16x4*>(b);
+  bf16x4* yr = reinterpret_cast<bf16x4*>(y + (size_t)row * H);
+#pragma unroll
+  for (int c = 0; c < C4; ++c) {
+    const bf16x4 gg = gr[lane + 64 * c], bb = br[lane + 64 * c];
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (bf16)((v[c][i] - mu) * inv * (float)gg[i] + (float)bb[i]);
+    yr[lane + 64 * c] = o;
+  }
+}
+
 static inline void pick_geometry(int H, int* threads, int* cpt) {
   const int nchunk = H / 8;
   int t = nchunk >= 256 ? 256 : ((nchunk + 63) / 64) * 64;
@@ -245,6 +296,21 @@ PENNY_API int penny_layernorm(const void* x, const void* res, const void* g, con
                               float eps, int add_residual, hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8) return (int)hipErrorInvalidValue;
+  if (H % 256 == 0 && H <= 4096) {
+    const dim3 grid((T + 3) / 4);
+#define WAVE_LN(C4_)                                                                                           \
+  if (H == 256 * C4_) {                                                                                        \
+    if (add_residual)                                                                                          \
+      hipLaunchKernelGGL((layernorm_wave_kernel<C4_, true>), grid, dim3(256), 0, stream, (const bf16*)x,       \
+                         (const bf16*)res, (const bf16*)g, (const bf16*)b, (bf16*)y, T, H, eps);               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((layernorm_wave_kernel<C4_, false>), grid, dim3(256), 0, stream, (const bf16*)x,      \
+                         (const bf16*)res, (const bf16*)g, (const bf16*)b, (bf16*)y, T, H, eps);               \
+    PENNY_RETURN_LAUNCH();                                                                                     \
+  }
+    WAVE_LN(1) WAVE_LN(2) WAVE_LN(3) WAVE_LN(4) WAVE_LN(8) WAVE_LN(16)
+#undef WAVE_LN
+  }
   int threads, cpt;
   pick_geometry(H, &threads, &cpt);
   if (add_residual) {

@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.attention import KV_BS
+from ..ops.gemm import linear_bias
 from .common import random_tensor
 from .configs import ModelConfig
 
@@ -103,13 +104,13 @@ class BertEncoder:
         scale = 1.0 / math.sqrt(self.D)
         for i in range(c.num_layers):
             p = f"layers.{i}."
-            qkv = F.linear(x, w[p + "qkv"], w[p + "qkv_b"])
+            qkv = linear_bias(x, w[p + "qkv"], w[p + "qkv_b"])
             q = ops.rope_kv_write(qkv, pos_t, None, slots_t, kc, vc, self.nh, self.nh, self.D, apply_rope=False)
             a = ops.prefill(q, cu_t, lens_t, bt, kc, vc, scale, causal=False, max_q_len=max(lens))
-            o = F.linear(a.view(T, self.H), w[p + "o"], w[p + "o_b"])
+            o = linear_bias(a.view(T, self.H), w[p + "o"], w[p + "o_b"])
             x = ops.layer_norm(o, w[p + "ln1_g"], w[p + "ln1_b"], c.norm_eps, residual=x)
-            h = ops.gelu_(F.linear(x, w[p + "fc1"], w[p + "fc1_b"]))
-            y = F.linear(h, w[p + "fc2"], w[p + "fc2_b"])
+            h = linear_bias(x, w[p + "fc1"], w[p + "fc1_b"], gelu=True)      # bias + GELU fused
+            y = linear_bias(h, w[p + "fc2"], w[p + "fc2_b"])
             x = ops.layer_norm(y, w[p + "ln2_g"], w[p + "ln2_b"], c.norm_eps, residual=x)
         return x, cu
 

@@ -298,7 +298,7 @@ def splitk_reduce(P: torch.Tensor, residual: Optional[torch.Tensor] = None,
 # ----------------------------------------------------------------------------------------------
 # Prefill GEMM (M > 256 token rows): 256x256-tile MFMA kernel with fused epilogues
 # ----------------------------------------------------------------------------------------------
-PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3}
+PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_gelu": 6}
 
 
 # Which path each Llama-3-8B projection takes at a prefill step of M rows (M > 256), measured with
@@ -320,7 +320,8 @@ def _default_choice(M: int, N_: int, K: int, epilogue: Optional[str]) -> str:
     """Unmeasured shapes: the tile kernel once its 256x256 tiles cover the 256 CUs (one tile
     alone runs ~80 us at K = 4096, so fewer tiles lose to the library's smaller ones)."""
     tiles = -(-M // 256) * (N_ // 256)
-    return "hip" if tiles >= 224 or (epilogue == "silu" and tiles >= 112) else "lib"
+    # a fused activation also saves the library path's separate pass over the [M, N] output
+    return "hip" if tiles >= 224 or (epilogue in ("silu", "bias_gelu") and tiles >= 112) else "lib"
 
 
 def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slabs: bool = False) -> str:
@@ -368,19 +369,23 @@ def prefill_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None, S: int = 1,
-                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                 bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ w.T on the hand-written 256x256 MFMA tile kernel (``gemm_prefill.hip``).
 
     ``epilogue``: None -> bf16 [M, N]; "silu" -> silu(gate)*up bf16 [M, N/2] from the
     interleave16 gate|up weight; "slabs" -> f32 split-K partials [S, M, N]; "residual" -> bf16
-    x @ w.T + residual.  The torch path (CPU) computes the same math in f32."""
+    x @ w.T + residual; "bias" / "bias_gelu" -> bf16(x @ w.T + bias) [-> exact GELU].  The torch
+    path (CPU) computes the same math in f32."""
     M, K = x.shape
     N_ = w.shape[0]
     if not N.use_native(x):
         if epilogue == "slabs":
             xs = x.float().view(M, S, K // S).transpose(0, 1)
             return torch.einsum("smk,snk->smn", xs, w.float().view(N_, S, K // S).transpose(0, 1))
-        y = F.linear(x.float(), w.float()).to(x.dtype)
+        y = F.linear(x.float(), w.float(), bias.float() if bias is not None else None).to(x.dtype)
+        if epilogue == "bias_gelu":
+            return F.gelu(y.float()).to(x.dtype)
         if epilogue == "silu":
             return silu_mul(y, interleave16=True)
         if epilogue == "residual":
@@ -394,8 +399,24 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
         cols = N_ // 2 if epilogue == "silu" else N_
         y = out if out is not None else torch.empty((M, cols), dtype=x.dtype, device=x.device)
         ldy = y.stride(0)
-    N.call("penny_gemm_prefill", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), ldy, N.ptr(residual),
+    R = bias if epilogue in ("bias", "bias_gelu") else residual
+    N.call("penny_gemm_prefill", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), ldy, N.ptr(R),
            residual.stride(0) if residual is not None else 0, M, N_, S, PREFILL_EPI[epilogue], N.stream())
+    return y
+
+
+def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = False) -> torch.Tensor:
+    """Encoder projection bf16(x @ w.T + b) [-> exact GELU]: the tile kernel with the bias (+GELU)
+    epilogue once its tiles fill the chip (bulk ingest), hipBLASLt's bias GEMM + the HIP GELU pass
+    for query-size batches (``PENNY_PREFILL_GEMM=0``: always the library)."""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if M > 256 and prefill_ok(x, w) and prefill_choice(M, N_, K, "bias_gelu" if gelu else "bias") == "hip":
+        return prefill_gemm(x, w, "bias_gelu" if gelu else "bias", bias=b)
+    y = F.linear(x, w, b)
+    if gelu:
+        from .activation import gelu_
+        return gelu_(y)
     return y
 
 

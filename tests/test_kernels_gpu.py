@@ -48,11 +48,14 @@ def test_rmsnorm(T, H):
     close(y2, y2_ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("T,H", [(3, 768), (50, 1024)])
-def test_layernorm(T, H):
+@pytest.mark.parametrize("T,H", [(3, 768), (50, 1024), (4099, 768), (7, 200), (9, 4096)])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_layernorm(T, H, with_res):
+    """wave-per-row kernel (H % 256 == 0) and the block kernel (other H) vs the f32 reference"""
     torch.manual_seed(1)
     x, r, g, b = rnd(T, H), rnd(T, H), rnd(H) * 0.1 + 1, rnd(H) * 0.1
-    close(ops.layer_norm(x.to(DEV), g.to(DEV), b.to(DEV), 1e-12, residual=r.to(DEV)),
+    r = r if with_res else None
+    close(ops.layer_norm(x.to(DEV), g.to(DEV), b.to(DEV), 1e-12, residual=r.to(DEV) if with_res else None),
           ops.layer_norm(x, g, b, 1e-12, residual=r), atol=3e-2)
 
 
@@ -631,3 +634,30 @@ def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
     close(q, q_ref, atol=2e-2 * scale)
     close(kc[1], kc[0], atol=2e-2 * scale)
     close(vc[1], vc[0], atol=2e-2 * scale)
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+def test_prefill_gemm_bias_gelu_epilogue(gelu):
+    """bge encoder projections: bf16(x @ w.T + b) [-> exact GELU] fused in the tile kernel."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(11)
+    M, N_, K = 1025, 768, 768
+    x, w, b = rnd(M, K, gen=g), rnd(N_, K, scale=0.05, gen=g), rnd(N_, scale=0.5, gen=g)
+    y = gemm.prefill_gemm(x.to(DEV), w.to(DEV), "bias_gelu" if gelu else "bias", bias=b.to(DEV))
+    ref = x.float() @ w.float().t() + b.float()
+    if gelu:
+        ref = torch.nn.functional.gelu(ref)
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+
+
+def test_bge_encoder_bulk_tile_kernels_match_library_path(monkeypatch):
+    """bge-base bulk batch (~24k tokens: the tile-kernel GEMMs with bias / GELU epilogues) vs the
+    same weights through hipBLASLt + the separate GELU pass (PENNY_PREFILL_GEMM=0)."""
+    from financial_chatbot_llm_amd.retrieval import BgeEmbedder
+    emb = BgeEmbedder("bge-base-en", device=DEV)
+    texts = [f"grocery purchase number {i} at store {i % 17} on the {i % 28 + 1}th" for i in range(2000)]
+    a = emb.embed(texts).float().cpu()
+    monkeypatch.setenv("PENNY_PREFILL_GEMM", "0")
+    b = emb.embed(texts).float().cpu()
+    cos = (a * b).sum(-1) / (a.norm(dim=-1) * b.norm(dim=-1))
+    assert float(cos.min()) > 0.995, float(cos.min())
