@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--no-tools", action="store_true",
                     help="BASELINE config 2: single-turn chat without tools (legacy llm_service.py chain); "
                          "no decide step, no retrieval")
+    ap.add_argument("--decide-always-limit", action="store_true",
+                    help="scripted decide always sends num_transactions=20 (round-2 workload); default follows "
+                         "the reference few-shot: time-window queries send no limit (10000 -> token clamp)")
     ap.add_argument("--no-jump-forward", action="store_true",
                     help="decode grammar-forced tool-call tokens one step each (A/B of jump-forward decoding)")
     ap.add_argument("--arrival", default="closed", choices=["closed", "wave"],
@@ -185,6 +188,8 @@ def main(argv=None) -> int:
     if args.max_batched_tokens is None:
         args.max_batched_tokens = 16384 if args.model.startswith("mixtral") else 4096
     os.environ.setdefault("LOG_LEVEL", "WARNING")
+    if args.decide_always_limit:
+        os.environ["PENNY_DECIDE_ALWAYS_LIMIT"] = "1"
     import torch
     import torch.distributed as dist
 
@@ -217,6 +222,8 @@ def main(argv=None) -> int:
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
                        "tool_steps": 0 if args.no_tools else args.tool_steps,
                        "decide_decoding": "tool-call grammar, jump-forward" if not args.no_jump_forward else "token by token",
+                       "decide_limits": ("num_transactions=20 on every call" if args.decide_always_limit else
+                                         "reference few-shot: time windows send no limit (10000 -> token clamp)"),
                        "agent": "single-chain chat (no tools)" if args.no_tools else "tool-calling RAG agent",
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
                        "parallelism": f"dp{ps.world_size}"},

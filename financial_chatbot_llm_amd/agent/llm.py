@@ -49,25 +49,37 @@ class LLMBackend:
 _RETRIEVAL_CUES = re.compile(
     r"\b(spen[dt]|spending|transactions?|purchases?|bought|paid|charges?|groceries|grocery|"
     r"subscriptions?|expenses?|bills?|merchant|last (week|month)|yesterday|days? ago)\b", re.I)
-_DAYS = re.compile(r"\b(\d+)\s+days?\b", re.I)
+_DAYS = re.compile(r"\b(\d+|one|two|three|four|five|six|seven|eight|nine|ten|fourteen|thirty)\s+days?\b", re.I)
+_NUM_WORDS = {"one": 1, "two": 2, "three": 3, "four": 4, "five": 5, "six": 6, "seven": 7, "eight": 8, "nine": 9,
+              "ten": 10, "fourteen": 14, "thirty": 30}
 
 
-def scripted_decision(user_query: str) -> Optional[ToolCall]:
-    """Heuristic tool decision mirroring the few-shot rules of ``tool_prompt.txt``."""
+def scripted_decision(user_query: str, always_limit: bool = False) -> Optional[ToolCall]:
+    """Heuristic tool decision mirroring the few-shot of ``tool_prompt.txt`` (reference
+    ``tool_prompt.txt:15-23``): a topical query carries ``num_transactions: 20``; a time-window
+    query ("two days ago") carries ``time_period_days`` and NO ``num_transactions``, so the tool's
+    limit falls back to 10000 (``tools/qdrant_tool.py:145``) and the agent's transaction-token
+    clamp decides how much of the window reaches the respond prompt.  ``always_limit=True`` keeps
+    ``num_transactions: 20`` on every call (the round-2 benchmark workload)."""
     if not _RETRIEVAL_CUES.search(user_query):
         return None
-    args: Dict[str, Any] = {"search_query": user_query.strip().rstrip("?.!") or "recent transactions",
-                            "num_transactions": 20}
+    args: Dict[str, Any] = {"search_query": user_query.strip().rstrip("?.!") or "recent transactions"}
     m = _DAYS.search(user_query)
     low = user_query.lower()
+    days = None
     if m:
-        args["time_period_days"] = int(m.group(1))
+        w = m.group(1).lower()
+        days = int(w) if w.isdigit() else _NUM_WORDS[w]
     elif "yesterday" in low:
-        args["time_period_days"] = 1
+        days = 1
     elif "last week" in low:
-        args["time_period_days"] = 7
+        days = 7
     elif "last month" in low:
-        args["time_period_days"] = 30
+        days = 30
+    if days is None or always_limit:
+        args["num_transactions"] = 20
+    if days is not None:
+        args["time_period_days"] = days
     return ToolCall(name="retrieve_transactions", args=args, id="call_0")
 
 

@@ -19,6 +19,7 @@ from __future__ import annotations
 import asyncio
 import datetime as _dt
 import json
+import os
 import random
 import time
 from dataclasses import dataclass, field
@@ -200,7 +201,10 @@ def decide_script(messages, tools) -> str:
         if PLOT_CALL.name in names and f"[{PLOT_CALL.name}]" not in system and not nothing:
             return format_tool_call(PLOT_CALL)
         return "No tool call"
-    call = scripted_decision(messages[-1].content) if messages else None
+    # PENNY_DECIDE_ALWAYS_LIMIT=1 (bench.py --decide-always-limit): num_transactions on every call,
+    # the round-2 workload; default: the reference few-shot (time windows carry no limit)
+    always = os.environ.get("PENNY_DECIDE_ALWAYS_LIMIT", "0") == "1"
+    call = scripted_decision(messages[-1].content, always_limit=always) if messages else None
     if call is None or not any(t.name == call.name for t in tools):
         return "No tool call"
     return format_tool_call(call)

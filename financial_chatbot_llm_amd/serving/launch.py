@@ -72,9 +72,11 @@ def build_leader_services(args, engine, device):
     if args.no_tools or not serving.tools:
         agent = LLMService(llm, temperature=serving.temperature, max_response_tokens=serving.max_response_tokens)
     else:
+        from .factory import retrieval_limit_tokens
         agent = LLMAgent(llm, make_retrieval_tool(retrieval), extra_tools=[make_plot_tool()],
                          temperature=serving.temperature, max_response_tokens=serving.max_response_tokens,
-                         max_decide_tokens=serving.max_decide_tokens, max_tool_steps=args.tool_steps)
+                         max_decide_tokens=serving.max_decide_tokens, max_tool_steps=args.tool_steps,
+                         max_transaction_tokens=retrieval_limit_tokens())     # PENNY_MAX_TRANSACTION_TOKENS
     broker = InMemoryBroker() if args.smoke else None
     return Services(db=Database(uri="" if args.smoke else None), kafka=KafkaClient(broker=broker), agent=agent,
                     engine=engine, retrieval=retrieval, serving=serving)

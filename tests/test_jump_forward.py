@@ -42,7 +42,7 @@ def test_grammar_forces_skeleton_only():
 
 
 def test_jump_mask_marks_forced_tokens_of_a_real_call():
-    text = format_tool_call(scripted_decision("What did I spend on groceries last month?"))
+    text = format_tool_call(scripted_decision("What did I spend on groceries last month?", always_limit=True))
     ids = TOK.encode(text, allow_special=False) + [EOT]
     m = jump_mask(ids, TOK.decode, ToolCallGrammar([RET]), EOT)
     assert not m[0] and m[-1]                      # first token sampled, final EOT forced
@@ -50,6 +50,18 @@ def test_jump_mask_marks_forced_tokens_of_a_real_call():
     assert "What" in free and "20" in free and "30" in free               # values stay free
     assert 0.4 < sum(m) / len(m) < 0.75
     assert parse_tool_calls(TOK.decode(ids), [RET])[0].args["num_transactions"] == 20
+
+
+def test_scripted_decide_follows_the_reference_few_shot():
+    """tool_prompt.txt:15-23: a topical query carries num_transactions 20; a time-window query
+    carries time_period_days and no num_transactions (limit -> 10000, qdrant_tool.py:145)."""
+    topical = scripted_decision("What did I spend on groceries?")
+    assert topical.args == {"search_query": "What did I spend on groceries", "num_transactions": 20}
+    window = scripted_decision("How much did I spend two days ago?")
+    assert window.args["time_period_days"] == 2 and "num_transactions" not in window.args
+    assert scripted_decision("How should I invest for retirement?") is None
+    legacy = scripted_decision("How much did I spend last week?", always_limit=True)
+    assert legacy.args["num_transactions"] == 20 and legacy.args["time_period_days"] == 7
 
 
 def _run(params_list, prompts, mode):
