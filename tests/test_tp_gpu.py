@@ -1,5 +1,7 @@
 """Tensor parallelism on the GPU kernels: 2 ranks sharing one MI355X (gloo carries the
-collectives, as the 1-GPU box allows), TP=2 against TP=1 with the HIP kernel library.
+collectives, as the 1-GPU box allows), TP=2 against TP=1 with the HIP kernel library: prefill
+logits compared as numbers and every decoded token checked against the TP=1 argmax of its
+prefix (8-rank shapes: test_world8_gpu.py).
 
 ``PENNY_SPLITK=force`` puts every decode-size projection of the tiny model on the split-K path, so
 the column-parallel QKV shard's f32 slabs feed the RoPE/KV-write pass under TP (the path Llama-3-70B
@@ -49,6 +51,18 @@ def _run(tp: int, rank: int = 0, graphs: bool = False):
     return out
 
 
+def _model(tp_rank=0, tp_size=1):
+    from financial_chatbot_llm_amd.models.configs import get_model_config
+    from financial_chatbot_llm_amd.models.llama import LlamaModel
+    return LlamaModel(get_model_config("llama-tiny-tp"), device="cuda", tp_rank=tp_rank,
+                      tp_size=tp_size).init_random(seed=11, std=0.05)
+
+
+def _logits(tp_rank=0, tp_size=1, ids=None):
+    from test_world8_gpu import _prefill_logits
+    return _prefill_logits(_model(tp_rank, tp_size), ids or PROMPTS[2])
+
+
 def _worker(rank, world, port, q, graphs=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), PENNY_SPLITK="force", PENNY_TP_OVERLAP_MIN_ROWS="64")
@@ -56,12 +70,13 @@ def _worker(rank, world, port, q, graphs=False):
         from financial_chatbot_llm_amd.parallel import comm
         from financial_chatbot_llm_amd.parallel.dist import init_distributed, shutdown
         init_distributed(tp_size=world, backend="gloo", device_type="cuda")
+        logits = _logits(rank, world)
         out = _run(world, rank, graphs)
         if graphs:   # the decode graphs ran on the custom one-shot AR + all-gather kernels
             assert comm._CUSTOM_AR is not None and int(comm._CUSTOM_AR.counter.item()) > 0
             comm._CUSTOM_AR.check()
         torch.cuda.synchronize()
-        q.put((rank, out))
+        q.put((rank, (out, logits.cpu())))
         shutdown()
     except Exception:  # noqa: BLE001
         import traceback
@@ -86,6 +101,16 @@ def test_tp2_gpu_matches_tp1(monkeypatch, graphs):
         p.join(timeout=60)
     for r, v in res.items():
         assert not (isinstance(v, str) and v.startswith("ERR")), v
-    got = res[0]
-    agree = sum(a == b for g, w in zip(got, ref) for a, b in zip(g, w)) / sum(len(w) for w in ref)
-    assert agree >= 0.85, (got, ref)    # bf16: TP partial sums round in a different order
+    got, logits2 = res[0]
+    from test_world8_gpu import _assert_logits_close
+    # numbers, not tokens: the TP=2 prefill logits match TP=1 within bf16 noise (a shard bug that
+    # corrupts a few heads moves them far beyond it), and every TP=2 greedy token is, within the
+    # same noise, the TP=1 argmax of its teacher-forced prefix
+    _assert_logits_close(logits2, _logits().cpu())
+    ref_model = _model()
+    from test_world8_gpu import _prefill_logits
+    for prompt, toks in zip(PROMPTS, got):
+        for j, t in enumerate(toks):
+            lg = _prefill_logits(ref_model, prompt + toks[:j])[-1].cpu()
+            assert float(lg.max() - lg[t]) <= 0.03 * float(lg.abs().max()), (j, t, int(lg.argmax()))
+    assert len(got) == len(ref) and all(len(g) == len(w) for g, w in zip(got, ref))
