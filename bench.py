@@ -107,7 +107,9 @@ async def run(args, ps):
                         graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype,
                         # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
                         kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
-                        sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)))
+                        sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)),
+                        step_time_target_ms=float(os.environ.get("PENNY_STEP_TIME_TARGET_MS",
+                                                                 EngineConfig.step_time_target_ms)))
     if args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
         from financial_chatbot_llm_amd.engine.process_engine import ProcessAsyncEngine
         engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device() if on_gpu else None)

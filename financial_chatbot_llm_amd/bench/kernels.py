@@ -527,8 +527,6 @@ def bench_moe_prefill(dev) -> List[Dict]:
     for T in (512, 1024, 2048, 4096, 8192, 16384):
         h = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
         logits = (h @ router.t()).contiguous()
-        dev_us = timeit(lambda: moe.moe_prefill_fp8(h, logits, t13, s13, t2, s2, K), iters=5)
-
         def loop():
             topw, topi = moe.topk_softmax(logits, K)
             order, offsets, tok_idx, tok_w = moe.route(topi, topw, E)
@@ -545,14 +543,20 @@ def bench_moe_prefill(dev) -> List[Dict]:
                     ys[a:b] = torch._scaled_mm(aq, q2[e].t(), scale_a=asc[:, None], scale_b=s2[e][None, :],
                                                out_dtype=torch.bfloat16)
             return moe.combine_weighted(ys, order, tok_w, T, K)
-        loop_us = timeit(loop, iters=5)
+        ts = interleaved({"device": lambda: moe.moe_prefill_fp8(h, logits, t13, s13, t2, s2, K),
+                          "tiles": lambda: moe.moe_prefill_fp8_tiles(h, logits, q13, s13, q2, s2, K),
+                          "loop": loop}, rounds=5, iters=3)
         a = moe.moe_prefill_fp8(h, logits, t13, s13, t2, s2, K).float()
+        c = moe.moe_prefill_fp8_tiles(h, logits, q13, s13, q2, s2, K).float()
         b = loop().float()
         flops = 2 * T * K * 3 * H * F_
-        out.append({"op": "moe_prefill", "T": T, "device_fp8_us": round(dev_us, 1),
-                    "device_TFLOPs": round(flops / dev_us / 1e6, 1), "hipblaslt_fp8_loop_us": round(loop_us, 1),
-                    "loop_TFLOPs": round(flops / loop_us / 1e6, 1),
-                    "rel_diff": round(float((a - b).abs().max() / b.abs().max()), 4)})
+        out.append({"op": "moe_prefill", "T": T, "device_fp8_us": round(ts["device"], 1),
+                    "device_TFLOPs": round(flops / ts["device"] / 1e6, 1),
+                    "tiles_fp8_us": round(ts["tiles"], 1), "tiles_TFLOPs": round(flops / ts["tiles"] / 1e6, 1),
+                    "hipblaslt_fp8_loop_us": round(ts["loop"], 1), "loop_TFLOPs": round(flops / ts["loop"] / 1e6, 1),
+                    "rel_diff_device": round(float((a - b).abs().max() / b.abs().max()), 4),
+                    "rel_diff_tiles": round(float((c - b).abs().max() / b.abs().max()), 4)})
+        print(json.dumps(out[-1]), flush=True)
     return out
 
 

@@ -122,6 +122,11 @@ class EngineConfig:
     max_model_len: int = 8192
     step_token_quantum: int = 256           # step rows rounded down to a multiple (prefill GEMM M)
     sched_aging_s: float = 1.0              # a waiting long-output request joins the priority class after this
+    # step-time bound (TTFT): while a short-output request (the agent's decide call) is decoding,
+    # cap each step's prefill tokens so the step's modelled device time stays under this (ms;
+    # 0 = off).  Cost model: base + per decode row + per prefill token (engine/scheduler.py)
+    step_time_target_ms: float = 0.0
+    step_cost_ms: tuple = (3.0, 0.07, 0.013)
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
     # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
@@ -148,6 +153,7 @@ class EngineConfig:
             max_model_len=_env_int("PENNY_MAX_MODEL_LEN", cls.max_model_len),
             step_token_quantum=_env_int("PENNY_STEP_TOKEN_QUANTUM", cls.step_token_quantum),
             sched_aging_s=_env_float("PENNY_SCHED_AGING_S", cls.sched_aging_s),
+            step_time_target_ms=_env_float("PENNY_STEP_TIME_TARGET_MS", cls.step_time_target_ms),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),

@@ -52,7 +52,19 @@ constexpr int HALF = 128 * 128;      // half-tile: 128 rows x 64 bf16 = 16 KiB
 constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
 constexpr int GM = 4;                // token tiles per L2 group
 enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
-enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6 };
+enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6,
+       EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8 };
+
+// Grouped fp8 MoE GEMM (penny_moe_gemm_prefill_fp8): rows sorted by expert, bucket bounds on the
+// DEVICE (offsets [E+1]), so tiles are found without a host round trip.
+struct MoeArgs {
+  const int* offsets;     // [E+1] sorted-row bucket bounds per expert
+  const int* rows;        // [P] token row of each sorted row in X (GEMM1 gather), null: X is sorted
+  const float* xs;        // per-row activation scale: xs[rows[p]] (GEMM1) / xs[p] (GEMM2)
+  const float* ws;        // [E, N] per-output-row weight scales
+  const float* route_w;   // [P] routing weight of each sorted row (EPI_MOE_ROUTE)
+  int E;
+};
 
 struct RopeArgs {
   const int* positions;   // [M]
@@ -64,11 +76,22 @@ struct RopeArgs {
   int Hq, Hkv;
 };
 
-__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+// LDS row swizzle of 16-B chunks, per fragment-read pattern (ds_read_b128 16-lane phases, 2 rows
+// per 256-B bank row): bf16 fragments read chunk 4kk + g, fp8 (16x16x128) fragments chunks 2g and
+// 2g + 1 -- (r >> 1) & 7 and (r >> 1) & 5 make those conflict-free (exhaustive check over the
+// linear XOR maps, profiles/r3_lds_swizzle_search.txt).
+template <bool FP8>
+__device__ __forceinline__ int swz(int r) { return FP8 ? ((r >> 1) & 5) : ((r >> 1) & 7); }
 
 union Frag {
   uint4 u;
   bf16x8 v;
+};
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// the two 16-B chunks a lane reads per fragment row: two bf16 k-steps, or ONE fp8 16x16x128 operand
+union FragPair {
+  Frag f[2];
+  i32x8 v;
 };
 
 // Two 4-column groups of bf16 accumulators, lo = columns 16f + 4g .. +3 and hi = 16(f+1) + 4g .. +3
@@ -96,34 +119,48 @@ __device__ __forceinline__ void bar() { __builtin_amdgcn_s_barrier(); }
 
 // Fragment reads.  Row r of a half-tile is at r*128; this lane's row within a 16-row fragment is
 // (lane & 15), whose swizzle (lane >> 1) & 7 is folded into choff[kk].
-__device__ __forceinline__ void read_w(const char* __restrict__ h, Frag (&a)[4][2], int wa, int rowoff,
+__device__ __forceinline__ void read_w(const char* __restrict__ h, FragPair (&a)[4], int wa, int rowoff,
                                        const int (&choff)[2]) {
 #pragma unroll
   for (int f = 0; f < 4; ++f)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
-      a[f][kk].u = *reinterpret_cast<const uint4*>(h + (wa * 64 + f * 16) * 128 + rowoff + choff[kk]);
+      a[f].f[kk].u = *reinterpret_cast<const uint4*>(h + (wa * 64 + f * 16) * 128 + rowoff + choff[kk]);
 }
 
-__device__ __forceinline__ void read_x(const char* __restrict__ h, Frag (&b)[2][2], int wb, int rowoff,
+__device__ __forceinline__ void read_x(const char* __restrict__ h, FragPair (&b)[2], int wb, int rowoff,
                                        const int (&choff)[2]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
-      b[t][kk].u = *reinterpret_cast<const uint4*>(h + (wb * 32 + t * 16) * 128 + rowoff + choff[kk]);
+      b[t].f[kk].u = *reinterpret_cast<const uint4*>(h + (wb * 32 + t * 16) * 128 + rowoff + choff[kk]);
 }
 
-template <int F0, int T0>
-__device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const Frag (&a)[4][2], const Frag (&b)[2][2]) {
+// bf16: 2 k-steps of v_mfma_f32_16x16x32_bf16 per fragment pair.  fp8 (OCP e4m3): the whole
+// 128-byte K-tile row in ONE v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair, unit block
+// scales (E8M0 127 = 2^0) -- 2x the bf16 MFMA rate; lane (row l & 15) feeds its 32 bytes k-block
+// (l >> 4) of A and of B alike, so the k order inside a block is the same on both operands.
+template <int F0, int T0, bool FP8>
+__device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], const FragPair (&b)[2]) {
   __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
+  if constexpr (FP8) {
 #pragma unroll
     for (int f = 0; f < 4; ++f)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        acc[F0 + f][T0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk].v, b[t][kk].v, acc[F0 + f][T0 + t], 0, 0, 0);
+        acc[F0 + f][T0 + t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            a[f].v, b[t].v, acc[F0 + f][T0 + t], 0, 0, 0, 127, 0, 127);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc[F0 + f][T0 + t] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f].f[kk].v, b[t].f[kk].v, acc[F0 + f][T0 + t], 0, 0, 0);
+  }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -131,12 +168,19 @@ __device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const Frag (&a)[4][2], c
 // 2 = no fragment ds_reads inside the K loop, 3 = LDS-DMA issued but never waited for in the
 // steady state (wrong results; timing attribution only)
 // BAL: balanced fragment-read schedule (below); 0 = the plain 12/4/8/0 schedule (A/B reference)
-template <int EPI, int ABL = 0, int BAL = 1>
-__global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restrict__ X, int ldx,
-                                                           const bf16* __restrict__ W, int K,
+// FP8: X and W are OCP e4m3 bytes (K-tile = 128 elements), the grouped MoE form: W is [E, N, K],
+// M counts sorted rows, the grid covers ceil(M/256) + E token tiles per column tile and the
+// surplus workgroups exit before touching LDS.
+template <int EPI, int ABL = 0, int BAL = 1, bool FP8 = false>
+__global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restrict__ Xv, int ldx,
+                                                           const void* __restrict__ Wv, int K,
                                                            void* __restrict__ Y, int ldy,
                                                            const bf16* __restrict__ R, int ldr,
-                                                           int M, int N, int S, RopeArgs ra) {
+                                                           int M, int N, int S, RopeArgs ra, MoeArgs ma) {
+  constexpr int ESZ = FP8 ? 1 : 2;        // bytes per element
+  constexpr int BKE = 128 / ESZ;          // elements per K-tile row (128 bytes)
+  const char* __restrict__ X = static_cast<const char*>(Xv);
+  const char* __restrict__ W = static_cast<const char*>(Wv);
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -144,7 +188,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
   const int g = lane >> 4, col = lane & 15;
 
   // ---- tile of this workgroup: bijective XCD remap, then L2 groups of GM token tiles ----
-  const int Mt = (M + TM - 1) / TM, Nt = N / TN, tiles = Mt * Nt, nwg = tiles * S;
+  const int Mt = (M + TM - 1) / TM + (FP8 ? ma.E : 0), Nt = N / TN, tiles = Mt * Nt, nwg = tiles * S;
   int id = blockIdx.x;
   {
     const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
@@ -154,9 +198,25 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
   const int grp = tile / (GM * Nt), first = grp * GM, gm = min(Mt - first, GM);
   const int within = tile - grp * GM * Nt;
   const int tm = first + within % gm, tn = within / gm;
-  const int m0 = tm * TM, n0 = tn * TN;
-  const int kc = K / S, k0 = s * kc, nt = kc / BK;
-  PENNY_DASSERT(N % TN == 0 && kc % BK == 0 && tm < Mt && tn < Nt);
+  int m0 = tm * TM, mend = M, e = 0;
+  const int n0 = tn * TN;
+  if constexpr (FP8) {
+    // token tile tm -> (expert e, its bucket's tile): walk the bucket sizes (E is small)
+    int rem = tm;
+    for (e = 0; e < ma.E; ++e) {
+      const int lo = ma.offsets[e], hi = ma.offsets[e + 1], nte = (hi - lo + TM - 1) / TM;
+      if (rem < nte) {
+        m0 = lo + rem * TM;
+        mend = hi;
+        break;
+      }
+      rem -= nte;
+    }
+    if (e == ma.E) return;                 // surplus tile of the upper-bound grid: whole WG exits
+    W += (long)e * N * K;
+  }
+  const int kc = K / S, k0 = s * kc, nt = kc / BKE;
+  PENNY_DASSERT(N % TN == 0 && kc % BKE == 0 && tm < Mt && tn < Nt);
 
   // ---- per-lane LDS-DMA sources: half h, piece i -> LDS rows 16w + 8i .. +7 of that half ----
   const char* src[4][2];
@@ -165,13 +225,14 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int lr = 16 * w + 8 * i + (lane >> 3);
-      const int c = (lane & 7) ^ swz(lr);                 // logical 16-B chunk held by this slot
+      const int c = (lane & 7) ^ swz<FP8>(lr);            // logical 16-B chunk held by this slot
       if (h == H_W0 || h == H_W1) {
         const int n = n0 + (lr >> 6) * 128 + (h == H_W1 ? 64 : 0) + (lr & 63);
-        src[h][i] = reinterpret_cast<const char*>(W + (long)n * K + k0 + 8 * c);
+        src[h][i] = W + ((long)n * K + k0) * ESZ + 16 * c;
       } else {
-        const int m = min(m0 + (lr >> 5) * 64 + (h == H_X1 ? 32 : 0) + (lr & 31), M - 1);
-        src[h][i] = reinterpret_cast<const char*>(X + (long)m * ldx + k0 + 8 * c);
+        int m = min(m0 + (lr >> 5) * 64 + (h == H_X1 ? 32 : 0) + (lr & 31), mend - 1);
+        if (FP8 && ma.rows) m = ma.rows[m];              // GEMM1 gathers the routed token rows
+        src[h][i] = X + ((long)m * ldx + k0) * ESZ + 16 * c;
       }
     }
   // The LDS-DMA is issued from inline asm, invisible to hipcc's waitcnt pass: with the builtin,
@@ -183,7 +244,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
     if (ABL == 1 && t > 1) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const char* gp = src[h][i] + (long)t * (BK * 2);
+      const char* gp = src[h][i] + (long)t * 128;
       const unsigned dst = buf + h * HALF + (16 * w + 8 * i) * 128;
       unsigned keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -194,14 +255,16 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
   };
 
   const int rowoff = col * 128;
-  const int choff[2] = {((0 + g) ^ ((col >> 1) & 7)) << 4, ((4 + g) ^ ((col >> 1) & 7)) << 4};
+  // fragment chunks of this lane: bf16 {g, 4 + g} (one per 32-k MFMA step), fp8 {2g, 2g + 1} (the
+  // 32-byte k-block of the 16x16x128 MFMA); row (lane & 15)'s swizzle folded in
+  const int choff[2] = {((FP8 ? 2 * g : g) ^ swz<FP8>(col)) << 4, ((FP8 ? 2 * g + 1 : 4 + g) ^ swz<FP8>(col)) << 4};
 
   f32x4 acc[8][4];
 #pragma unroll
   for (int f = 0; f < 8; ++f)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Frag a[4][2], b0[2][2], b1[2][2];
+  FragPair a[4], b0[2], b1[2];
 
   // ---- prologue: K-tile 0 whole, K-tile 1 halves W0, X0, X1 ----
 #pragma unroll
@@ -225,11 +288,11 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
   if (wa == 1) bar();
 
   // one phase: [fragment reads + DMA issued by the caller] barrier lgkmcnt(0) 16 MFMAs barrier
-  auto phase = [&](auto F0c, auto T0c, const Frag (&aa)[4][2], const Frag (&bb)[2][2]) {
+  auto phase = [&](auto F0c, auto T0c, const FragPair (&aa)[4], const FragPair (&bb)[2]) {
     constexpr int F0 = decltype(F0c)::value, T0 = decltype(T0c)::value;
     bar();
     wait_lgkm0();
-    mma<F0, T0>(acc, aa, bb);
+    mma<F0, T0, FP8>(acc, aa, bb);
     bar();
   };
   using I0 = std::integral_constant<int, 0>;
@@ -242,8 +305,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
     // 12 / 4 / 8 / 0 (phase 1's 48 KB of reads + 16 KB of landing DMA filled its whole MFMA
     // window on the LDS).  The extra wait: vmcnt(8) in phase 3 retires X_q0 (and W_q0) of t+1
     // (4 younger half-tiles may stay in flight), a phase before it is read.
-    Frag c0[2][2];
-    auto tile = [&](int t, Frag (&bc)[2][2], Frag (&bn)[2][2]) {
+    FragPair c0[2];
+    auto tile = [&](int t, FragPair (&bc)[2], FragPair (&bn)[2]) {
       const char* cur = smem + (t & 1) * BUF;
       const char* nx = smem + ((t + 1) & 1) * BUF;
       const unsigned lcur = lds0 + (t & 1) * BUF, lnxt = lds0 + ((t + 1) & 1) * BUF;
@@ -319,8 +382,42 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int m = m0 + wb * 64 + t * 16 + col;
-    if (m >= M) continue;
-    if constexpr (EPI == EPI_ROPE) {
+    if (m >= mend) continue;
+    if constexpr (EPI == EPI_MOE_SILU || EPI == EPI_MOE_ROUTE) {
+      // dequantise (activation row scale x weight row scale), then the decode pipeline's epilogue
+      // roundings (moe.hip moe_gemm_kernel): SiLU(gate) * up, or x routing weight
+      const float sx = ma.xs[ma.rows ? ma.rows[m] : m];
+      const float* wsc = ma.ws + (long)e * N + n0 + wa * 128;
+      if constexpr (EPI == EPI_MOE_SILU) {
+        bf16x4 o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 sg = *reinterpret_cast<const f32x4*>(wsc + 32 * q + 4 * g);
+          const f32x4 su = *reinterpret_cast<const f32x4*>(wsc + 32 * q + 16 + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gv = (float)(bf16)(acc[2 * q][t][r] * sx * sg[r]);
+            const float uv = (float)(bf16)(acc[2 * q + 1][t][r] * sx * su[r]);
+            o[q][r] = (bf16)((float)(bf16)(gv / (1.f + __expf(-gv))) * uv);
+          }
+        }
+        bf16* y = static_cast<bf16*>(Y) + (long)m * ldy + ((n0 + wa * 128) >> 5) * 16 + lane_off;
+#pragma unroll
+        for (int q = 0; q < 4; q += 2) *reinterpret_cast<uint4*>(y + 16 * q) = pair16(o[q], o[q + 1]);
+      } else {
+        const float rw = sx * ma.route_w[m];
+        bf16* y = static_cast<bf16*>(Y) + (long)m * ldy + n0 + wa * 128 + lane_off;
+#pragma unroll
+        for (int f = 0; f < 8; f += 2) {
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(wsc + 16 * f + 4 * g);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(wsc + 16 * f + 16 + 4 * g);
+          bf16x4 lo, hi;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lo[r] = (bf16)(acc[f][t][r] * s0[r] * rw), hi[r] = (bf16)(acc[f + 1][t][r] * s1[r] * rw);
+          *reinterpret_cast<uint4*>(y + 16 * f) = pair16(lo, hi);
+        }
+      }
+    } else if constexpr (EPI == EPI_ROPE) {
       constexpr int D = 128;
       const int hd = (n0 + wa * 128) >> 7;     // this wave's head (q heads, then k, then v)
       const int slot = ra.slots[m];
@@ -419,8 +516,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const bf16* __restric
 template <int EPI, int ABL = 0, int BAL = 1>
 static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
                    const void* R, int ldr, int M, int N, int S, const RopeArgs& ra) {
-  hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, (const bf16*)X, ldx, (const bf16*)W, K, Y,
-                     ldy, (const bf16*)R, ldr, M, N, S, ra);
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy,
+                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{});
 }
 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
@@ -478,5 +575,30 @@ PENNY_API int penny_gemm_prefill_ablate(const void* X, int ldx, const void* W, i
   else if (ablate == 3) launch<EPI_BF16, 3>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
   else if (ablate == 2) launch<EPI_BF16, 2>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
   else launch<EPI_BF16, 0>(grid_for(M, N, 1), stream, X, ldx, W, K, Y, ldy, nullptr, 0, M, N, 1, ra);
+  return (int)hipGetLastError();
+}
+
+// Grouped fp8 x fp8 MoE GEMM over expert buckets at prefill sizes (K13), no host round trip:
+//   epi 7 (GEMM1): Y[p, N/2] = silu(gate) * up of X[rows[p]] (fp8 [T, K], row scales xs[token]) x
+//                  W13_e (fp8 [E, N, K] row-major, 16-row gate|up interleave, row scales ws [E, N])
+//   epi 8 (GEMM2): Y[p, N] = X[p] (fp8 [P, K], scales xs[p]) x W2_e * route_w[p]
+// offsets [E+1] int32 on the device (bucket bounds of the P sorted rows).  Grid: (ceil(P/256) + E)
+// token tiles x N/256 -- an upper bound of the per-expert tile counts; surplus workgroups exit.
+// Contract (checked): N % 256 == 0, K % 128 == 0, ldx % 16 == 0, ldy % 8 == 0.
+PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows, const float* xs, const int* offsets,
+                                         const void* W, const float* ws, const float* route_w, void* Y, int ldy,
+                                         int P, int E, int N, int K, int epi, hipStream_t stream) {
+  if (P <= 0) return 0;
+  if (N % TN || K % 128 || ldx % 16 || ldy % 8 || E <= 0 || E > 256 || !offsets || !xs || !ws)
+    return (int)hipErrorInvalidValue;
+  if ((epi != EPI_MOE_SILU && epi != EPI_MOE_ROUTE) || (epi == EPI_MOE_ROUTE && !route_w)) return (int)hipErrorInvalidValue;
+  const MoeArgs ma{offsets, rows, xs, ws, route_w, E};
+  const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
+  if (epi == EPI_MOE_SILU)
+    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_SILU, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma);
+  else
+    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_ROUTE, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma);
   return (int)hipGetLastError();
 }

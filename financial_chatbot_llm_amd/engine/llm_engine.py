@@ -24,7 +24,7 @@ from ..utils.logging import get_logger
 from ..utils.profiling import StepProfiler, marker
 from .block_manager import make_block_manager
 from .model_runner import ModelRunner, build_step_inputs
-from .scheduler import Scheduler
+from .scheduler import Scheduler, StepCostModel
 from .sequence import PENDING, SamplingParams, Sequence
 from .tokenizer import BaseTokenizer, load_tokenizer
 
@@ -70,9 +70,11 @@ class LLMEngine:
         self.kv = KVCache(self.model.cfg.num_layers, nblocks, self.model.hkv, self.model.D,
                           dtype=getattr(self.model, "dtype", torch.bfloat16), device=device)
         self.bm = make_block_manager(nblocks, KV_BS, cfg.enable_prefix_caching)
+        base, per_row, per_tok = cfg.step_cost_ms
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
                                    token_quantum=cfg.step_token_quantum if device.type == "cuda" else 0,
-                                   aging_s=cfg.sched_aging_s)
+                                   aging_s=cfg.sched_aging_s,
+                                   cost_model=StepCostModel(cfg.step_time_target_ms, base, per_row, per_tok))
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)
@@ -347,6 +349,7 @@ class LLMEngine:
                 "kv_usage": self.bm.usage(), "prefix_hit_rate": self.bm.hit_rate(),
                 "kv_blocks": self.bm.num_blocks, "kv_evictions": int(getattr(self.bm, "evictions", 0)),
                 "preemptions": self.scheduler.num_preemptions,
+                "time_capped_steps": self.scheduler.num_capped_steps,
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
                 "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),

@@ -14,6 +14,13 @@ decide call (``max_tokens <= short_output_tokens``: a tool call or "No tool call
 turn's TTFT and its prompt is mostly prefix-cached, so it should not queue behind long respond
 prefills -- then everything else, each class FCFS.  Aging keeps it starvation-free: a request
 that has waited ``aging_s`` joins the first class.
+
+Step-time bound (``StepCostModel``, off unless ``step_time_target_ms`` > 0): every token of a
+decide call costs one engine step, so its latency is (tokens) x (step time) -- and a mixed step
+carrying a full prefill chunk takes ~3.5x a decode-only one.  While a short-output sequence is
+DECODING, the step's prefill tokens are capped so that the modelled step time stays under the
+target; prefill still gets at least ``min_prefill_tokens`` per step (never starved), and the cap
+lifts as soon as no decide call is decoding.
 """
 from __future__ import annotations
 
@@ -43,10 +50,27 @@ class ScheduledBatch:
         return not self.prefill and not self.decode
 
 
+@dataclass
+class StepCostModel:
+    """Modelled device time of one step (ms) = base + per_row * decode rows + per_token * prefill
+    tokens (defaults: Llama-3-8B on MI355X at the driver config -- decode-only steps of ~128 rows
+    ~12 ms, mixed steps ~44 ms at ~2.4k prefill tokens, profiles/r2_bench128_20x5_step_gpu_timing.txt)."""
+    target_ms: float = 0.0
+    base_ms: float = 3.0
+    per_row_ms: float = 0.07
+    per_token_ms: float = 0.013
+    min_prefill_tokens: int = 256
+
+    def prefill_cap(self, decode_rows: int) -> int:
+        room = self.target_ms - self.base_ms - self.per_row_ms * decode_rows
+        return max(self.min_prefill_tokens, int(room / self.per_token_ms))
+
+
 class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
-                 aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0):
+                 aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
+                 cost_model: "StepCostModel" = None):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -58,6 +82,8 @@ class Scheduler:
         self.aging_s = aging_s
         self.clock = clock
         self.token_quantum = token_quantum
+        self.cost = cost_model if cost_model is not None else StepCostModel()
+        self.num_capped_steps = 0
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
@@ -114,6 +140,13 @@ class Scheduler:
             self.bm.grow(seq, seq.num_tokens)
             batch.decode.append(seq)
             budget -= 1
+        # step-time bound: a decide call is decoding -> keep this step short (its next token waits
+        # for it); the cap never drops below min_prefill_tokens, so prefill always progresses
+        if self.cost.target_ms > 0 and any(s.params.max_tokens <= self.short_output_tokens for s in batch.decode):
+            cap = self.cost.prefill_cap(len(batch.decode))
+            if cap < budget:
+                budget = cap
+                self.num_capped_steps += 1
         # 2) continuing prefills
         for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting),
                           key=lambda s: s.arrival):

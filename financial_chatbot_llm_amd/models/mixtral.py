@@ -170,6 +170,13 @@ class MixtralModel(DecoderModel):
                                          self.w[p + "w13_scale"], self.w[p + "w2_t"], self.w[p + "w2_scale"],
                                          c.top_k_experts, self._moe_workspace(T))
             return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
+        if (self.fp8 and ops._native.use_native(h) and (p + "w13_q") in self.w
+                and moe_ops.PREFILL_TILES and self.w[p + "w13_q"].shape[1] % 256 == 0):
+            # prefill-size step: grouped fp8 tile GEMMs over device-side expert buckets (no host sync)
+            out = moe_ops.moe_prefill_fp8_tiles(h.contiguous(), logits.contiguous(), self.w[p + "w13_q"],
+                                                self.w[p + "w13_scale"], self.w[p + "w2_q"], self.w[p + "w2_scale"],
+                                                c.top_k_experts)
+            return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
         topw, topi = moe_ops.topk_softmax(logits, c.top_k_experts)
         order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
         offs = offsets.tolist()

@@ -37,6 +37,7 @@ _SIGS = {
     "penny_gemm_prefill": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gemm_prefill_qkv_rope": [P, c_int, P, c_int, c_int, P, P, P, P, P, P, c_int, c_int, P],
     "penny_gemm_prefill_ablate": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P],
+    "penny_moe_gemm_prefill_fp8": [P, c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gelu": [P, c_long, P],
     "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],

@@ -21,6 +21,11 @@ def topk_softmax(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tens
     return w, i.to(torch.int32)
 
 
+# prefill-size fp8 MoE steps run moe_prefill_fp8_tiles (PENNY_MOE_PREFILL_TILES=0: the per-expert
+# hipBLASLt fp8 loop with one host read of the bucket sizes per layer)
+PREFILL_TILES = os.environ.get("PENNY_MOE_PREFILL_TILES", "1") != "0"
+
+
 def route(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
     """Bucket (token, expert) pairs by expert.
 
@@ -81,6 +86,39 @@ def moe_prefill_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Te
     y2 = torch.empty((P, H), dtype=torch.bfloat16, device=h.device)
     N.call("penny_moe_gemm_fp8", N.ptr(aq), N.ptr(as_), None, N.ptr(offsets), N.ptr(w2t), N.ptr(s2), N.ptr(tok_w),
            N.ptr(y2), E, H, F_, 2, ntf2, st)
+    out = torch.empty_like(h)
+    N.call("penny_moe_combine", N.ptr(y2), N.ptr(inv), T, top_k, H, N.ptr(out), st)
+    return out
+
+
+def moe_prefill_fp8_tiles(h: torch.Tensor, router_logits: torch.Tensor, w13q: torch.Tensor, s13: torch.Tensor,
+                          w2q: torch.Tensor, s2: torch.Tensor, top_k: int) -> torch.Tensor:
+    """Prefill-size fp8 MoE on the 256x256 tile kernel (gemm_prefill.hip, block-scaled
+    v_mfma_scale_f32_16x16x128_f8f6f4 at unit scales = 2x the bf16 MFMA rate), no host sync:
+    device routing (:func:`route_device`), per-row fp8 activations, grouped GEMM1 over the expert
+    buckets gathering the routed token rows with the SiLU(gate)*up epilogue, per-row fp8 of the
+    intermediate, grouped GEMM2 with the routing weight in its epilogue, atomics-free combine.
+    ``w13q`` / ``w2q`` are the row-major e4m3 experts [E, N, K] (W13 16-row gate|up interleave)."""
+    from . import _native as N
+    T, H = h.shape
+    E, F2 = s13.shape
+    F_ = F2 // 2
+    P = T * top_k
+    topw, topi = topk_softmax(router_logits, top_k)
+    offsets, tok_idx, tok_w, inv = route_device(topi, topw, E)
+    st = N.stream()
+    xq = torch.empty((T, H), dtype=torch.uint8, device=h.device)
+    xs = torch.empty(T, dtype=torch.float32, device=h.device)
+    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(xq), N.ptr(xs), st)
+    a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
+           N.ptr(s13), None, N.ptr(a), F_, P, E, F2, H, 7, st)
+    aq = torch.empty((P, F_), dtype=torch.uint8, device=h.device)
+    as_ = torch.empty(P, dtype=torch.float32, device=h.device)
+    N.call("penny_quant_rows_fp8", N.ptr(a), F_, P, F_, N.ptr(aq), N.ptr(as_), st)
+    y2 = torch.empty((P, H), dtype=torch.bfloat16, device=h.device)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(aq), F_, None, N.ptr(as_), N.ptr(offsets), N.ptr(w2q), N.ptr(s2),
+           N.ptr(tok_w), N.ptr(y2), H, P, E, H, F_, 8, st)
     out = torch.empty_like(h)
     N.call("penny_moe_combine", N.ptr(y2), N.ptr(inv), T, top_k, H, N.ptr(out), st)
     return out

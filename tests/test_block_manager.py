@@ -202,3 +202,40 @@ def test_scheduler_quantises_step_rows():
     c = _mk_params(list(range(200)), "c", 64, arrival=1.0)
     small.add(c)
     assert small.schedule().num_tokens == 200           # below one quantum: untouched
+
+
+def test_step_time_bound_caps_prefill_only_while_a_decide_decodes():
+    """StepCostModel: with a short-output (decide) sequence decoding, the step's prefill tokens
+    are capped to the modelled time target (never below min_prefill_tokens); with no decide
+    decoding, the full token budget is used.  Long prompts still progress every step."""
+    from financial_chatbot_llm_amd.engine.block_manager import make_block_manager
+    from financial_chatbot_llm_amd.engine.scheduler import Scheduler, StepCostModel
+    from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
+    bm = make_block_manager(2048, 64, True)
+    cost = StepCostModel(target_ms=10.0, base_ms=2.0, per_row_ms=0.1, per_token_ms=0.01, min_prefill_tokens=128)
+    sch = Scheduler(bm, max_num_seqs=64, max_num_batched_tokens=4096, max_model_len=16384, cost_model=cost)
+    decide = Sequence("d", list(range(100)), SamplingParams(max_tokens=64))
+    sch.add(decide)
+    b = sch.schedule()                                   # decide prompt prefilled
+    decide.num_computed = decide.num_tokens
+    decide.output_ids.append(7)                          # now decoding
+    long_prompt = Sequence("r", list(range(10000)), SamplingParams(max_tokens=512))
+    sch.add(long_prompt)
+    b = sch.schedule()
+    assert b.decode == [decide]
+    cap = cost.prefill_cap(1)                            # (10 - 2 - 0.1) / 0.01 = 790
+    assert cap == 790 and b.num_prefill_tokens == cap and sch.num_capped_steps == 1
+    # the decide finishes: the long prompt gets the whole budget again
+    sch.finish(decide, "stop")
+    for s_, st, n in b.prefill:
+        s_.num_computed = st + n
+    b2 = sch.schedule()
+    assert b2.num_prefill_tokens == 4096
+    # a tight target never starves prefill
+    assert StepCostModel(target_ms=1.0).prefill_cap(200) == 256
+
+
+def test_step_time_bound_off_by_default():
+    from financial_chatbot_llm_amd.config import EngineConfig
+    from financial_chatbot_llm_amd.engine.scheduler import StepCostModel
+    assert EngineConfig().step_time_target_ms == 0.0 and StepCostModel().target_ms == 0.0

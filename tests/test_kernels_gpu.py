@@ -661,3 +661,41 @@ def test_bge_encoder_bulk_tile_kernels_match_library_path(monkeypatch):
     b = emb.embed(texts).float().cpu()
     cos = (a * b).sum(-1) / (a.norm(dim=-1) * b.norm(dim=-1))
     assert float(cos.min()) > 0.995, float(cos.min())
+
+
+@pytest.mark.parametrize("T,E", [(300, 8), (2100, 8), (777, 4)])
+def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
+    """Grouped fp8 tile GEMMs over device expert buckets (block-scaled 16x16x128 MFMA at unit
+    scales) == the per-expert fp8 x fp8 reference loop on the same quantized experts."""
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    g = torch.Generator(device=DEV).manual_seed(T)
+    H, F_, K = 1024, 1536, 2
+    w13 = (torch.randn((E, 2 * F_, H), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    w13 = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    w2 = (torch.randn((E, H, F_), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    h = torch.randn((T, H), device=DEV, generator=g).to(torch.bfloat16)
+    logits = (torch.randn((T, E), device=DEV, generator=g) * 2).to(torch.bfloat16)
+    if E == 4:                                   # an empty expert bucket
+        logits[:, 3] = -30.0
+    got = moe.moe_prefill_fp8_tiles(h, logits, q13.contiguous(), s13, q2.contiguous(), s2, K).float()
+    # reference: dequantised experts in f32, the same per-row fp8 activation rounding
+    topw, topi = moe.topk_softmax(logits, K)
+    xq, xs = moe.quant_rows_fp8(h)
+    xd = xq.float() * xs[:, None]
+    ref = torch.zeros((T, H), device=DEV)
+    for e in range(E):
+        sel = (topi == e)
+        rows = sel.any(1).nonzero().flatten()
+        if rows.numel() == 0:
+            continue
+        w13d = q13[e].float() * s13[e][:, None]
+        w2d = q2[e].float() * s2[e][:, None]
+        a = gemm.silu_mul((xd[rows] @ w13d.t()).to(torch.bfloat16), interleave16=True)
+        aq, as_ = moe.quant_rows_fp8(a)
+        y = (aq.float() * as_[:, None]) @ w2d.t()
+        wgt = (topw * sel).sum(1)[rows]
+        ref[rows] += wgt[:, None] * y
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 0.03, err
