@@ -14,6 +14,7 @@ import re
 from collections import defaultdict
 
 CLASSES = [
+    ("gemm-prefill tile (HIP)", r"gemm_prefill_kernel"),
     ("attention-decode", r"decode_kernel|decode_reduce"),
     ("attention-prefill", r"prefill_kernel|prefill2_kernel|cascade_kernel"),
     ("gemm-skinny (HIP)", r"skinny"),

@@ -85,7 +85,10 @@ __global__ void __launch_bounds__(1024) topk_topp_threshold_kernel(const T* __re
                                                                    const int* __restrict__ topk,
                                                                    const float* __restrict__ topp,
                                                                    float* __restrict__ thresh, int V) {
-  __shared__ float hist[16][256];
+  // per-wave digit histograms in INTEGERS: counts for top-k, probability mass in 2^-44 fixed point
+  // for top-p -- integer adds commute, so the threshold is bitwise independent of the order in
+  // which waves and lanes reach the atomics (float atomics made the nucleus edge run-dependent)
+  __shared__ unsigned long long hist[16][256];
   __shared__ float red[16];
   __shared__ float bins[256];
   __shared__ uint32_t s_prefix;
@@ -104,18 +107,18 @@ __global__ void __launch_bounds__(1024) topk_topp_threshold_kernel(const T* __re
   if (do_k) {
     float want = (float)k;
     for (int shift = 24; shift >= 0; shift -= 8) {
-      for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0.f;
+      for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0ull;
       __syncthreads();
       for (int i = tid; i < V; i += 1024) {
         const uint32_t key = fkey(ld1(lr + i));
-        if ((key & pmask) == prefix) atomicAdd(&hist[wid][(key >> shift) & 255], 1.f);
+        if ((key & pmask) == prefix) atomicAdd(&hist[wid][(key >> shift) & 255], 1ull);
       }
       __syncthreads();
       if (tid < 256) {
-        float t = 0.f;
+        unsigned long long t = 0;
 #pragma unroll
         for (int w = 0; w < 16; ++w) t += hist[w][tid];
-        bins[tid] = t;
+        bins[tid] = (float)t;
       }
       __syncthreads();
       if (wid == 0) {
@@ -154,20 +157,22 @@ __global__ void __launch_bounds__(1024) topk_topp_threshold_kernel(const T* __re
   pmask = 0;
   float want = -1.f;                                  // set from the first pass's total
   for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0.f;
+    for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0ull;
     __syncthreads();
     for (int i = tid; i < V; i += 1024) {
       const float l = ld1(lr + i);
       const uint32_t key = fkey(l);
+      // exp <= 1 (l <= mx): x 2^44 fits 45 bits, a 128k-entry vocabulary sums below 2^62
       if (key >= kfloor && (key & pmask) == prefix)
-        atomicAdd(&hist[wid][(key >> shift) & 255], __expf((l - mx) * inv_t));
+        atomicAdd(&hist[wid][(key >> shift) & 255],
+                  (unsigned long long)(__expf((l - mx) * inv_t) * 17592186044416.f));
     }
     __syncthreads();
     if (tid < 256) {
-      float t = 0.f;
+      unsigned long long t = 0;
 #pragma unroll
       for (int w = 0; w < 16; ++w) t += hist[w][tid];
-      bins[tid] = t;
+      bins[tid] = (float)t * 5.684341886080802e-14f;   // 2^-44
     }
     __syncthreads();
     if (wid == 0) {

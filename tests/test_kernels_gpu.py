@@ -699,3 +699,20 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
         ref[rows] += wgt[:, None] * y
     err = float((got - ref).abs().max() / ref.abs().max())
     assert err < 0.03, err
+
+
+def test_topp_threshold_is_bitwise_repeatable():
+    """Integer (fixed-point) digit histograms: the top-p threshold of the same logits is bitwise
+    identical across repeated launches and batch positions (advisor finding: float atomics made
+    the nucleus edge depend on atomic ordering)."""
+    from financial_chatbot_llm_amd.ops.sampling import topk_topp_threshold
+    g = torch.Generator().manual_seed(5)
+    V = 128256
+    row = (torch.randn(1, V, generator=g) * 2.0).to(torch.bfloat16)
+    lg = row.repeat(24, 1).to(DEV)
+    t = torch.full((24,), 0.7, device=DEV)
+    k = torch.zeros(24, dtype=torch.int32, device=DEV)
+    p = torch.full((24,), 0.9, device=DEV)
+    ths = [topk_topp_threshold(lg, t, k, p).cpu() for _ in range(20)]
+    ref = ths[0][0]
+    assert all(bool((th == ref).all()) for th in ths)
