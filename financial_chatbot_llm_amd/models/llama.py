@@ -17,6 +17,7 @@ per decoding sequence (continuous batching); the attention split is described by
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -25,10 +26,16 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.dist import state as pstate
+from ..ops.attention import _side_stream
 from ..ops.gemm import interleave16, linear, prefill_qkv_rope, qkv_rope_fused, tile_weight, uses_tiled_weight
 from ..parallel.layers import shard_cols, shard_rows, shard_sections, vocab_range
 from .common import AttentionMetadata, KVCache, random_tensor
 from .configs import ModelConfig
+
+
+# mixed prefill+decode steps overlap the two attention kernels on two streams (PENNY_ATTN_OVERLAP=0:
+# one stream, prefill then decode)
+ATTN_OVERLAP = os.environ.get("PENNY_ATTN_OVERLAP", "1") != "0"
 
 
 class DecoderModel:
@@ -173,10 +180,22 @@ class DecoderModel:
             q = ops.rope_kv_write(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv, self.D)
         attn = torch.empty_like(q)
         tp = meta.num_prefill_tokens
+        side = None
+        if tp > 0 and meta.num_decode > 0 and ATTN_OVERLAP and q.is_cuda and meta.cascade is None:
+            # mixed step: the decode rows' attention (HBM-bound: streams their whole contexts) runs on
+            # a side stream CONCURRENTLY with the prefill rows' attention (MFMA-bound) -- the two read
+            # disjoint sequences' KV and write disjoint rows of attn; joined before the O projection
+            side = _side_stream(q.device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
+                           workspace=meta.decode_ws, out=attn[tp:])
         if tp > 0:
             ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, self.scale,
                         causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp])
-        if meta.num_decode > 0:
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
+        elif meta.num_decode > 0:
             ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
                        workspace=meta.decode_ws, out=attn[tp:], cascade=meta.cascade)
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"),
