@@ -164,12 +164,26 @@ class LLMEngine:
         return run[:room]
 
     def _stage_grammar(self, seq: Sequence) -> None:
-        """After a SAMPLED token: stage the output grammar's forced continuation (if any)."""
+        """After a SAMPLED token: stage the output grammar's forced continuation (if any).
+
+        The forced text is tokenized TOGETHER with the output so far: BPE merges across the
+        boundary (Llama-3: around '{"' or '": "') would otherwise give token ids the model would
+        never have produced itself.  Only the tokens past the current output are appended, and
+        only if the output is a token-prefix of that joint encoding; otherwise this token jumps
+        nothing and the model continues sampling."""
         g = seq.params.grammar
         if g is None or seq.params.forced_output is not None:
             return
-        forced, ends = g.forced(self.tokenizer.decode(seq.output_ids))
-        run = self.tokenizer.encode(forced, allow_special=False) if forced else []
+        text = self.tokenizer.decode(seq.output_ids)
+        forced, ends = g.forced(text)
+        run: List[int] = []
+        if forced:
+            joint = self.tokenizer.encode(text + forced, allow_special=False)
+            n = len(seq.output_ids)
+            if joint[:n] != list(seq.output_ids) or len(joint) <= n:
+                seq.jump_queue = []
+                return
+            run = joint[n:]
         if ends and self.eos_ids:
             run.append(self.tokenizer.special.get("<|eot_id|>", next(iter(self.eos_ids))))
         seq.jump_queue = run

@@ -133,3 +133,40 @@ def test_tokens_after_a_jump_chunk_match_plain_prefill(mode):
     ref_prompt = prompt + out[:1 + len(run)]
     (ref,), _ = _run([SamplingParams(temperature=0.0, max_tokens=12 - 1 - len(run), ignore_eos=True)], [ref_prompt], mode)
     assert out[1 + len(run):] == ref.output_ids
+
+
+def test_jump_run_tokenized_jointly_with_the_output(tmp_path):
+    """With a real byte-level BPE (merges across '{"', '": "'), the staged jump run is exactly the
+    tail of the JOINT encoding of output + forced text, and a non-canonical output (its tokens
+    are not a prefix of that encoding) jumps nothing (advisor finding on _stage_grammar)."""
+    from types import SimpleNamespace
+
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    from financial_chatbot_llm_amd.engine.llm_engine import LLMEngine
+    from financial_chatbot_llm_amd.engine.tokenizer import HFTokenizer
+    tk = Tokenizer(models.BPE())
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    corpus = ['{"name": "retrieve_transactions", "parameters": {"search_query": "groceries", "num_transactions": 20}}']
+    tk.train_from_iterator(corpus * 300, trainers.BpeTrainer(vocab_size=420, special_tokens=["<|eot_id|>"],
+                                                             initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    path = tmp_path / "tokenizer.json"
+    tk.save(str(path))
+    tok = HFTokenizer(str(path))
+    eng = SimpleNamespace(tokenizer=tok, eos_ids=set(tok.eos_ids))
+    g = ToolCallGrammar([RET])
+    text = '{"'
+    out = tok.encode(text, allow_special=False)
+    seq = SimpleNamespace(params=SimpleNamespace(grammar=g, forced_output=None), output_ids=list(out), jump_queue=[])
+    LLMEngine._stage_grammar(eng, seq)
+    forced, _ = g.forced(text)
+    assert forced and seq.jump_queue
+    assert list(out) + seq.jump_queue == tok.encode(text + forced, allow_special=False)
+    # non-canonical: '{' sampled alone where the joint encoding merges '{"' -> no jump
+    brace = tok.encode("{", allow_special=False)
+    joint = tok.encode("{" + g.forced("{")[0], allow_special=False)
+    if joint[:len(brace)] != brace:
+        seq2 = SimpleNamespace(params=seq.params, output_ids=list(brace), jump_queue=[1, 2])
+        LLMEngine._stage_grammar(eng, seq2)
+        assert seq2.jump_queue == []
