@@ -15,6 +15,7 @@ import statistics
 import time
 from typing import Callable, Dict, List
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -113,6 +114,67 @@ def bench_decode_mixed(dev) -> List[Dict]:
         uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2
         out.append({"op": "decode_attn_mixed", "B": B, "ctx_mean": round(sum(ctxs) / B), "us": round(us, 1),
                     "GBps_unique": round(uniq / us / 1e3, 1)})
+    return out
+
+
+def bench_decode_lean(dev) -> List[Dict]:
+    """Work-balanced (lean) vs partitioned split-K decode on workload-shaped batches, interleaved
+    rounds; with and without the shared-prefix cascade.  GB/s counts unique KV bytes (the shared
+    prefix once) and logical bytes (every row's full context)."""
+    from ..ops import attention as A
+    out = []
+    g = torch.Generator(device=dev).manual_seed(3)
+    Hq, Hkv, D = 32, 8, 128
+    for B, lo, hi, shared in [(64, 1500, 6500, 1024), (128, 1500, 6500, 1024), (96, 2000, 8000, 2048),
+                              (64, 2048, 2049, 0), (256, 1000, 3000, 768), (16, 1100, 8000, 1024)]:
+        rng = torch.Generator().manual_seed(B + lo)
+        ctxs = torch.randint(lo, hi, (B,), generator=rng).tolist()
+        nsh = shared // KV_BS
+        W = max((c + KV_BS - 1) // KV_BS for c in ctxs)
+        tables = torch.zeros((B, W), dtype=torch.int32)
+        nxt = nsh
+        for b, c in enumerate(ctxs):
+            nb = (c + KV_BS - 1) // KV_BS
+            tables[b, :nsh] = torch.arange(nsh, dtype=torch.int32)
+            tables[b, nsh:nb] = torch.arange(nxt, nxt + nb - nsh, dtype=torch.int32)
+            nxt += nb - nsh
+        kc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        vc = torch.randn((nxt + 1, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        tables_d = tables.to(dev)
+        q = torch.randn((B, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        lens = torch.tensor(ctxs, dtype=torch.int32, device=dev)
+        ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
+        o = torch.empty_like(q)
+        plan = ops.plan_cascade(np.asarray(ctxs, np.int32), tables.numpy(), Hq // Hkv) if shared else None
+        ci = ops.CascadeInputs.from_plan(plan, dev) if plan is not None else None
+
+        def mk(lean, cas):
+            def f():
+                A.DECODE_LEAN = lean
+                ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o, cascade=cas)
+            return f
+        fns = {"part": mk(False, None), "lean": mk(True, None)}
+        if ci is not None:
+            fns.update({"part_cascade": mk(False, ci), "lean_cascade": mk(True, ci)})
+        ref = None
+        errs = {}
+        for k, f in fns.items():
+            f()
+            torch.cuda.synchronize()
+            ref = o.float().clone() if ref is None else ref
+            errs[k] = float((o.float() - ref).abs().max())
+        ts = interleaved(fns, rounds=7, iters=20)
+        A.DECODE_LEAN = True
+        uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2
+        logical = sum(ctxs) * Hkv * D * 2 * 2
+        row = {"op": "decode_lean_ab", "B": B, "ctx_range": [lo, hi], "ctx_mean": round(sum(ctxs) / B),
+               "shared": shared, "MB_unique": round(uniq / 1e6, 1), "max_abs_diff": errs}
+        for k, us in ts.items():
+            row[k + "_us"] = round(us, 1)
+            row[k + "_GBps_unique"] = round(uniq / us / 1e3, 1)
+            row[k + "_GBps_logical"] = round(logical / us / 1e3, 1)
+        print(json.dumps(row), flush=True)
+        out.append(row)
     return out
 
 
@@ -774,7 +836,7 @@ def main(argv=None) -> int:
     dev = torch.device("cuda")
     res = []
     for name in args.only.split(","):
-        res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
+        res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,

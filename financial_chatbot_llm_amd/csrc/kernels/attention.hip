@@ -535,6 +535,259 @@ __global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int
   if (d < D) out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 
+// ------------------------------------------------------------------------------------------
+// Lean (work-balanced) split-K decode
+// ------------------------------------------------------------------------------------------
+// The partitioned kernel above gives every (row, kv head, partition) its own workgroup, so a
+// batch whose contexts spread over 1.5-6.5k keys leaves long partitions running alone at the end
+// (and short rows waste whole workgroups).  Here each kv head's (row, block) units of the batch's
+// per-row SUFFIX (blocks from kv_start on -- cascade handles shared prefixes) are flattened
+// row-major into one range that is cut into equal contiguous pieces, one per WAVE of the head's
+// share of a fixed grid sized to one round of the chip: every wave streams the same number of KV
+// blocks and the whole grid drains together.  Workgroup i serves kv head i % Hkv, so with the
+// round-robin workgroup dispatch over the 8 XCDs (Hkv == 8) each XCD streams ONE head and its 4 MB
+// L2 keeps that head's shared-prefix blocks (0.5 MB per 1k tokens) hot for every row.  A wave
+// writes one partial (m, l, unnormalised O) per row segment it touches, at slot (wave - first
+// wave of the segment); a segment one wave covers entirely is normalised and written straight to
+// `out` (no partial, no merge).  The plan (per-row prefix sums, units per wave) is recomputed by
+// every workgroup from ctx_lens/kv_start (device data: hipGraph-capturable), and workgroup 0
+// publishes it in `meta` for the merge kernel.
+constexpr int LEAN_MAX_B = 1024;
+
+struct LeanPlan {
+  int total;     // suffix blocks over all rows (per kv head)
+  int per_wave;  // units per wave
+};
+
+// s_pre[0..B]: exclusive prefix sums of the per-row suffix block counts
+__device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* __restrict__ ctx_lens,
+                                              const int* __restrict__ kv_start, int B, int nwaves, int nparts,
+                                              int min_per_wave) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int c[4], sum = 0, mx = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = 4 * t + i;
+    c[i] = b < B ? (ctx_lens[b] + KV_BS - 1) / KV_BS - (kv_start ? kv_start[b] : 0) : 0;
+    sum += c[i];
+    mx = max(mx, c[i]);
+  }
+  int inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+  if (lane == 63) s_w[w] = inc;
+  if (lane == 0) s_w[4 + w] = mx;
+  __syncthreads();
+  int excl = inc - sum, total = 0, maxn = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < w) excl += s_w[i];
+    total += s_w[i];
+    maxn = max(maxn, s_w[4 + i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = 4 * t + i;
+    if (b < B) s_pre[b] = excl;
+    excl += c[i];
+  }
+  if (t == 0) s_pre[B] = total;
+  __syncthreads();
+  // a segment of n blocks meets at most ceil(n / per_wave) + 1 waves: keep that <= nparts slots
+  const int want = (total + nwaves - 1) / nwaves;
+  const int cap = (maxn + nparts - 2) / (nparts - 1);
+  return LeanPlan{total, max(max(want, cap), min_per_wave)};
+}
+
+// grid (nwg), nwg % Hkv == 0: workgroup i serves kv head i % Hkv with 4 waves; wave hw of a head
+// owns that head's units [hw*per_wave, (hw+1)*per_wave)
+template <int D>
+__global__ void __launch_bounds__(256) decode_lean_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o,
+    int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
+    int min_per_wave) {
+  constexpr int KC = D / 32, DT = D / 16;
+  __shared__ int s_pre[LEAN_MAX_B + 1];
+  __shared__ int s_w[8];
+  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, kv_start, B, gridDim.x / Hkv * 4, nparts, min_per_wave);
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i <= B; i += 256) meta[i] = s_pre[i];
+    if (threadIdx.x == 0) meta[B + 1] = pl.per_wave;
+  }
+  const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  const int h = blockIdx.x % Hkv;
+  const int hw = (blockIdx.x / Hkv) * 4 + (threadIdx.x >> 6);
+  const int G = Hq / Hkv;
+  int u = hw * pl.per_wave;
+  const int uend = min(pl.total, u + pl.per_wave);
+  if (u >= uend) return;   // no barrier below this point
+  // row of unit u: the last b with s_pre[b] <= u (skips empty rows)
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_pre[mid] <= u) lo = mid;
+    else hi = mid - 1;
+  }
+  int b = lo;
+
+  while (u < uend) {
+    const int seg0 = s_pre[b], n = s_pre[b + 1] - seg0;
+    const int k0 = u - seg0, k1 = min(n, uend - seg0);
+    const int ctx = ctx_lens[b];
+    const int kvs = kv_start ? kv_start[b] : 0;
+    const int* bt = block_tables + (long)b * max_blocks + kvs;
+
+    Frag qf[KC];
+    {
+      const bool valid = col < G;
+      const bf16* qrow = q + ((long)b * Hq + h * G + (valid ? col : 0)) * D;
+#pragma unroll
+      for (int c = 0; c < KC; ++c)
+        qf[c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
+    }
+    f32x4 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    int ids = 0;
+    for (int k = k0; k < k1; ++k) {
+      const int it = k - k0;
+      if ((it & 63) == 0) {
+        const int kl = k + lane;
+        ids = kl < k1 ? bt[kl] : 0;
+      }
+      const long phys = __builtin_amdgcn_readlane(ids, it & 63);
+      PENNY_DASSERT(phys >= 0);
+      const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+      const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+      Frag kf[4][KC], vf[DT][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int c = 0; c < KC; ++c) kf[t][c].u = kb[(t * KC + c) * 64 + lane];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) vf[dt][st].u = vb[(dt * 2 + st) * 64 + lane];
+      const int j = kvs + k;
+      f32x4 sc[4];
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < KC; ++c) sc[t] = mfma16(kf[t][c].v, qf[c].v, sc[t]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = j * KV_BS + 16 * t + 4 * g + r;
+          const float v = key < ctx ? sc[t][r] * scale_log2 : -INFINITY;
+          sc[t][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      }
+      mt = rowgroup_max(mt);
+      const bool grow = mt > m + 8.f;
+      if (__any(grow)) {
+        const float mn = grow ? mt : m;
+        const float alpha = grow ? fast_exp2(m - mn) : 1.f;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+        m = mn;
+      }
+      const float mref = (m == -INFINITY) ? 0.f : m;
+      float ls = 0.f;
+      Frag pf[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(sc[t][r] - mref);
+          ls += pv;
+          pf[t >> 1].v[4 * (t & 1) + r] = (bf16)pv;
+        }
+      }
+      l += ls;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        o[dt] = mfma16(vf[dt][0].v, pf[0].v, o[dt]);
+        o[dt] = mfma16(vf[dt][1].v, pf[1].v, o[dt]);
+      }
+    }
+    l = rowgroup_sum(l);
+    if (col < G) {
+      const int hq = h * G + col;
+      if (k0 == 0 && k1 == n && kvs == 0) {   // whole segment, no cascade part: final output
+        const float inv = 1.f / l;
+        bf16* orow = out + ((long)b * Hq + hq) * D;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[dt][r] * inv);
+          *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v;
+        }
+      } else {
+        const long pi = ((long)b * Hq + hq) * part_stride + (hw - seg0 / pl.per_wave);
+        PENNY_DASSERT(hw - seg0 / pl.per_wave < nparts);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(part_o + pi * D + 16 * dt + 4 * g) = o[dt];
+        if (g == 0) {
+          part_m[pi] = m;
+          part_l[pi] = l;
+        }
+      }
+    }
+    u = seg0 + k1;
+    do {
+      ++b;
+    } while (b < B - 1 && s_pre[b + 1] == s_pre[b]);
+  }
+}
+
+// grid (Hq, B), D threads: merges a row's lean partials (slots 0..) and cascade chunks (slots
+// nparts..), skipping rows one wave already finished
+template <int D>
+__global__ void decode_lean_reduce_kernel(const int* __restrict__ meta, const int* __restrict__ ctx_lens,
+                                          const int* __restrict__ kv_start, const float* __restrict__ part_m,
+                                          const float* __restrict__ part_l, const float* __restrict__ part_o,
+                                          bf16* __restrict__ out, int B, int Hq, int Hkv, int nparts,
+                                          int part_stride, int chunk_blocks) {
+  const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
+  const int pre = meta[b], n = meta[b + 1] - pre, pw = meta[B + 1];
+  const int s0 = kv_start ? kv_start[b] : 0;
+  const int nc = s0 > 0 ? (s0 + chunk_blocks - 1) / chunk_blocks : 0;
+  int np = 0;
+  if (n > 0) {
+    const int fw = pre / pw, lw = (pre + n - 1) / pw;
+    if (fw == lw && nc == 0) return;   // written by its one wave
+    np = lw - fw + 1;
+  }
+  const long base = ((long)b * Hq + hq) * part_stride;
+  float M = -INFINITY;
+  for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
+  for (int i = 0; i < nc; ++i) M = fmaxf(M, part_m[base + nparts + i]);
+  float L = 0.f, O = 0.f;
+  for (int i = 0; i < np; ++i) {
+    const float f = exp2f(part_m[base + i] - M);
+    L += part_l[base + i] * f;
+    O += part_o[(base + i) * D + d] * f;
+  }
+  for (int i = nparts; i < nparts + nc; ++i) {
+    const float f = exp2f(part_m[base + i] - M);
+    L += part_l[base + i] * f;
+    O += part_o[(base + i) * D + d] * f;
+  }
+  out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+}
+
 
 // Pipelined prefill (the production prefill path for tiles of > 128 rows).
 // One workgroup = NW waves x 32 rows = NW*32 (token*G + head) rows of one sequence and kv head:
@@ -728,7 +981,8 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      int part_stride, float scale, const int* kv_start, const int* members,
                                      const int* cu_g, const int* g_ctx, const int* g_bt, const int* work,
                                      const int* nwork, int grid_work, int g_max_blocks, int chunk_blocks,
-                                     int phases, hipStream_t stream) {
+                                     int phases, int lean_grid, int* lean_meta, int lean_min_per_wave,
+                                     hipStream_t stream) {
   // phases: 1 cascade (shared-prefix tiles), 2 split-K decode, 4 merge -- the caller may run
   // phase 1 on a side stream concurrently with phase 2 (ops/attention.py), joining before 4
   if (B <= 0) return 0;
@@ -736,6 +990,11 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   const bool cascade = kv_start != nullptr;
   if (cascade && (chunk_blocks <= 0 || grid_work <= 0 || 128 % (Hq / Hkv) ||
                   part_stride < nparts + (g_max_blocks + chunk_blocks - 1) / chunk_blocks))
+    return (int)hipErrorInvalidValue;
+  // lean_grid > 0: the work-balanced suffix kernel (decode_lean_kernel) and its merge replace
+  // phases 2 and 4
+  const bool lean = lean_grid > 0;
+  if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv))
     return (int)hipErrorInvalidValue;
   // measured (profiles/r1_decode_head_fast.txt): head-fastest wins at B <= 16 (18.5 vs 21.6 us at
   // ctx 2048 / 1024 shared), sequence-fastest at B >= 64 (a sequence's 8 heads of a KV block are
@@ -752,15 +1011,24 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   if (cascade && (phases & 1))                                                                                  \
     hipLaunchKernelGGL(cascade_kernel<DD>, dim3(grid_work, Hkv), dim3(256), 0, stream, (const bf16*)q, cu_g, g_ctx,  \
                        g_bt, (const bf16*)k_cache, (const bf16*)v_cache, sl2, Hq, Hkv, g_max_blocks, ca);         \
-  if ((phases & 2) && head_fast)                                                                                \
+  if ((phases & 2) && lean)                                                                                     \
+    hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
+                       kv_start, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,   \
+                       part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,              \
+                       lean_min_per_wave);                                                                       \
+  if ((phases & 4) && lean)                                                                                     \
+    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, ctx_lens,       \
+                       kv_start, part_m, part_l, part_o, (bf16*)out, B, Hq, Hkv, nparts, part_stride,            \
+                       chunk_blocks);                                                                            \
+  if ((phases & 2) && !lean && head_fast)                                                                       \
     hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start,  \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
                        part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
-  if ((phases & 2) && !head_fast)                                                                               \
+  if ((phases & 2) && !lean && !head_fast)                                                                      \
     hipLaunchKernelGGL((decode_kernel<DD, false>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start, \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
                        part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
-  if ((phases & 4) && (nparts > 1 || cascade))                                                                  \
+  if ((phases & 4) && !lean && (nparts > 1 || cascade))                                                         \
     hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, ctx_lens, kv_start, part_m,     \
                        part_l, part_o, (bf16*)out, Hq, pb, nparts, part_stride, chunk_blocks);
   if (D == 128) {

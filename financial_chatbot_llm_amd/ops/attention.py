@@ -213,6 +213,7 @@ class DecodeWorkspace:
     pb: int
     nparts: int
     part_stride: int = 0    # partition slots per (row, head): nparts suffix + cascade chunk slots
+    lean_meta: Optional[torch.Tensor] = None   # [max_batch + 2] int32: the lean kernel's plan
 
     def partitioning(self, B: int):
         """(pb, nparts) for a decode batch of B rows.  Batches of 32+ rows already fill the chip
@@ -233,11 +234,12 @@ class DecodeWorkspace:
     @classmethod
     def create(cls, max_batch: int, Hq: int, D: int, max_ctx: int, device, pb: int = 8) -> "DecodeWorkspace":
         nblk = (max_ctx + KV_BS - 1) // KV_BS
-        nparts = max(1, (nblk + pb - 1) // pb)
+        nparts = max(2, (nblk + pb - 1) // pb)
         stride = nparts + CASCADE_MAX_CHUNKS
         f = dict(dtype=torch.float32, device=device)
         return cls(torch.empty((max_batch, Hq, stride), **f), torch.empty((max_batch, Hq, stride), **f),
-                   torch.empty((max_batch, Hq, stride, D), **f), pb, nparts, stride)
+                   torch.empty((max_batch, Hq, stride, D), **f), pb, max(nparts, 2), stride,
+                   torch.zeros(max_batch + 2, dtype=torch.int32, device=device))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -383,6 +385,23 @@ class CascadeInputs:
 
 _SIDE_STREAMS = {}
 
+# Work-balanced ("lean") split-K decode for the per-row suffixes (decode_lean_kernel): every wave
+# of a one-round grid streams the same number of KV blocks.  PENNY_DECODE_LEAN=0 restores the
+# per-(row, head, partition) workgroup kernel; LEAN_MIN_B: smaller batches keep it (A/B knob).
+DECODE_LEAN = os.environ.get("PENNY_DECODE_LEAN", "1") != "0"
+LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
+LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
+LEAN_MIN_PER_WAVE = 2
+_CU_COUNT = {}
+
+
+def _lean_grid(device, Hkv: int) -> int:
+    """One round of workgroups, a multiple of Hkv (workgroup i serves kv head i % Hkv)."""
+    key = torch.device(device).index
+    if key not in _CU_COUNT:
+        _CU_COUNT[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    return max(1, LEAN_WG_PER_CU * _CU_COUNT[key] // Hkv) * Hkv
+
 
 def _side_stream(device) -> "torch.cuda.Stream":
     key = torch.device(device).index
@@ -412,12 +431,14 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         cas = ((N.ptr(c.kv_start), N.ptr(c.members), N.ptr(c.cu_g), N.ptr(c.g_ctx), N.ptr(c.g_bt), N.ptr(c.work),
                 N.ptr(c.nwork), c.grid, CASCADE_MAX_BLOCKS, CASCADE_CHUNK) if c is not None
                else (None, None, None, None, None, None, None, 0, 0, 0))
-        pb, nparts = ws.partitioning(B) if c is None else (ws.pb, ws.nparts)
+        lean = DECODE_LEAN and B >= LEAN_MIN_B and ws.lean_meta is not None and ws.lean_meta.numel() >= B + 2
+        pb, nparts = ws.partitioning(B) if (c is None and not lean) else (ws.pb, ws.nparts)
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale), *cas]
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE) if lean else (0, None, 1))
         if c is None:
-            N.call("penny_attention_decode", *args, 7, N.stream())
+            N.call("penny_attention_decode", *args, 7, *lean_args, N.stream())
         else:
             # shared-prefix tiles on a side stream, concurrent with the per-row suffix partitions;
             # join before the merge (fork/join via events: hipGraph-capturable)
@@ -425,10 +446,10 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
             side = _side_stream(q.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                N.call("penny_attention_decode", *args, 1, side.cuda_stream)
-            N.call("penny_attention_decode", *args, 2, main.cuda_stream)
+                N.call("penny_attention_decode", *args, 1, *lean_args, side.cuda_stream)
+            N.call("penny_attention_decode", *args, 2, *lean_args, main.cuda_stream)
             main.wait_stream(side)
-            N.call("penny_attention_decode", *args, 4, main.cuda_stream)
+            N.call("penny_attention_decode", *args, 4, *lean_args, main.cuda_stream)
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()

@@ -133,15 +133,20 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
 @pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
                                          # B >= 96 / >= 192: longer partitions (pb 16 / 32)
                                          (32, 8, [(37 * i) % 3000 + 1 for i in range(100)]),
-                                         (8, 2, [(53 * i) % 4000 + 1 for i in range(200)])])
-def test_decode_attention(Hq, Hkv, ctxs):
+                                         (8, 2, [(53 * i) % 4000 + 1 for i in range(200)]),
+                                         # lean split: one long row among short ones, many rows
+                                         (32, 8, [8000] + [70] * 40 + [3000, 1]),
+                                         (32, 8, [(97 * i) % 500 + 1 for i in range(700)])])
+@pytest.mark.parametrize("lean", [True, False])
+def test_decode_attention(Hq, Hkv, ctxs, lean, monkeypatch):
+    monkeypatch.setattr(ops.attention, "DECODE_LEAN", lean)
     g = torch.Generator().manual_seed(5)
     D = 128
     tables, kc, vc = _paged_setup(ctxs, Hkv, D, gen=g)
     q = rnd(len(ctxs), Hq, D, gen=g)
     ctx_t = torch.tensor(ctxs, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    ws = ops.DecodeWorkspace.create(len(ctxs), Hq, D, 4096, DEV)
+    ws = ops.DecodeWorkspace.create(len(ctxs), Hq, D, max(ctxs), DEV)
     out = ops.decode(q.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, workspace=ws)
     ref = ops.decode(q, ctx_t, tables, kc, vc, scale)
     close(out, ref, atol=2e-2)
@@ -407,8 +412,10 @@ def _shared_prefix_tables(B, groups, W, num_blocks, gen):
     return tables
 
 
+@pytest.mark.parametrize("lean", [True, False])
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 8, 4)])
-def test_cascade_decode_matches_reference(D, Hq, Hkv):
+def test_cascade_decode_matches_reference(D, Hq, Hkv, lean, monkeypatch):
+    monkeypatch.setattr(ops.attention, "DECODE_LEAN", lean)
     g = torch.Generator().manual_seed(12)
     # group A: 40 rows x 10 shared blocks (2 member tiles, chunks 4+4+2); group B: 5 rows x 3; 3 loners
     groups = [(40, 10), (5, 3)]
