@@ -148,12 +148,13 @@ def bench_decode_lean(dev) -> List[Dict]:
         plan = ops.plan_cascade(np.asarray(ctxs, np.int32), tables.numpy(), Hq // Hkv) if shared else None
         ci = ops.CascadeInputs.from_plan(plan, dev) if plan is not None else None
 
-        def mk(lean, cas):
+        def mk(lean, cas, chunks=0):
             def f():
-                A.DECODE_LEAN = lean
+                A.DECODE_LEAN, A.LEAN_CHUNKS_PER_WAVE = lean, chunks
                 ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o, cascade=cas)
             return f
-        fns = {"part": mk(False, None), "lean": mk(True, None)}
+        fns = {"part": mk(False, None), "lean": mk(True, None, 0), "lean_dyn2": mk(True, None, 2),
+               "lean_dyn4": mk(True, None, 4)}
         if ci is not None:
             fns.update({"part_cascade": mk(False, ci), "lean_cascade": mk(True, ci)})
         ref = None
@@ -164,7 +165,27 @@ def bench_decode_lean(dev) -> List[Dict]:
             ref = o.float().clone() if ref is None else ref
             errs[k] = float((o.float() - ref).abs().max())
         ts = interleaved(fns, rounds=7, iters=20)
-        A.DECODE_LEAN = True
+        # mixed-step shape: the decode rows' attention on a side stream concurrently with a prefill
+        # attention (4 x 512 new tokens behind 2k context) on the main stream, as llama.py runs it
+        ptab, pkc, pvc, _ = _paged(4, 2560, 0, Hkv, D, dev, g)
+        pq = torch.randn((2048, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        pcu = torch.arange(0, 2049, 512, dtype=torch.int32, device=dev)
+        plens = torch.full((4,), 2560, dtype=torch.int32, device=dev)
+        po = torch.empty_like(pq)
+        side = torch.cuda.Stream()
+
+        def pair(f):
+            def g2():
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    f()
+                ops.prefill(pq, pcu, plens, ptab, pkc, pvc, 0.088, True, 512, out=po)
+                torch.cuda.current_stream().wait_stream(side)
+            return g2
+        tp = interleaved({"prefill_only": lambda: ops.prefill(pq, pcu, plens, ptab, pkc, pvc, 0.088, True, 512, out=po),
+                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean", "lean_dyn2", "lean_dyn4")}},
+                         rounds=7, iters=20)
+        A.DECODE_LEAN, A.LEAN_CHUNKS_PER_WAVE = True, 0
         uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2
         logical = sum(ctxs) * Hkv * D * 2 * 2
         row = {"op": "decode_lean_ab", "B": B, "ctx_range": [lo, hi], "ctx_mean": round(sum(ctxs) / B),
@@ -173,6 +194,7 @@ def bench_decode_lean(dev) -> List[Dict]:
             row[k + "_us"] = round(us, 1)
             row[k + "_GBps_unique"] = round(uniq / us / 1e3, 1)
             row[k + "_GBps_logical"] = round(logical / us / 1e3, 1)
+        row["concurrent_with_prefill_us"] = {k: round(v, 1) for k, v in tp.items()}
         print(json.dumps(row), flush=True)
         out.append(row)
     return out

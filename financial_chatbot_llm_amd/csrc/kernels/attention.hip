@@ -604,30 +604,44 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
   return LeanPlan{total, max(max(want, cap), min_per_wave)};
 }
 
-// grid (nwg), nwg % Hkv == 0: workgroup i serves kv head i % Hkv with 4 waves; wave hw of a head
-// owns that head's units [hw*per_wave, (hw+1)*per_wave)
+// grid (nwg), nwg % Hkv == 0: workgroup i serves kv head i % Hkv with 4 waves.  A head's units
+// are cut into chunks of per_wave blocks.  Static (chunks_per_wave == 0): wave hw of the head owns
+// chunk hw.  Dynamic (chunks_per_wave = k > 0): chunks are k times smaller and each wave claims
+// the next one from the head's counter (meta[h], one vector atomic per chunk) until none is left,
+// so workgroups that start late -- the grid shares the chip with a concurrent prefill attention
+// in mixed steps -- simply take fewer chunks.  Either way a chunk's partial slots depend only on
+// its index, and the merge kernel re-zeroes the counters for the next launch.
+constexpr int LEAN_META0 = 64;   // meta[0..64): per-head chunk counters; plan from meta[64]
+
 template <int D>
 __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o,
     int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
-    int min_per_wave) {
+    int min_per_wave, int chunks_per_wave) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
-  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, kv_start, B, gridDim.x / Hkv * 4, nparts, min_per_wave);
+  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, kv_start, B, gridDim.x / Hkv * 4 * max(chunks_per_wave, 1),
+                                nparts, min_per_wave);
   if (blockIdx.x == 0) {
-    for (int i = threadIdx.x; i <= B; i += 256) meta[i] = s_pre[i];
-    if (threadIdx.x == 0) meta[B + 1] = pl.per_wave;
+    for (int i = threadIdx.x; i <= B; i += 256) meta[LEAN_META0 + i] = s_pre[i];
+    if (threadIdx.x == 0) meta[LEAN_META0 + B + 1] = pl.per_wave;
   }
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const int h = blockIdx.x % Hkv;
-  const int hw = (blockIdx.x / Hkv) * 4 + (threadIdx.x >> 6);
   const int G = Hq / Hkv;
-  int u = hw * pl.per_wave;
+  const int nch = (pl.total + pl.per_wave - 1) / pl.per_wave;
+  auto claim = [&]() {
+    int v = 0;
+    if (lane == 0) v = atomicAdd(meta + h, 1);
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  int chunk = chunks_per_wave > 0 ? claim() : (blockIdx.x / Hkv) * 4 + (threadIdx.x >> 6);
+  while (chunk < nch) {   // no barrier below this point
+  int u = chunk * pl.per_wave;
   const int uend = min(pl.total, u + pl.per_wave);
-  if (u >= uend) return;   // no barrier below this point
   // row of unit u: the last b with s_pre[b] <= u (skips empty rows)
   int lo = 0, hi = B - 1;
   while (lo < hi) {
@@ -735,8 +749,8 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
           *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v;
         }
       } else {
-        const long pi = ((long)b * Hq + hq) * part_stride + (hw - seg0 / pl.per_wave);
-        PENNY_DASSERT(hw - seg0 / pl.per_wave < nparts);
+        const long pi = ((long)b * Hq + hq) * part_stride + (chunk - seg0 / pl.per_wave);
+        PENNY_DASSERT(chunk - seg0 / pl.per_wave < nparts);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(part_o + pi * D + 16 * dt + 4 * g) = o[dt];
         if (g == 0) {
@@ -750,18 +764,21 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
       ++b;
     } while (b < B - 1 && s_pre[b + 1] == s_pre[b]);
   }
+  chunk = chunks_per_wave > 0 ? claim() : nch;
+  }
 }
 
 // grid (Hq, B), D threads: merges a row's lean partials (slots 0..) and cascade chunks (slots
 // nparts..), skipping rows one wave already finished
 template <int D>
-__global__ void decode_lean_reduce_kernel(const int* __restrict__ meta, const int* __restrict__ ctx_lens,
+__global__ void decode_lean_reduce_kernel(int* __restrict__ meta, const int* __restrict__ ctx_lens,
                                           const int* __restrict__ kv_start, const float* __restrict__ part_m,
                                           const float* __restrict__ part_l, const float* __restrict__ part_o,
                                           bf16* __restrict__ out, int B, int Hq, int Hkv, int nparts,
                                           int part_stride, int chunk_blocks) {
   const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
-  const int pre = meta[b], n = meta[b + 1] - pre, pw = meta[B + 1];
+  if (b == 0 && hq == 0 && d < Hkv) meta[d] = 0;   // chunk counters for the next launch
+  const int pre = meta[LEAN_META0 + b], n = meta[LEAN_META0 + b + 1] - pre, pw = meta[LEAN_META0 + B + 1];
   const int s0 = kv_start ? kv_start[b] : 0;
   const int nc = s0 > 0 ? (s0 + chunk_blocks - 1) / chunk_blocks : 0;
   int np = 0;
@@ -982,7 +999,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      const int* cu_g, const int* g_ctx, const int* g_bt, const int* work,
                                      const int* nwork, int grid_work, int g_max_blocks, int chunk_blocks,
                                      int phases, int lean_grid, int* lean_meta, int lean_min_per_wave,
-                                     hipStream_t stream) {
+                                     int lean_chunks_per_wave, hipStream_t stream) {
   // phases: 1 cascade (shared-prefix tiles), 2 split-K decode, 4 merge -- the caller may run
   // phase 1 on a side stream concurrently with phase 2 (ops/attention.py), joining before 4
   if (B <= 0) return 0;
@@ -994,7 +1011,8 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   // lean_grid > 0: the work-balanced suffix kernel (decode_lean_kernel) and its merge replace
   // phases 2 and 4
   const bool lean = lean_grid > 0;
-  if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv))
+  if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv ||
+               Hkv > LEAN_META0 || lean_chunks_per_wave < 0))
     return (int)hipErrorInvalidValue;
   // measured (profiles/r1_decode_head_fast.txt): head-fastest wins at B <= 16 (18.5 vs 21.6 us at
   // ctx 2048 / 1024 shared), sequence-fastest at B >= 64 (a sequence's 8 heads of a KV block are
@@ -1015,7 +1033,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
     hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
                        kv_start, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,   \
                        part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,              \
-                       lean_min_per_wave);                                                                       \
+                       lean_min_per_wave, lean_chunks_per_wave);                                                 \
   if ((phases & 4) && lean)                                                                                     \
     hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, ctx_lens,       \
                        kv_start, part_m, part_l, part_o, (bf16*)out, B, Hq, Hkv, nparts, part_stride,            \

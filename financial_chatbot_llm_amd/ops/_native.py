@@ -44,7 +44,7 @@ _SIGS = {
     "penny_rope_kv_write_slabs": [P, c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P],
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                               c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P],
+                               c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P],
     "penny_sample": [P, c_int, c_long, P, P, P, P, P, P, c_int, c_int, P],
     "penny_topk_topp_threshold": [P, c_int, c_long, P, P, P, P, c_int, c_int, P],
     "penny_moe_route": [P, c_int, c_int, c_int, P, P, P, P, P],

@@ -213,7 +213,7 @@ class DecodeWorkspace:
     pb: int
     nparts: int
     part_stride: int = 0    # partition slots per (row, head): nparts suffix + cascade chunk slots
-    lean_meta: Optional[torch.Tensor] = None   # [max_batch + 2] int32: the lean kernel's plan
+    lean_meta: Optional[torch.Tensor] = None   # [64 + max_batch + 2] int32: chunk counters + lean plan
 
     def partitioning(self, B: int):
         """(pb, nparts) for a decode batch of B rows.  Batches of 32+ rows already fill the chip
@@ -239,7 +239,7 @@ class DecodeWorkspace:
         f = dict(dtype=torch.float32, device=device)
         return cls(torch.empty((max_batch, Hq, stride), **f), torch.empty((max_batch, Hq, stride), **f),
                    torch.empty((max_batch, Hq, stride, D), **f), pb, max(nparts, 2), stride,
-                   torch.zeros(max_batch + 2, dtype=torch.int32, device=device))
+                   torch.zeros(LEAN_META0 + max_batch + 2, dtype=torch.int32, device=device))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -392,6 +392,12 @@ DECODE_LEAN = os.environ.get("PENNY_DECODE_LEAN", "1") != "0"
 LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
+# 0 (default): one static chunk per wave.  k > 0: chunks k times smaller claimed from a per-head
+# atomic counter -- meant to absorb a concurrent prefill attention holding CUs, but the claim
+# round trip costs more than it saves: 185 vs 140 us at B=64 alone, 279 vs 249 us concurrent with
+# a prefill (profiles/r3_decode_lean_vs_partitioned.jsonl)
+LEAN_CHUNKS_PER_WAVE = int(os.environ.get("PENNY_DECODE_LEAN_CHUNKS", "0"))
+LEAN_META0 = 64             # lean_meta[0:64] per-head chunk counters (attention.hip LEAN_META0)
 _CU_COUNT = {}
 
 
@@ -431,12 +437,14 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         cas = ((N.ptr(c.kv_start), N.ptr(c.members), N.ptr(c.cu_g), N.ptr(c.g_ctx), N.ptr(c.g_bt), N.ptr(c.work),
                 N.ptr(c.nwork), c.grid, CASCADE_MAX_BLOCKS, CASCADE_CHUNK) if c is not None
                else (None, None, None, None, None, None, None, 0, 0, 0))
-        lean = DECODE_LEAN and B >= LEAN_MIN_B and ws.lean_meta is not None and ws.lean_meta.numel() >= B + 2
+        lean = (DECODE_LEAN and B >= LEAN_MIN_B and ws.lean_meta is not None
+                and ws.lean_meta.numel() >= LEAN_META0 + B + 2)
         pb, nparts = ws.partitioning(B) if (c is None and not lean) else (ws.pb, ws.nparts)
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale), *cas]
-        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE) if lean else (0, None, 1))
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE)
+                     if lean else (0, None, 1, 0))
         if c is None:
             N.call("penny_attention_decode", *args, 7, *lean_args, N.stream())
         else:
