@@ -13,12 +13,16 @@ JSON skeleton, the tool name, unambiguous keys, the closing braces) are appended
 sampling and computed as one chunk (jump-forward decoding) -- for scripted and sampled outputs
 alike; ``jump_forward=False`` decodes them one step each.
 
+Decide calls also decode with prompt-lookup speculation (``engine.speculative``, up to
+``prompt_lookup`` draft tokens per step): a tool call's arguments mostly copy the user's words.
+
 ``ephemeral_kv`` (agent hint): the prompt carries this turn's tool results, which the next turn
 will not repeat, so its freshly computed KV blocks are recycled before any other cached prefix
 (``PyBlockManager.free``) -- the conversation prefixes that DO recur survive in HBM.
 """
 from __future__ import annotations
 
+import os
 from typing import AsyncIterator, Callable, Optional, Sequence
 
 from ..agent.grammar import ToolCallGrammar, jump_mask
@@ -37,13 +41,15 @@ class EngineLLM(LLMBackend):
                  decide_script: Optional[Callable[[Sequence[ChatMessage], Sequence[Tool]], str]] = None,
                  respond_ignore_eos: bool = False, respond_tokens: Optional[int] = None,
                  stream_chunk_tokens: int = 1, history_token_budget: Optional[int] = None,
-                 jump_forward: bool = True):
+                 jump_forward: bool = True, prompt_lookup: Optional[int] = None):
         self.engine = engine
         self.tok = engine.tokenizer
         self.encoder = ChatEncoder(self.tok)
         self.max_model_len = max_model_len
         self.history_token_budget = history_token_budget
         self.jump_forward = jump_forward
+        self.prompt_lookup = (int(os.environ.get("PENNY_PROMPT_LOOKUP", "8")) if prompt_lookup is None
+                              else prompt_lookup)
         self.decide_script = decide_script
         self.respond_ignore_eos = respond_ignore_eos
         self.respond_tokens = respond_tokens
@@ -83,7 +89,8 @@ class EngineLLM(LLMBackend):
             if grammar is not None:
                 jump = jump_mask(forced, self.tok.decode, grammar, self.eot)
         params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced,
-                                forced_jump=jump, grammar=grammar, ephemeral_kv=bool(kw.get("ephemeral_kv")))
+                                forced_jump=jump, grammar=grammar, ephemeral_kv=bool(kw.get("ephemeral_kv")),
+                                prompt_lookup=self.prompt_lookup)
         out = await self.engine.generate_all(ids, params)
         self._account(kw.get("purpose", "decide"), len(ids), out.seq)
         text = self.tok.decode(out.seq.output_ids)

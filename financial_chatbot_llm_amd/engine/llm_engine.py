@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import time
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence as Seq
+from typing import Dict, List, Optional, Sequence as Seq, Tuple
 
 import torch
 
@@ -23,12 +23,14 @@ from ..parallel.dist import state as pstate
 from ..utils.logging import get_logger
 from ..utils.profiling import StepProfiler, marker
 from .block_manager import make_block_manager
-from .model_runner import ModelRunner, build_step_inputs
+from .model_runner import ModelRunner, build_step_inputs, sample_rows
 from .scheduler import Scheduler, StepCostModel
-from .sequence import PENDING, SamplingParams, Sequence
+from .sequence import PENDING, SamplingParams, Sequence, SeqStatus
+from .speculative import PromptLookup, accept_draft
 from .tokenizer import BaseTokenizer, load_tokenizer
 
 logger = get_logger(__name__)
+MAX_DRAFT = 16          # draft tokens per speculative chunk (ModelRunner sizes its sampler rows for it)
 
 
 @dataclass
@@ -80,6 +82,7 @@ class LLMEngine:
                                   cascade=cfg.enable_cascade_attention)
         self.requests: Dict[str, Sequence] = {}
         self.timing = {"prepare_s": 0.0, "execute_s": 0.0, "post_s": 0.0}   # host-side step anatomy
+        self.spec_stats = {"proposed": 0, "accepted": 0}   # prompt-lookup draft tokens
         self.async_scheduling = bool(getattr(cfg, "async_scheduling", True))
         self._inflight = None      # (batch, samplers, PendingStep) of the step on the GPU
         self.ps = pstate()
@@ -127,8 +130,26 @@ class LLMEngine:
 
     # -- overlap (one-step lookahead) ------------------------------------------------------------
     def _samplers(self, batch) -> List[Sequence]:
-        """Rows of a batch that sample a token, in sampled-vector order."""
-        return [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
+        """Rows of a batch that sample a token, in sampled-vector order (a speculative chunk's
+        sequence repeats once per verified position)."""
+        rows: List[Sequence] = []
+        for seq, start, n in batch.prefill:
+            if start + n == seq.num_tokens:
+                rows.extend([seq] * sample_rows(seq, n))
+        return rows + list(batch.decode)
+
+    @staticmethod
+    def _group(samplers: List[Sequence], sampled: Optional[List[int]] = None):
+        """(seq, first row, its sampled ids) per sequence of a sampler list."""
+        out = []
+        i = 0
+        while i < len(samplers):
+            j = i + 1
+            while j < len(samplers) and samplers[j] is samplers[i]:
+                j += 1
+            out.append((samplers[i], i, sampled[i:j] if sampled is not None else None))
+            i = j
+        return out
 
     def _ends_after(self, seq: Sequence, tok: Optional[int], run: int = 1) -> bool:
         """Will the token(s) about to be appended certainly finish ``seq``?  ``tok``: the known
@@ -188,19 +209,84 @@ class LLMEngine:
             run.append(self.tokenizer.special.get("<|eot_id|>", next(iter(self.eos_ids))))
         seq.jump_queue = run
 
+    # -- prompt-lookup speculation (engine.speculative) -------------------------------------------
+    def _propose(self, seq: Sequence, after: Seq[int] = (), min_ngram: int = 0) -> List[int]:
+        """Draft tokens to follow output + ``after``, capped so the chunk never reaches max_tokens,
+        max_model_len or the teacher-forced output's last token; cut before any stop token (the
+        model's own stop token then arrives as the bonus sample and ends the sequence as usual)."""
+        p = seq.params
+        if p.prompt_lookup <= 0 or seq.finished:
+            return []
+        k = len(seq.output_ids) + len(after)
+        room = min(p.prompt_lookup, MAX_DRAFT, p.max_tokens - k - 1, self.cfg.max_model_len - seq.num_tokens - len(after) - 2)
+        if p.forced_output is not None:
+            room = min(room, len(p.forced_output) - k - 1)
+        if room <= 0:
+            return []
+        if seq.spec_lookup is None:
+            seq.spec_lookup = PromptLookup(seq.prompt_ids)
+        draft = seq.spec_lookup.propose(list(seq.output_ids) + list(after), room, min_ngram)
+        if not p.ignore_eos:
+            stops = self.eos_ids | set(p.stop_token_ids)
+            for i, t in enumerate(draft):
+                if t in stops:
+                    draft = draft[:i]
+                    break
+        return draft
+
+    def _model_tokens(self, seq: Sequence, base: int, toks: Seq[int], m: int) -> List[int]:
+        """The model's tokens at output positions base .. base+m-1: the teacher-forced ones, or
+        the samples of the verified rows."""
+        forced = seq.params.forced_output
+        if forced is not None:
+            return list(forced[base:base + m])
+        return [int(t) for t in toks[:m]]
+
+    def _verify(self, seq: Sequence, toks: Seq[int]) -> Tuple[List[int], int]:
+        """Resolve a speculative chunk of ``seq`` (its draft is the output tail): drop the rejected
+        draft tokens and clamp ``num_computed`` to the valid prefix.  Returns (accepted draft,
+        bonus sample: the model's token after the accepted prefix)."""
+        m = seq.spec_rows - 1
+        base = len(seq.output_ids) - m
+        draft = seq.output_ids[base:]
+        j = accept_draft(draft, self._model_tokens(seq, base, toks, m))
+        del seq.output_ids[base + j:]
+        seq.spec_rows = 0
+        seq.spec_proposed += m
+        seq.spec_accepted += j
+        self.spec_stats["proposed"] += m
+        self.spec_stats["accepted"] += j
+        seq.num_computed = min(seq.num_computed, seq.num_tokens)
+        return draft[:j], int(toks[j])
+
+    def _sit_out(self, seq: Sequence) -> bool:
+        """Overlap mode, sampled output: skip the next step so the NEXT token is known at the
+        following launch and a draft can ride with it -- only inside a copy span (the last 2+
+        tokens occur earlier in the prompt), where a draft will likely be accepted."""
+        if seq.params.prompt_lookup <= 0 or PENDING in seq.output_ids[-3:]:
+            return False
+        return bool(self._propose(seq, min_ngram=2))
+
     def _advance(self, batch, samplers: List[Sequence]) -> None:
         """Host view of an in-flight step as if it had completed: KV written (num_computed), full
         blocks committed, one placeholder token per sampler (device-gathered by the next step)
         -- or the known run of tokens (teacher-forced / grammar-forced), appended at once; a
-        run longer than one token is computed as a prefill chunk by the next step."""
+        run longer than one token is computed as a prefill chunk by the next step.  A known run
+        also carries a prompt-lookup draft: teacher-forced drafts are verified right here (the
+        model's tokens are known), so only the accepted part is kept after the chunk launches."""
         for seq, start, n in batch.prefill:
             if not seq.finished:
-                seq.num_computed = start + n
+                seq.num_computed = min(start + n, seq.num_tokens)
         for seq in batch.decode:
             if not seq.finished:
                 seq.num_computed = seq.num_tokens
-        for i, seq in enumerate(samplers):
+        for seq, i, _ in self._group(samplers):
             if seq.finished:
+                continue
+            if seq.spec_rows > 1:              # sampled draft in flight: verified on resolve
+                seq.awaiting = True
+                seq.jump_tail = []
+                self.bm.commit(seq)
                 continue
             run = self._known_run(seq)
             tok = run[-1] if run else None
@@ -208,9 +294,23 @@ class LLMEngine:
                 seq.awaiting = True            # sits out the next step; resolved by _resolve
                 seq.jump_tail = run
             elif run:
-                seq.output_ids.extend(run)
+                # a draft rides with a teacher-forced run only: sampled runs (grammar jumps) leave
+                # the model's tokens unknown at launch
+                draft = self._propose(seq, run) if seq.params.forced_output is not None else []
+                j = accept_draft(draft, self._model_tokens(seq, len(seq.output_ids) + len(run), (), len(draft)))
+                seq.output_ids.extend(run + draft)
                 seq.pending_src = -1
-                seq.last_run = run
+                seq.last_run = run + draft[:j]
+                seq.spec_rows = len(draft) + 1 if draft else 0
+                seq.spec_reject = len(draft) - j
+                if draft:
+                    seq.spec_proposed += len(draft)
+                    seq.spec_accepted += j
+                    self.spec_stats["proposed"] += len(draft)
+                    self.spec_stats["accepted"] += j
+            elif self._sit_out(seq):
+                seq.awaiting = True
+                seq.jump_tail = []
             else:
                 seq.output_ids.append(PENDING)
                 seq.pending_src = i
@@ -234,15 +334,28 @@ class LLMEngine:
     def _resolve(self, samplers: List[Sequence], sampled: List[int]) -> List[StepOutput]:
         now = time.perf_counter()
         outs: List[StepOutput] = []
-        for seq, tok in zip(samplers, sampled):
+        for seq, _, toks in self._group(samplers, sampled):
+            tok = toks[-1]
             if seq.finished:                   # aborted (or finished) while in flight
                 continue
             was_sampled = False
+            sat_out = False                    # not in the step launched just now: may draft
             if seq.awaiting:
                 seq.awaiting = False
-                new = seq.jump_tail or [int(tok)]
-                seq.jump_tail = []
-                seq.output_ids.extend(new)
+                sat_out = True
+                if seq.spec_rows > 1:          # sampled draft: keep the accepted prefix + bonus
+                    acc, bonus = self._verify(seq, toks)
+                    seq.output_ids.append(bonus)
+                    new = acc + [bonus]
+                    was_sampled = True
+                elif seq.jump_tail:
+                    new = seq.jump_tail
+                    seq.jump_tail = []
+                    seq.output_ids.extend(new)
+                else:
+                    new = [int(tok)]
+                    seq.output_ids.extend(new)
+                    was_sampled = seq.params.forced_output is None
             elif seq.pending_src >= 0:
                 new = [int(tok)]
                 seq.output_ids[-1] = new[0]
@@ -262,6 +375,11 @@ class LLMEngine:
                 self.requests.pop(seq.request_id, None)
             elif was_sampled:
                 self._stage_grammar(seq)    # used by the next launch (overrides its sample)
+                if sat_out and not seq.jump_queue and seq.status == SeqStatus.RUNNING:
+                    draft = self._propose(seq)
+                    if draft:                  # rides with the just-known token next step
+                        seq.output_ids.extend(draft)
+                        seq.spec_rows = len(draft) + 1
             outs.append(StepOutput(seq.request_id, new, reason is not None, reason, seq))
         return outs
 
@@ -279,6 +397,15 @@ class LLMEngine:
                 comm.broadcast_step(si)
             t1 = time.perf_counter()
             launched = (batch, self._samplers(batch), self.runner.launch(si))
+            # teacher-forced drafts were verified at _advance: drop the rejected tail now that the
+            # chunk (all of it, as a real verification computes) is on its way
+            for seq, _, _ in batch.prefill:
+                if seq.spec_reject:
+                    del seq.output_ids[len(seq.output_ids) - seq.spec_reject:]
+                    seq.spec_reject = 0
+                    seq.spec_rows = 0
+                elif seq.spec_rows and seq.params.forced_output is not None:
+                    seq.spec_rows = 0
         t2 = time.perf_counter()
         outs: List[StepOutput] = []
         if prev is not None:
@@ -307,13 +434,16 @@ class LLMEngine:
         tm["prepare_s"] += t1 - t0
         tm["execute_s"] += now - t1
         outs: List[StepOutput] = []
+        samplers = self._samplers(batch)   # before num_computed moves (sampled-vector order)
         for seq, start, n in batch.prefill:
             seq.num_computed = start + n
         for seq in batch.decode:
             seq.num_computed = seq.num_tokens
-        # sampled order: completed prefills (in batch order), then decodes
-        samplers = [seq for seq, start, n in batch.prefill if start + n == seq.num_tokens] + list(batch.decode)
-        for seq, tok in zip(samplers, sampled):
+        for seq, _, toks in self._group(samplers, sampled):
+            acc: List[int] = []
+            tok = toks[-1]
+            if seq.spec_rows > 1:
+                acc, tok = self._verify(seq, toks)
             known = self._known_run(seq)
             run = known or [int(tok)]
             seq.output_ids.extend(run)
@@ -332,7 +462,12 @@ class LLMEngine:
             if reason is not None:
                 self.scheduler.finish(seq, reason)
                 self.requests.pop(seq.request_id, None)
-            outs.append(StepOutput(seq.request_id, run, reason is not None, reason, seq))
+            else:
+                draft = self._propose(seq)
+                if draft:
+                    seq.output_ids.extend(draft)
+                    seq.spec_rows = len(draft) + 1
+            outs.append(StepOutput(seq.request_id, acc + run, reason is not None, reason, seq))
         for seq, start, n in batch.prefill:
             if start + n < seq.num_tokens:
                 self.bm.commit(seq)
@@ -364,6 +499,7 @@ class LLMEngine:
                 "kv_blocks": self.bm.num_blocks, "kv_evictions": int(getattr(self.bm, "evictions", 0)),
                 "preemptions": self.scheduler.num_preemptions,
                 "time_capped_steps": self.scheduler.num_capped_steps,
+                "spec_draft_tokens": self.spec_stats["proposed"], "spec_accepted_tokens": self.spec_stats["accepted"],
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
                 "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),

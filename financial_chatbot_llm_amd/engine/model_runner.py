@@ -106,6 +106,12 @@ def _slots(seq: Sequence, start: int, n: int) -> List[int]:
     return [bt[p // KV_BS] * KV_BS + p % KV_BS for p in range(start, start + n)]
 
 
+def sample_rows(seq, n: int) -> int:
+    """Sampled positions at the end of a sequence's final chunk of n tokens: the whole draft + 1
+    for a speculative chunk (engine.speculative), else the last token only."""
+    return max(1, min(seq.spec_rows, n))
+
+
 def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
     ids: List[int] = []
     pos: List[int] = []
@@ -124,11 +130,15 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
         tables_p.append(seq.block_table)
         max_q = max(max_q, n)
         if start + n == seq.num_tokens:
-            logits_idx.append(cu[-1] - 1)
-            temps.append(seq.params.temperature)
-            seeds.append(seq.step_seed())
-            tk.append(seq.params.top_k)
-            tp.append(seq.params.top_p)
+            # a speculative chunk samples its last spec_rows positions (verification), others one
+            r = sample_rows(seq, n)
+            k0 = len(seq.output_ids) - r + 1
+            for i in range(r):
+                logits_idx.append(cu[-1] - r + i)
+                temps.append(seq.params.temperature)
+                seeds.append(seq.step_seed_at(k0 + i))
+                tk.append(seq.params.top_k)
+                tp.append(seq.params.top_p)
     Tp = cu[-1]
     ctx_d, tables_d, src = [], [], []
     for j, seq in enumerate(batch.decode):
@@ -235,7 +245,8 @@ class ModelRunner:
         self._gpu_timing = self.on_gpu and os.environ.get("PENNY_STEP_GPU_TIMING", "0") == "1"
         # sampled ids of the latest step stay on the device: the next step gathers its decode ids
         # from here when it was launched before this one's ids reached the host (overlap mode)
-        self.max_samplers = max(self.max_decode_batch, max_decode_batch) + 1024
+        # a speculative chunk samples draft + 1 rows (engine.speculative: drafts <= 16 tokens)
+        self.max_samplers = 17 * max(self.max_decode_batch, max_decode_batch) + 1024
         self.last_sampled = torch.zeros(self.max_samplers, dtype=torch.int32, device=self.device)
         # one slot past the sampled ids carries the custom all-reduce's timeout flag back with them
         self._pinned_out = ([torch.zeros(self.max_samplers + 1, dtype=torch.int32).pin_memory() for _ in range(2)]

@@ -113,6 +113,8 @@ class Scheduler:
         seq.status = SeqStatus.FINISHED
 
     def _preempt(self, seq: Sequence, batch: ScheduledBatch) -> None:
+        if seq.spec_rows and not seq.awaiting:
+            seq.drop_draft()                # not launched: recomputed later without it
         self.running.remove(seq)
         self.bm.free(seq)
         seq.num_computed = 0
@@ -140,6 +142,15 @@ class Scheduler:
             self.bm.grow(seq, seq.num_tokens)
             batch.decode.append(seq)
             budget -= 1
+        # 1b) speculative chunks (last token + prompt-lookup draft, engine.speculative): decode-class
+        # rows, scheduled whole -- every draft position must be sampled in the same step
+        for seq in sorted((s for s in self.running if s.spec_rows and not s.awaiting
+                           and s.remaining_prefill >= s.spec_rows), key=lambda s: s.arrival):
+            n = seq.remaining_prefill
+            if not self.bm.grow(seq, seq.num_tokens):
+                continue
+            batch.prefill.append((seq, seq.num_computed, n))
+            budget -= n
         # step-time bound: a decide call is decoding -> keep this step short (its next token waits
         # for it); the cap never drops below min_prefill_tokens, so prefill always progresses
         if self.cost.target_ms > 0 and any(s.params.max_tokens <= self.short_output_tokens for s in batch.decode):
@@ -148,8 +159,8 @@ class Scheduler:
                 budget = cap
                 self.num_capped_steps += 1
         # 2) continuing prefills
-        for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting),
-                          key=lambda s: s.arrival):
+        for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting
+                           and not s.spec_rows), key=lambda s: s.arrival):
             if budget <= 0:
                 break
             n = min(seq.remaining_prefill, budget)
@@ -196,7 +207,7 @@ class Scheduler:
         if total <= q or r == 0:
             return
         seq, start, n = batch.prefill[-1]
-        if n <= r:
+        if n <= r or seq.spec_rows:
             return
         batch.prefill[-1] = (seq, start, n - r)
         seq.num_prefilled -= r

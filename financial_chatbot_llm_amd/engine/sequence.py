@@ -26,6 +26,9 @@ class SamplingParams:
     # KV retention hint: the prompt's uncached part will not recur (e.g. the respond prompt around
     # a one-off retrieval context), so its blocks are recycled before any other cached block
     ephemeral_kv: bool = False
+    # prompt-lookup speculative decoding (engine.speculative): up to this many draft tokens copied
+    # from the prompt are verified per step (0 = off)
+    prompt_lookup: int = 0
 
 
 class SeqStatus(enum.Enum):
@@ -66,6 +69,25 @@ class Sequence:
         self.jump_queue: List[int] = []    # grammar-forced tokens staged for the next launch
         self.last_run: List[int] = []      # tokens appended at launch (emitted on resolve)
         self.jump_tail: List[int] = []     # final run of an awaiting sequence
+        # prompt-lookup speculation: spec_rows -- sampled positions at the tail of the next chunk
+        # (draft + 1; 0 = an ordinary row); spec_reject -- draft tokens already known to be rejected
+        # at launch (teacher-forced output) and dropped once the chunk is launched
+        self.spec_rows = 0
+        self.spec_reject = 0
+        self.spec_lookup = None
+        self.spec_proposed = 0
+        self.spec_accepted = 0
+
+    def drop_draft(self) -> None:
+        """Forget a prompt-lookup draft that was appended but never launched (preemption)."""
+        m = self.spec_rows - 1
+        if m > 0:
+            accepted = m - self.spec_reject
+            del self.output_ids[len(self.output_ids) - m:]
+            if self.last_run and accepted:
+                self.last_run = self.last_run[:len(self.last_run) - accepted]
+        self.spec_rows = 0
+        self.spec_reject = 0
 
     @property
     def all_ids(self) -> List[int]:
@@ -92,4 +114,8 @@ class Sequence:
 
     def step_seed(self) -> int:
         """Per-token seed: depends only on the request and the position (batch-invariant)."""
-        return (self.seed * 0x9E3779B1 + len(self.output_ids) * 0x85EBCA77 + 1) & 0x7FFFFFFFFFFFFFFF
+        return self.step_seed_at(len(self.output_ids))
+
+    def step_seed_at(self, k: int) -> int:
+        """Seed of the sample that becomes output token k."""
+        return (self.seed * 0x9E3779B1 + k * 0x85EBCA77 + 1) & 0x7FFFFFFFFFFFFFFF

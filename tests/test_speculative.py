@@ -1,0 +1,95 @@
+"""Prompt-lookup speculative decoding (engine.speculative, LLMEngine).
+
+* the n-gram draft source finds the most recent earlier occurrence of the output's tail;
+* teacher-forced decide outputs (the benchmark's scripted tool calls, whose arguments copy the
+  user's words) come out identical with fewer engine steps, in both step modes;
+* sampled outputs (greedy and seeded temperature sampling) are identical with and without
+  speculation -- drafts are verified against the model's own samples at the same seeds -- and
+  drafts do get accepted (a random tiny model falls into repetition loops it can copy from);
+* a draft never runs past max_tokens and never carries a stop token.
+"""
+import pytest
+
+from financial_chatbot_llm_amd.agent import scripted_decision
+from financial_chatbot_llm_amd.agent.grammar import ToolCallGrammar, jump_mask
+from financial_chatbot_llm_amd.agent.toolcall import format_tool_call
+from financial_chatbot_llm_amd.config import EngineConfig
+from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
+from financial_chatbot_llm_amd.engine.speculative import PromptLookup, accept_draft
+from financial_chatbot_llm_amd.engine.tokenizer import SyntheticLlamaTokenizer
+from financial_chatbot_llm_amd.tools import make_retrieval_tool
+
+BASE = dict(model="llama-tiny", device="cpu", max_model_len=1024, max_num_batched_tokens=256,
+            use_cuda_graph=False, max_num_seqs=8, num_kv_blocks=96)
+TOK = SyntheticLlamaTokenizer()
+EOT = TOK.special["<|eot_id|>"]
+RET = make_retrieval_tool(None)
+
+
+def test_prompt_lookup_most_recent_longest_match():
+    pl = PromptLookup([5, 6, 7, 8, 1, 2, 5, 6, 9, 9, 4])
+    assert pl.propose([5, 6], 3) == [9, 9, 4]          # 2-gram (5, 6): most recent occurrence
+    assert pl.propose([7], 2) == [8, 1]
+    assert pl.propose([3], 4) == []
+    assert pl.propose([2, 5, 6], 2, min_ngram=2) == [9, 9]
+    assert pl.propose([1, 3], 2, min_ngram=2) == []     # no 2-gram match
+    assert accept_draft([1, 2, 3], [1, 2, 4]) == 2 and accept_draft([], [1]) == 0
+
+
+def _run(params_list, prompts, mode, **cfg):
+    eng = LLMEngine(EngineConfig(async_scheduling=mode, seed=0, **{**BASE, **cfg}))
+    seqs = [eng.add_request(f"r{i}", p, sp) for i, (p, sp) in enumerate(zip(prompts, params_list))]
+    while any(not s.finished for s in seqs) or eng.has_work():
+        eng.step()
+    return seqs, eng
+
+
+@pytest.mark.parametrize("mode", [True, False])
+def test_forced_decide_identical_with_fewer_steps(mode):
+    g = ToolCallGrammar([RET])
+    qs = ["What did I spend on groceries last month?", "Show me my recent transactions at Amazon.",
+          "How should I invest for retirement?"]
+    forced, prompts = [], []
+    for i, q in enumerate(qs):
+        call = scripted_decision(q)
+        f = TOK.encode(format_tool_call(call) if call else "No tool call", allow_special=False) + [EOT]
+        forced.append(f)
+        prompts.append(list(range(300 + 7 * i, 340 + 7 * i)) + TOK.encode(" user: " + q, allow_special=False))
+
+    def params(lookup):
+        return [SamplingParams(temperature=0.5, max_tokens=96, forced_output=f, forced_jump=jump_mask(f, TOK.decode, g, EOT),
+                               grammar=g, prompt_lookup=lookup) for f in forced]
+    a, ea = _run(params(0), prompts, mode)
+    b, eb = _run(params(8), prompts, mode)
+    for sa, sb, f in zip(a, b, forced):
+        assert sa.output_ids == f and sb.output_ids == f
+        assert sa.finish_reason == sb.finish_reason == "stop"
+    assert eb.spec_stats["accepted"] >= 6
+    assert eb.runner.stats["steps"] < ea.runner.stats["steps"]
+
+
+@pytest.mark.parametrize("mode", [True, False])
+@pytest.mark.parametrize("temperature", [0.0, 0.8])
+def test_sampled_outputs_identical_with_speculation(mode, temperature):
+    prompts = [[400 + (i * 13) % 50 for i in range(60)] + [900 + i for i in range(20)],
+               [700 + (i * 7) % 30 for i in range(90)]]
+
+    def params(lookup):
+        return [SamplingParams(temperature=temperature, max_tokens=48, ignore_eos=True, seed=11 + i,
+                               prompt_lookup=lookup) for i in range(len(prompts))]
+    a, _ = _run(params(0), prompts, mode)
+    b, eb = _run(params(8), prompts, mode)
+    for sa, sb in zip(a, b):
+        assert sa.output_ids == sb.output_ids
+        assert len(sb.output_ids) == 48
+    if temperature == 0.0:
+        assert eb.spec_stats["accepted"] > 0            # greedy loops get copied
+
+
+def test_draft_respects_max_tokens_and_stops():
+    eng = LLMEngine(EngineConfig(async_scheduling=False, seed=0, **BASE))
+    seq = eng.add_request("r", [9, 1, 2, 3, EOT, 7, 4, 5, 6, 7, 8, 9, 10], SamplingParams(max_tokens=6, prompt_lookup=8))
+    seq.output_ids = [1, 2]
+    assert eng._propose(seq) == [3]                       # cut before the stop token
+    seq.output_ids = [4]
+    assert eng._propose(seq) == [5, 6, 7, 8]              # k=1 -> room = 6 - 1 - 1 = 4
