@@ -6,7 +6,9 @@ and a plot call repeats column names of the retrieved rows.  Every copied token 
 cost one full engine step on the TTFT-critical path.
 
 Proposal: the most recent earlier occurrence of the sequence's last n tokens (n = 3, 2, 1) in
-prompt + output; the tokens that followed it are the draft (up to ``k``).  Verification: the
+prompt + output; the tokens that followed it are the draft (up to ``k``).  Longer n-grams win
+unless a shorter one occurs more than ``recency`` tokens later (the user's latest message sits at
+the end of the prompt, the few-shot examples thousands of tokens above it).  Verification: the
 draft is appended after the next token and computed as ONE chunk whose last ``len(draft) + 1``
 positions are all sampled; draft token i is accepted while it equals the token the model sampled
 at the position before it, and the first mismatch's sample is the bonus token.  The output is
@@ -26,16 +28,18 @@ class PromptLookup:
     numpy array; each proposal is a vectorised match of the last token plus a check of the n-1
     tokens before it (~20 us on a 7k-token prompt)."""
 
-    def __init__(self, prompt_ids: Seq[int], max_ngram: int = 3, min_ngram: int = 1):
+    def __init__(self, prompt_ids: Seq[int], max_ngram: int = 3, min_ngram: int = 1, recency: int = 0):
         self.prompt = np.asarray(prompt_ids, dtype=np.int64)
         self.max_ngram = max_ngram
         self.min_ngram = min_ngram
+        self.recency = recency
 
     def propose(self, output_ids: Seq[int], k: int, min_ngram: int = 0) -> List[int]:
         if k <= 0:
             return []
         ids = np.concatenate([self.prompt, np.asarray(output_ids, dtype=np.int64)]) if output_ids else self.prompt
         L = len(ids)
+        best_e, best_n = -1, 0
         for n in range(min(self.max_ngram, L - 1), max(min_ngram, self.min_ngram) - 1, -1):
             pat = ids[L - n:]
             # candidate ends: earlier positions e (< L - 1) with ids[e] == last token
@@ -45,12 +49,17 @@ class PromptLookup:
                 if not len(ends):
                     break
                 ends = ends[ids[ends - back] == pat[-1 - back]]
-            if len(ends):
-                e = int(ends[-1])              # most recent occurrence
-                draft = ids[e + 1:e + 1 + k]
-                if len(draft):
-                    return draft.tolist()
-        return []
+            if len(ends) and ends[-1] + 1 < L - 1:
+                e = int(ends[-1])              # most recent occurrence of this n-gram
+                if not self.recency:
+                    best_e, best_n = e, n
+                    break
+                # recency: a shorter n-gram wins if it occurs later by more than `recency` tokens
+                if best_e < 0 or e > best_e + self.recency:
+                    best_e, best_n = e, n
+        if best_e < 0:
+            return []
+        return ids[best_e + 1:best_e + 1 + k].tolist()
 
 
 def accept_draft(draft: Seq[int], model_tokens: Seq[int]) -> int:

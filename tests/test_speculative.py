@@ -34,6 +34,10 @@ def test_prompt_lookup_most_recent_longest_match():
     assert pl.propose([2, 5, 6], 2, min_ngram=2) == [9, 9]
     assert pl.propose([1, 3], 2, min_ngram=2) == []     # no 2-gram match
     assert accept_draft([1, 2, 3], [1, 2, 4]) == 2 and accept_draft([], [1]) == 0
+    # recency: the 1-gram (6,) 300 tokens after the 2-gram (5, 6) wins at recency 256, not at 0
+    ids = [5, 6, 1] + [0] * 300 + [6, 2]
+    assert PromptLookup(ids).propose([5, 6], 1) == [1]
+    assert PromptLookup(ids, recency=256).propose([5, 6], 1) == [2]
 
 
 def _run(params_list, prompts, mode, **cfg):
