@@ -236,6 +236,10 @@ def main(argv=None) -> int:
             "plots": {"ok": sum(r["plots_ok"] for r in allr), "failed": sum(r["plots_failed"] for r in allr)},
             "ttft_p50_breakdown_ms": {k: round(1e3 * statistics.median(v), 1) if v else None
                                       for k, v in allr[0]["stages"].items()},
+            "ttft_p90_ms": None if not ttfts else round(1e3 * ttfts[min(len(ttfts) - 1, int(0.9 * len(ttfts)))], 1),
+            # per-stage p99 (each stage's own tail; they need not come from the same turns)
+            "ttft_stage_p99_ms": {k: round(1e3 * sorted(v)[min(len(v) - 1, int(0.99 * len(v)))], 1) if v else None
+                                  for k, v in allr[0]["stages"].items()},
             "prompt_tokens_rank0": allr[0]["tokens"],
             "engine_rank0": allr[0]["engine"],
         }

@@ -32,7 +32,7 @@ from ..tools.base import Tool
 from ..wire import ChatMessage
 from .async_engine import AsyncEngine
 from .chat_template import ChatEncoder
-from .sequence import SamplingParams
+from .sequence import TURN_START, SamplingParams
 from .tokenizer import IncrementalDetokenizer
 
 
@@ -90,7 +90,7 @@ class EngineLLM(LLMBackend):
                 jump = jump_mask(forced, self.tok.decode, grammar, self.eot)
         params = SamplingParams(temperature=temperature, max_tokens=max_tokens, forced_output=forced,
                                 forced_jump=jump, grammar=grammar, ephemeral_kv=bool(kw.get("ephemeral_kv")),
-                                prompt_lookup=self.prompt_lookup)
+                                prompt_lookup=self.prompt_lookup, priority_ts=TURN_START.get())
         out = await self.engine.generate_all(ids, params)
         self._account(kw.get("purpose", "decide"), len(ids), out.seq)
         text = self.tok.decode(out.seq.output_ids)
@@ -101,7 +101,7 @@ class EngineLLM(LLMBackend):
         n = self.respond_tokens or max_tokens
         ids = self._encode(messages, None, n)
         params = SamplingParams(temperature=temperature, max_tokens=n, ignore_eos=self.respond_ignore_eos,
-                                ephemeral_kv=bool(kw.get("ephemeral_kv")))
+                                ephemeral_kv=bool(kw.get("ephemeral_kv")), priority_ts=TURN_START.get())
         detok = IncrementalDetokenizer(self.tok)
         buf, k = [], 0
         async for o in self.engine.generate(ids, params):

@@ -13,7 +13,10 @@ Admission order (TTFT): preempted sequences first, then SHORT-OUTPUT requests --
 decide call (``max_tokens <= short_output_tokens``: a tool call or "No tool call") gates the whole
 turn's TTFT and its prompt is mostly prefix-cached, so it should not queue behind long respond
 prefills -- then everything else, each class FCFS.  Aging keeps it starvation-free: a request
-that has waited ``aging_s`` joins the first class.
+that has waited ``aging_s`` joins the first class.  Within a class the key is the request's
+``priority_time``: the start of the user turn it serves when the serving layer provides one
+(``sequence.TURN_START``), so the respond prefill of an older turn goes before the decide
+prefills of newer turns -- the oldest TTFT clock first.
 
 Step-time bound (``StepCostModel``, off unless ``step_time_target_ms`` > 0): every token of a
 decide call costs one engine step, so its latency is (tokens) x (step time) -- and a mixed step
@@ -92,7 +95,7 @@ class Scheduler:
             cls = 1
         else:
             cls = 2
-        return (cls, seq.arrival)
+        return (cls, seq.priority_time)
 
     def add(self, seq: Sequence) -> None:
         if seq.num_tokens >= self.max_model_len:
@@ -160,7 +163,7 @@ class Scheduler:
                 self.num_capped_steps += 1
         # 2) continuing prefills
         for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting
-                           and not s.spec_rows), key=lambda s: s.arrival):
+                           and not s.spec_rows), key=lambda s: s.priority_time):
             if budget <= 0:
                 break
             n = min(seq.remaining_prefill, budget)

@@ -1,11 +1,19 @@
 """Request / sequence state for the continuous-batching engine."""
 from __future__ import annotations
 
+import contextvars
 import enum
 import itertools
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence as Seq
+
+
+# Start of the user turn a request belongs to (time.perf_counter), set by the serving layer for
+# everything the turn awaits (serving.worker): the scheduler orders prefill work by it, so a
+# turn's respond prefill -- already a decide call deep into its TTFT -- is not queued behind the
+# decide prefills of turns that arrived after it.
+TURN_START: contextvars.ContextVar = contextvars.ContextVar("penny_turn_start", default=None)
 
 
 @dataclass
@@ -29,6 +37,7 @@ class SamplingParams:
     # prompt-lookup speculative decoding (engine.speculative): up to this many draft tokens copied
     # from the prompt are verified per step (0 = off)
     prompt_lookup: int = 0
+    priority_ts: Optional[float] = None   # scheduling time (TURN_START); None: the request's arrival
 
 
 class SeqStatus(enum.Enum):
@@ -88,6 +97,10 @@ class Sequence:
                 self.last_run = self.last_run[:len(self.last_run) - accepted]
         self.spec_rows = 0
         self.spec_reject = 0
+
+    @property
+    def priority_time(self) -> float:
+        return self.arrival if self.params.priority_ts is None else self.params.priority_ts
 
     @property
     def all_ids(self) -> List[int]:

@@ -21,6 +21,7 @@ import json
 from typing import Any, Dict, Optional, Set
 
 from .. import config
+from ..engine.sequence import TURN_START
 from ..utils.logging import get_logger
 from ..utils.metrics import METRICS, TurnTrace, now
 from ..wire import chunk_event, complete_event, decode_user_message, error_event, timeout_event
@@ -44,6 +45,7 @@ class ChatWorker:
         value = decode_user_message(message.value())
         msg, conversation_id = value["message"], value["conversation_id"]
         trace = trace or TurnTrace(conversation_id=conversation_id)
+        TURN_START.set(trace.t_receive)     # engine requests of this turn are scheduled by it
         full_message = ""
         logger.info(f"Received message from Kafka: |{conversation_id}| {msg}")
         try:

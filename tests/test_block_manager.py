@@ -161,6 +161,23 @@ def test_scheduler_admits_short_output_requests_first():
     assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("decide", 0, 60), ("respond", 0, 68)]
 
 
+def test_scheduler_orders_a_class_by_turn_start():
+    """Within a priority class the older TURN goes first: a respond call whose turn started
+    before a newer turn's decide call is admitted ahead of it although it arrived later."""
+    from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
+    clock = [100.0]
+    bm = PyBlockManager(64, BS, True)
+    sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=64, max_model_len=4096, clock=lambda: clock[0])
+    decide_new = Sequence("decide-turn2", list(range(2000, 2060)), SamplingParams(max_tokens=96, priority_ts=99.5),
+                          arrival=99.6)
+    respond_old = Sequence("respond-turn1", list(range(3000, 3060)), SamplingParams(max_tokens=128, priority_ts=98.0),
+                           arrival=99.8)
+    sch.add(decide_new)
+    sch.add(respond_old)
+    batch = sch.schedule()
+    assert [s.request_id for s, _, _ in batch.prefill] == ["respond-turn1", "decide-turn2"]
+
+
 def test_scheduler_aging_is_starvation_free():
     """A long request keeps losing to fresh short ones only until it has waited aging_s; then,
     being older, it is admitted ahead of every newer short request."""
