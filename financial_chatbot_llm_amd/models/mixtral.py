@@ -157,9 +157,18 @@ class MixtralModel(DecoderModel):
         if self.ep:
             grouped = None
             if self.fp8 and ops._native.use_native(h):   # one grouped fp8 call, device bucket offsets
-                grouped = lambda rows, ids: moe_ops.moe_grouped_fp8(  # noqa: E731
-                    rows.contiguous(), ids, self.w[p + "w13_t"], self.w[p + "w13_scale"], self.w[p + "w2_t"],
-                    self.w[p + "w2_scale"])
+                tiles = ((p + "w13_q") in self.w and moe_ops.PREFILL_TILES
+                         and self.w[p + "w13_q"].shape[1] % 256 == 0)
+
+                def grouped(rows, ids):
+                    # prefill-size receives: the 256x256 fp8 tile kernel; decode-size: the
+                    # weight-streaming grouped kernel
+                    if tiles and rows.shape[0] >= moe_ops.EP_TILE_MIN_ROWS:
+                        return moe_ops.moe_grouped_fp8_tiles(rows.contiguous(), ids, self.w[p + "w13_q"],
+                                                             self.w[p + "w13_scale"], self.w[p + "w2_q"],
+                                                             self.w[p + "w2_scale"])
+                    return moe_ops.moe_grouped_fp8(rows.contiguous(), ids, self.w[p + "w13_t"], self.w[p + "w13_scale"],
+                                                   self.w[p + "w2_t"], self.w[p + "w2_scale"])
             return ep_moe(h, logits, c.top_k_experts, c.num_experts, lambda rows, e: self._expert(p, rows, e),
                           group=pstate().tp_group, grouped_fn=grouped)
         # fp8 MFMA pipeline while the step is weight-bandwidth-bound; bigger prefill chunks go to

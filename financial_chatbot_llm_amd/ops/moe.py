@@ -24,6 +24,8 @@ def topk_softmax(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tens
 # prefill-size fp8 MoE steps run moe_prefill_fp8_tiles (PENNY_MOE_PREFILL_TILES=0: the per-expert
 # hipBLASLt fp8 loop with one host read of the bucket sizes per layer)
 PREFILL_TILES = os.environ.get("PENNY_MOE_PREFILL_TILES", "1") != "0"
+# expert-parallel receives of at least this many rows run moe_grouped_fp8_tiles
+EP_TILE_MIN_ROWS = int(os.environ.get("PENNY_EP_TILE_MIN_ROWS", "512"))
 
 
 def route(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
@@ -158,6 +160,45 @@ def moe_grouped_fp8(x: torch.Tensor, expert_ids: torch.Tensor, w13t: torch.Tenso
     y = torch.empty_like(y2)
     y.index_copy_(0, order, y2)
     return torch.where((ids >= 0)[:, None], y, torch.zeros_like(y))
+
+
+def moe_grouped_fp8_tiles(x: torch.Tensor, expert_ids: torch.Tensor, w13q: torch.Tensor, s13: torch.Tensor,
+                          w2q: torch.Tensor, s2: torch.Tensor) -> torch.Tensor:
+    """:func:`moe_grouped_fp8` for prefill-size receives (expert-parallel receive side): the same
+    per-row result on the 256x256 fp8 tile kernel (gemm_prefill.hip) instead of the decode-shaped
+    grouped kernel -- rows sorted by expert on the device, GEMM1 gathers them through the sort
+    order, GEMM2 runs at unit routing weights (the home rank applies the real ones), padding rows
+    (id -1) sort last, outside every expert bucket, and come back as zeros.  No host sync.
+    ``w13q`` / ``w2q``: row-major e4m3 [E_local, N, K]."""
+    from . import _native as N
+    M, H = x.shape
+    E, F2 = s13.shape
+    F_ = F2 // 2
+    ids = expert_ids.long()
+    key = torch.where(ids >= 0, ids, torch.full_like(ids, E))
+    order = torch.argsort(key, stable=True)
+    counts = torch.zeros(E + 1, dtype=torch.int32, device=x.device)
+    counts.scatter_add_(0, key, torch.ones_like(key, dtype=torch.int32))
+    offsets = torch.zeros(E + 1, dtype=torch.int32, device=x.device)
+    offsets[1:] = counts[:E].cumsum(0)
+    rows = order.to(torch.int32)
+    st = N.stream()
+    xq = torch.empty((M, H), dtype=torch.uint8, device=x.device)
+    xs = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.call("penny_quant_rows_fp8", N.ptr(x), x.stride(0), M, H, N.ptr(xq), N.ptr(xs), st)
+    a = torch.zeros((M, F_), dtype=torch.bfloat16, device=x.device)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(rows), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
+           N.ptr(s13), None, N.ptr(a), F_, M, E, F2, H, 7, st)
+    aq = torch.empty((M, F_), dtype=torch.uint8, device=x.device)
+    as_ = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.call("penny_quant_rows_fp8", N.ptr(a), F_, M, F_, N.ptr(aq), N.ptr(as_), st)
+    ones = torch.ones(M, dtype=torch.float32, device=x.device)
+    y2 = torch.zeros((M, H), dtype=torch.bfloat16, device=x.device)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(aq), F_, None, N.ptr(as_), N.ptr(offsets), N.ptr(w2q), N.ptr(s2),
+           N.ptr(ones), N.ptr(y2), H, M, E, H, F_, 8, st)
+    y = torch.empty_like(y2)
+    y.index_copy_(0, order, y2)
+    return y
 
 
 def quant_rows_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

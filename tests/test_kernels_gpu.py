@@ -709,6 +709,36 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
     assert err < 0.03, err
 
 
+def test_moe_grouped_fp8_tiles_matches_reference():
+    """Expert-parallel receive side on the tile kernel: y[i] = expert_{ids[i]}(x[i]) in the
+    received (unsorted) row order, padding rows (id -1) zero."""
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    g = torch.Generator(device=DEV).manual_seed(21)
+    M, E, H, F_ = 700, 4, 1024, 1536
+    w13 = (torch.randn((E, 2 * F_, H), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    w13 = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    w2 = (torch.randn((E, H, F_), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    x = torch.randn((M, H), device=DEV, generator=g).to(torch.bfloat16)
+    ids = torch.randint(-1, E, (M,), device=DEV, generator=g, dtype=torch.int32)
+    ids[ids == 2] = 1                                # an empty local expert
+    got = moe.moe_grouped_fp8_tiles(x, ids, q13.contiguous(), s13, q2.contiguous(), s2).float()
+    xq, xs = moe.quant_rows_fp8(x)
+    xd = xq.float() * xs[:, None]
+    ref = torch.zeros((M, H), device=DEV)
+    for e in range(E):
+        rows = (ids == e).nonzero().flatten()
+        if rows.numel() == 0:
+            continue
+        a = gemm.silu_mul((xd[rows] @ (q13[e].float() * s13[e][:, None]).t()).to(torch.bfloat16), interleave16=True)
+        aq, as_ = moe.quant_rows_fp8(a)
+        ref[rows] = (aq.float() * as_[:, None]) @ (q2[e].float() * s2[e][:, None]).t()
+    assert float(got[ids < 0].abs().max()) == 0.0
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 0.03, err
+
+
 def test_topp_threshold_is_bitwise_repeatable():
     """Integer (fixed-point) digit histograms: the top-p threshold of the same logits is bitwise
     identical across repeated launches and batch positions (advisor finding: float atomics made
