@@ -13,14 +13,17 @@ Execution forms:
   activations, grouped fp8 x fp8 MFMA GEMMs over expert buckets with fused SiLU / routing-weight
   epilogues, atomics-free combine.  Weights are OCP e4m3 with per-output-row scales, stored in
   MFMA-fragment tiles, halving the expert bytes streamed per decode step vs bf16.
-* otherwise (prefill, CPU, bf16 experts): tokens are bucketed by expert (``ops.moe.route``) and
-  each expert runs one GEMM pair over its bucket (hipBLASLt fp8 x fp8 with per-row scales; bf16
-  or dequantised experts elsewhere).  This form reads the bucket sizes on the host once per layer.
-  A device-only form exists (``ops.moe.moe_prefill_fp8``: device routing + the grouped fp8 MFMA
-  kernels, no host sync) and is what the hipGraph / EP paths use, but at prefill sizes the
-  per-expert hipBLASLt GEMMs are 2.3-3.4x faster (T=2048-16384: 0.95-1.85 PF/s vs 0.56-0.58,
-  ``profiles/r2_moe_prefill_device_vs_hipblaslt.jsonl``) while the one host read per layer costs
-  well under 1 % of a prefill step, so prefill keeps the library GEMMs by measurement.
+* fp8 experts, prefill-sized steps: ``ops.moe.moe_prefill_fp8_tiles`` -- device routing, grouped
+  256x256 fp8 tile GEMMs over the expert buckets (``gemm_prefill.hip``, block-scaled 16x16x128
+  MFMA) with the SiLU / routing-weight epilogues, no host sync: 1.48-1.79 PF/s per MoE layer at
+  T = 4096-16384 vs 1.18-1.88 for the per-expert hipBLASLt loop it replaced
+  (``profiles/r3_moe_prefill_tiles_vs_hipblaslt.jsonl``; ``PENNY_MOE_PREFILL_TILES=0`` restores it).
+* bf16 experts, decode-sized steps: every expert densely over the step's rows, weighted by the
+  routing weights (decode streams every expert's weights anyway; no host sync, so hipGraph
+  decode captures it).
+* otherwise (bf16 prefill, CPU): tokens are bucketed by expert (``ops.moe.route``) and each
+  expert runs one GEMM pair over its bucket; this form reads the bucket sizes on the host once
+  per layer.
 
 Under TP the experts are parallelised one of two ways (``moe_parallel``):
 * ``"tp"`` (default, hipGraph decode path): every expert's intermediate dimension is sharded
@@ -42,6 +45,10 @@ from ..parallel import comm
 from ..parallel.dist import state as pstate
 from ..parallel.ep import ep_moe, expert_range
 from .llama import DecoderModel
+
+# bf16 experts: steps of at most this many (token, expert) pairs run every expert densely (no host
+# sync, hipGraph-capturable); larger ones the bucketed per-expert loop
+BF16_DENSE_MAX_PAIRS = 512
 
 
 class MixtralModel(DecoderModel):
@@ -187,6 +194,18 @@ class MixtralModel(DecoderModel):
                                                 c.top_k_experts)
             return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
         topw, topi = moe_ops.topk_softmax(logits, c.top_k_experts)
+        if not self.fp8 and (T * c.top_k_experts <= BF16_DENSE_MAX_PAIRS
+                             or (h.is_cuda and torch.cuda.is_current_stream_capturing())):
+            # bf16 decode sizes: every expert over every row, weighted by the (mostly zero) routing
+            # weights -- decode streams all experts' weights each step anyway, and this form has no
+            # host sync, so it is hipGraph-capturable (the bucketed loop below reads sizes on the host)
+            wfull = torch.zeros((T, c.num_experts), dtype=torch.float32, device=h.device)
+            wfull.scatter_(1, topi.long(), topw.float())
+            out = torch.zeros((T, h.shape[1]), dtype=torch.float32, device=h.device)
+            for e in range(c.num_experts):
+                out.add_(self._expert_bf16(p, h, e).float() * wfull[:, e:e + 1])
+            out = out.to(h.dtype)
+            return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
         order, offsets, tok_idx, tok_w = moe_ops.route(topi, topw, c.num_experts)
         offs = offsets.tolist()
         xs = h.index_select(0, tok_idx)
