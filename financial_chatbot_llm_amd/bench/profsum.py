@@ -15,7 +15,7 @@ from collections import defaultdict
 
 CLASSES = [
     ("gemm-prefill tile (HIP)", r"gemm_prefill_kernel"),
-    ("attention-decode", r"decode_kernel|decode_reduce"),
+    ("attention-decode", r"decode_kernel|decode_reduce|decode_lean"),
     ("attention-prefill", r"prefill_kernel|prefill2_kernel|cascade_kernel"),
     ("gemm-skinny (HIP)", r"skinny"),
     ("gemm-splitk (HIP)", r"splitk"),

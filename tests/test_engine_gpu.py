@@ -45,8 +45,10 @@ def test_gpu_forward_matches_cpu_reference(name):
     assert (a.argmax(-1) == b.argmax(-1)).float().mean() > 0.85
 
 
-def test_graph_decode_matches_eager():
-    base = dict(model="llama-tiny", device="cuda", num_kv_blocks=128, max_model_len=2048, max_num_seqs=16,
+@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
+def test_graph_decode_matches_eager(model):
+    """bf16 Mixtral included: its decode MoE must be capturable (no host sync)."""
+    base = dict(model=model, device="cuda", num_kv_blocks=128, max_model_len=2048, max_num_seqs=16,
                 graph_batch_sizes=(1, 2, 4, 8, 16))
     prompts = [list(range(100 + 7 * i, 100 + 7 * i + 30 + 17 * i)) for i in range(5)]
     sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
