@@ -285,6 +285,14 @@ def bench_elementwise(dev) -> List[Dict]:
         vc = torch.zeros(((T + 63) // 64 + 1, 8, 64 * 128), device=dev, dtype=torch.bfloat16)
         us = timeit(lambda: ops.rope_kv_write(qkv, pos, cs, pos, kc, vc, 32, 8, 128))
         out.append({"op": "rope_kv_write", "T": T, "us": round(us, 2), "GBps": round(2 * T * 48 * 128 * 2 / us / 1e3, 1)})
+    # bge encoder LayerNorm (H = 768) at query-batch sizes: rows = queries x ~24 tokens
+    for T in (24, 192, 768, 4096):
+        x = torch.randn((T, 768), device=dev).to(torch.bfloat16)
+        r = torch.randn((T, 768), device=dev).to(torch.bfloat16)
+        gw = torch.ones(768, device=dev, dtype=torch.bfloat16)
+        bw = torch.zeros(768, device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.layer_norm(x, gw, bw, 1e-12, residual=r), iters=50)
+        out.append({"op": "layernorm_768", "T": T, "us": round(us, 2), "GBps": round(3 * T * 768 * 2 / us / 1e3, 1)})
     V = 128256
     for B in (64, 256):
         lg = torch.randn((B, V), device=dev).to(torch.bfloat16)
