@@ -852,6 +852,27 @@ def check_gemm_hip(dev) -> List[Dict]:
     return out
 
 
+def gemm_lds_probe(dev) -> List[Dict]:
+    """A few launches of the bf16 tile GEMM (4096^3) and of the grouped fp8 MoE tile GEMMs, for
+    rocprofv3 --pmc runs (LDS bank-conflict counters of the swizzled fragment reads)."""
+    from ..ops import gemm, moe
+    x = (torch.randn((4096, 4096), device=dev) * 0.5).to(torch.bfloat16)
+    w = (torch.randn((4096, 4096), device=dev) * 0.05).to(torch.bfloat16)
+    for _ in range(5):
+        gemm.prefill_gemm(x, w, None, 1)
+    E, H, F_ = 8, 4096, 14336
+    w13q = torch.randint(0, 120, (E, 2 * F_, H), dtype=torch.uint8, device=dev)
+    w2q = torch.randint(0, 120, (E, H, F_), dtype=torch.uint8, device=dev)
+    s13 = torch.full((E, 2 * F_), 1e-3, device=dev)
+    s2 = torch.full((E, H), 1e-3, device=dev)
+    h = torch.randn((4096, H), device=dev).to(torch.bfloat16)
+    logits = torch.randn((4096, E), device=dev).to(torch.bfloat16)
+    for _ in range(3):
+        moe.moe_prefill_fp8_tiles(h, logits, w13q, s13, w2q, s2, 2)
+    torch.cuda.synchronize()
+    return [{"op": "gemm_lds_probe", "done": True}]
+
+
 def interleave16_rows(w: torch.Tensor) -> torch.Tensor:
     from ..ops.gemm import interleave16
     half = w.shape[0] // 2
@@ -870,7 +891,7 @@ def main(argv=None) -> int:
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
-                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "prefill_policy": bench_prefill_policy, "gemm_ablate": bench_gemm_ablate,
+                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),

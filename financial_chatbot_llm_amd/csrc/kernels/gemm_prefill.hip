@@ -79,7 +79,8 @@ struct RopeArgs {
 // LDS row swizzle of 16-B chunks, per fragment-read pattern (ds_read_b128 16-lane phases, 2 rows
 // per 256-B bank row): bf16 fragments read chunk 4kk + g, fp8 (16x16x128) fragments chunks 2g and
 // 2g + 1 -- (r >> 1) & 7 and (r >> 1) & 5 make those conflict-free (exhaustive check over the
-// linear XOR maps, profiles/r3_lds_swizzle_search.txt).
+// linear XOR maps); rocprofv3 counts SQ_LDS_BANK_CONFLICT = 0 for the bf16 and fp8 variants
+// (profiles/r3_gemm_prefill_lds_bank_conflicts_pmc.txt).
 template <bool FP8>
 __device__ __forceinline__ int swz(int r) { return FP8 ? ((r >> 1) & 5) : ((r >> 1) & 7); }
 
