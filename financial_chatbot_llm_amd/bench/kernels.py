@@ -225,6 +225,7 @@ def bench_prefill(dev) -> List[Dict]:
 # prompts (~200 new tokens behind ~4.6k cached ones)
 MIXED_STEPS = {
     "respond+8decides": [(1600, 3400)] + [(220, 4600)] * 8,
+    "respond+16spec+4decides": [(1500, 3600)] + [(9, 5200)] * 16 + [(220, 4600)] * 4,
     "2respond": [(1800, 3000), (1900, 3900)],
     "16decides": [(200, 4800)] * 16,
     "respond-long": [(2400, 6400), (1600, 5200)],
@@ -259,11 +260,18 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=dev)
         lens = torch.tensor([c for _, c in shape], dtype=torch.int32, device=dev)
         o = torch.empty_like(q)
-        us = timeit(lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o), iters=5)
+        wl = ops.attention.prefill_work_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv)
+        wd = torch.from_numpy(wl).to(dev) if wl is not None else None
+        ts = interleaved({"grid": lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o),
+                          "lpt": lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
+                                                     work=wd)}, rounds=7, iters=5)
         keys = sum(ql * (c - ql) + ql * (ql + 1) / 2 for ql, c in shape)
         flops = 4 * keys * Hq * D
-        out.append({"op": "prefill_attn_mixed", "step": name, "T": T, "us": round(us, 1),
-                    "TFLOPs": round(flops / us / 1e6, 1)})
+        row = {"op": "prefill_attn_mixed", "step": name, "T": T, "us": round(ts["lpt"], 1),
+               "TFLOPs": round(flops / ts["lpt"] / 1e6, 1), "grid_us": round(ts["grid"], 1),
+               "grid_TFLOPs": round(flops / ts["grid"] / 1e6, 1)}
+        print(json.dumps(row), flush=True)
+        out.append(row)
     return out
 
 

@@ -826,7 +826,7 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
-    float* __restrict__ lse) {
+    float* __restrict__ lse, const int* __restrict__ work) {
   constexpr int KC = D / 32, DT = D / 16;
   constexpr int TILE = KV_BS * D * 2;         // bytes of one K (or V) block tile
   constexpr int PIECES = TILE / 1024 / NW;    // 1-KiB glds pieces per wave per tile
@@ -838,11 +838,14 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   // HEAD_FAST grid (Hkv, tiles, seqs): with round-robin dispatch over the 8 XCDs every tile of a
   // (sequence, kv head) lands on the same XCD, so its K/V blocks are fetched into one L2 and
   // re-read from there by the other tiles (grid (tiles, Hkv, seqs) spreads them over all 8 L2s)
-  const int s = blockIdx.z;
+  // `work` (host-built, ops.attention.prefill_work_list): the step's real (sequence, tile) pairs,
+  // longest KV walk first across ALL sequences (LPT order: the short decide tiles fill the last
+  // round instead of trailing it, and no workgroup is launched for a tile past a short sequence's
+  // end).  Without it: grid (.., max tiles, sequences), each sequence's tiles longest first.
+  const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
+  const int s = work ? work[2 * item] : blockIdx.z;
   const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
-  const int tile = HEAD_FAST ? gridDim.y - 1 - blockIdx.y : gridDim.x - 1 - blockIdx.x;
-  const int ntiles = HEAD_FAST ? gridDim.y : gridDim.x;
-  (void)ntiles;
+  const int tile = work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item;
   const int G = Hq / Hkv;
   const int TQ = NW * 32 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
@@ -949,7 +952,7 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                       const void* k_cache, const void* v_cache, void* out, int num_seqs,
                                       int max_q_len, int Hq, int Hkv, int D, int max_blocks, float scale, int causal,
-                                      float* lse, hipStream_t stream) {
+                                      float* lse, const int* work, int nwork, hipStream_t stream) {
   if (num_seqs <= 0 || max_q_len <= 0) return 0;
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv;
@@ -967,16 +970,21 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
     return v ? atoi(v) : 1;
   }();
   const bool head_fast = head_fast_env != 0;
+  // work list (big tiles only): one workgroup per real (sequence, tile), LPT order
+  const bool wl = big && work != nullptr && nwork > 0;
   dim3 grid(ntiles, Hkv, num_seqs);
+  const dim3 grid2 = wl ? (head_fast ? dim3(Hkv, nwork, 1) : dim3(nwork, Hkv, 1))
+                        : (head_fast ? dim3(Hkv, ntiles, num_seqs) : grid);
+  const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
   if (big && head_fast)                                                                                          \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), dim3(Hkv, ntiles, num_seqs), dim3(512), 0, stream,     \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), grid2, dim3(512), 0, stream,                           \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse);                                         \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big)                                                                                                  \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, false>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q,     \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, false>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q,    \
                        ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,    \
-                       Hkv, max_blocks, causal, lse);                                                              \
+                       Hkv, max_blocks, causal, lse, wp);                                                          \
   else                                                                                                           \
     hipLaunchKernelGGL(prefill_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens,           \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \

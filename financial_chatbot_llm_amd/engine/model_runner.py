@@ -21,7 +21,7 @@ import torch
 
 from .. import ops
 from ..models.common import AttentionMetadata, KVCache
-from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade
+from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade, prefill_work_list
 from ..parallel import comm
 from ..utils.logging import get_logger
 from ..utils.profiling import marker
@@ -50,6 +50,7 @@ class StepInputs:
     top_k: np.ndarray               # [S]
     top_p: np.ndarray               # [S]
     src: Optional[np.ndarray] = None  # [Bd] row of the previous step's sampled vector (-1: ids[] is real)
+    pwork: Optional[np.ndarray] = None  # [n, 2] prefill attention work list (filled by the runner)
 
     @property
     def num_prefill_tokens(self) -> int:
@@ -57,7 +58,7 @@ class StepInputs:
 
     # -- C4 wire format: one flat byte buffer (no pickling) ------------------------------------
     _ARRAYS = ("ids", "positions", "slots", "cu_q", "ctx_p", "bt_p", "ctx_d", "bt_d", "logits_idx", "temps",
-               "seeds", "top_k", "top_p", "src")
+               "seeds", "top_k", "top_p", "src", "pwork")
 
     def pack(self) -> np.ndarray:
         """[header int64: max_q_len, then (dtype code, rows, cols) per array] + raw array bytes."""
@@ -318,6 +319,9 @@ class ModelRunner:
             m.ctx_lens_p = self._to_dev(si.ctx_p)
             m.block_tables_p = self._to_dev(si.bt_p)
             m.max_q_len = si.max_q_len
+            if self.on_gpu:   # LPT-ordered prefill attention tiles (staged with the step when precomputed)
+                work = si.pwork if si.pwork is not None else prefill_work_list(si.cu_q, si.ctx_p, self.G)
+                m.prefill_work = self._to_dev(work) if work is not None else None
         if si.num_decode:
             m.ctx_lens_d = self._to_dev(si.ctx_d)
             m.block_tables_d = self._to_dev(si.bt_d)
@@ -430,6 +434,8 @@ class ModelRunner:
             graph = True
         else:
             with marker(f"forward.eager[{len(si.ids)}]"):
+                if si.num_prefill_tokens and si.pwork is None and self.on_gpu:
+                    si.pwork = prefill_work_list(si.cu_q, si.ctx_p, self.G)
                 self._stage_inputs(si)
                 try:
                     out = self.sample(self.forward_logits(si), si)

@@ -27,6 +27,7 @@ class AttentionMetadata:
     decode_ws: Optional[DecodeWorkspace] = None
     cascade: Optional[CascadeInputs] = None     # shared-prefix groups of the decode rows
     causal: bool = True
+    prefill_work: Optional[torch.Tensor] = None  # [n, 2] int32 (ops.attention.prefill_work_list)
 
 
 class KVCache:

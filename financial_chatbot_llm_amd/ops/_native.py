@@ -42,7 +42,8 @@ _SIGS = {
     "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write_slabs": [P, c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
-    "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P],
+    "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P,
+                                c_int, P],
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P],
     "penny_sample": [P, c_int, c_long, P, P, P, P, P, P, c_int, c_int, P],

@@ -160,14 +160,45 @@ def _attend_ref(q, k, v, scale, causal_offset: Optional[int]):
     return torch.einsum("hqk,khd->qhd", p, vf)
 
 
+PREFILL_WORK_LIST = os.environ.get("PENNY_PREFILL_WORK_LIST", "1") != "0"
+
+
+def prefill_work_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, causal: bool = True) -> Optional[np.ndarray]:
+    """Host work list for the 8-wave prefill kernel: every real (sequence, 256-row tile) of a step,
+    ordered by the number of KV blocks its tile walks, longest first (LPT) -- [n, 2] int32, or None
+    when the step takes the 4-wave kernel (no tile above 128 rows) or the list is disabled
+    (``PENNY_PREFILL_WORK_LIST=0``).  Without it the grid is (max tiles x sequences): a step with one
+    1.6k-token respond chunk and eight 220-token decide chunks launches 4x the workgroups it needs,
+    and every sequence's short tiles trail its long ones."""
+    if not PREFILL_WORK_LIST or G <= 0 or 256 % G:
+        return None
+    cu = np.asarray(cu_q, np.int64)
+    ql = cu[1:] - cu[:-1]
+    if len(ql) == 0 or int(ql.max()) * G <= 128:
+        return None
+    ctx = np.asarray(ctx_lens, np.int64)
+    TQ = 256 // G
+    seqs, tiles, cost = [], [], []
+    for s_, (n, c) in enumerate(zip(ql.tolist(), ctx.tolist())):
+        for t in range((n + TQ - 1) // TQ):
+            last = min((t + 1) * TQ, n) - 1
+            kv_end = min(c, c - n + last + 1) if causal else c
+            seqs.append(s_)
+            tiles.append(t)
+            cost.append((kv_end + KV_BS - 1) // KV_BS)
+    order = np.argsort(-np.asarray(cost), kind="stable")
+    return np.stack([np.asarray(seqs, np.int32)[order], np.asarray(tiles, np.int32)[order]], 1)
+
+
 def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor,
             k_cache: torch.Tensor, v_cache: torch.Tensor, scale: float, causal: bool = True,
             max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None,
-            lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+            lse: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Varlen paged attention for the new tokens of S sequences (chunked prefill / prefix hits:
     query i of sequence s sits at absolute position ctx_lens[s] - q_len[s] + i).  ``lse`` [T, Hq]
     f32 (optional) receives each row's natural-log sum-exp of the scaled scores (-inf: no key
-    visible) -- what a ring-attention merge needs."""
+    visible) -- what a ring-attention merge needs.  ``work``: :func:`prefill_work_list` of the same
+    step on the device (optional; LPT tile order)."""
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     S = block_tables.shape[0]
@@ -178,7 +209,8 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
             max_q_len = int((cu_q[1:] - cu_q[:-1]).max().item())
         N.call("penny_attention_prefill", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),
                N.ptr(k_cache), N.ptr(v_cache), N.ptr(out), S, int(max_q_len), Hq, Hkv, D, block_tables.shape[1],
-               float(scale), int(causal), N.ptr(lse) if lse is not None else None, N.stream())
+               float(scale), int(causal), N.ptr(lse) if lse is not None else None,
+               N.ptr(work) if work is not None else None, int(work.shape[0]) if work is not None else 0, N.stream())
         return out
     out = torch.empty_like(q) if out is None else out
     cu = cu_q.tolist()

@@ -153,6 +153,26 @@ def test_decode_attention(Hq, Hkv, ctxs, lean, chunks, monkeypatch):
     close(out, ref, atol=2e-2)
 
 
+def test_prefill_work_list_matches_grid_order():
+    """LPT work list (one workgroup per real (sequence, tile), longest KV walk first) gives the
+    same attention as the (max tiles x sequences) grid, bitwise."""
+    g = torch.Generator().manual_seed(9)
+    Hq, Hkv, D = 32, 8, 128
+    lens = [(1600, 3400)] + [(220, 4600)] * 3 + [(9, 5000), (300, 300)]
+    ctx = [c for _, c in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor([a for a, _ in lens]).cumsum(0)), dtype=torch.int32)
+    q = rnd(int(cu[-1]), Hq, D, gen=g)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    work = ops.attention.prefill_work_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv)
+    assert work is not None and len(work) == 25 + 3 * 4 + 1 + 5
+    args = (q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), 0.088, True, 1600)
+    a = ops.prefill(*args)
+    b = ops.prefill(*args, work=torch.from_numpy(work).to(DEV))
+    assert torch.equal(a, b)
+    close(b, ops.prefill(q, cu, ctx_t, tables, kc, vc, 0.088, True), atol=2e-2)
+
+
 def test_decode_matches_prefill_last_row():
     g = torch.Generator().manual_seed(6)
     Hq, Hkv, D, L = 32, 8, 128, 517

@@ -186,3 +186,19 @@ def test_kernel_lib_override_path(monkeypatch):
     assert _native.lib_path().endswith("libpenny_kernels_debug.so")
     monkeypatch.setenv("PENNY_KERNEL_LIB", "/tmp/other/libpenny_kernels_ab.so")
     assert _native.lib_path() == "/tmp/other/libpenny_kernels_ab.so"
+
+
+def test_prefill_work_list_lpt_order():
+    """One entry per real (sequence, 256-row tile); tiles walking the most KV blocks first; None
+    when every chunk fits the 4-wave kernel's 128 rows."""
+    import numpy as np
+    from financial_chatbot_llm_amd.ops.attention import prefill_work_list
+    cu = np.array([0, 200, 220, 420], np.int32)          # q lens 200, 20, 200
+    ctx = np.array([4800, 100, 1000], np.int32)
+    w = prefill_work_list(cu, ctx, 4)                      # TQ = 64 tokens per tile
+    assert w.shape == (4 + 1 + 4, 2)
+    assert w[0][0] == 0 and w[0][1] in (2, 3)             # a last tile of the long-context sequence
+    blocks = [((min(c, c - n + min((t + 1) * 64, n)) + 63) // 64) for s, t in w.tolist()
+              for n, c in [((cu[s + 1] - cu[s]), ctx[s])]]
+    assert blocks == sorted(blocks, reverse=True)
+    assert prefill_work_list(np.array([0, 30, 60], np.int32), np.array([100, 200], np.int32), 4) is None
