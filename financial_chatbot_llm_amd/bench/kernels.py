@@ -385,6 +385,28 @@ def bench_lm_head(dev) -> List[Dict]:
     return out
 
 
+def bench_lm_head_fused(dev) -> List[Dict]:
+    """LM head + sampler per step (vocab 128256): hipBLASLt logits + the HIP sampler vs the fused
+    tile-kernel LM head that samples in its epilogue (ops.lm_head_sample), temperature rows."""
+    from .. import ops
+    from ..ops import gemm
+    gemm.load_gemm_tuning("llama3-8b")
+    out = []
+    V, K = 128256, 4096
+    w = torch.randn((V, K), device=dev).to(torch.bfloat16) * 0.02
+    for M in (1, 16, 32, 48, 64, 96, 128, 160, 192, 256):
+        x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+        t = torch.full((M,), 0.7, device=dev)
+        sd = torch.arange(M, dtype=torch.int64, device=dev) * 977
+        lib = timeit(lambda: ops.sample(torch.nn.functional.linear(x, w), t, sd), iters=10)
+        fused = timeit(lambda: ops.lm_head_sample(x, w, t, sd), iters=10)
+        same = bool(torch.equal(ops.lm_head_sample(x, w, t, sd), ops.sample(gemm.prefill_gemm(x, w), t, sd)))
+        out.append({"op": "lm_head_sample", "M": M, "lib_plus_sampler_us": round(lib, 1), "fused_us": round(fused, 1),
+                    "speedup": round(lib / fused, 3), "fused_TBps": round(V * K * 2 / fused / 1e6, 2),
+                    "fused_equals_tile_logits_then_sampler": same})
+    return out
+
+
 def bench_gemm_tune_sweep(dev) -> List[Dict]:
     """Prefill GEMMs at every M = 256k: hipBLASLt default heuristic vs a TunableOp-tuned solution
     (tuned here, written to ``PENNY_TUNE_OUT``): is a padded-M + tuned-solution policy worth it?"""
@@ -896,7 +918,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head,
+                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "gemm_ablate": bench_gemm_ablate,

@@ -116,4 +116,19 @@ __device__ __forceinline__ float u01_from_bits(uint32_t b) {
   return ((float)(b >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// Gumbel noise of vocabulary entry idx for a row seeded `seed` (K12 and the fused LM-head sampler
+// draw the SAME noise, so a row samples the same token on either path for equal logits)
+__device__ __forceinline__ float gumbel_noise(unsigned long long seed, int idx) {
+  const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
+  return -__logf(-__logf(u01_from_bits((uint32_t)r)));
+}
+
+// running (max value, smallest index on ties) of a Gumbel-max / argmax reduction
+__device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i < bi)) {
+    bv = v;
+    bi = i;
+  }
+}
+
 #define PENNY_RETURN_LAUNCH() return (int)hipGetLastError()

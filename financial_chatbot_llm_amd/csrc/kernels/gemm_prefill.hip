@@ -10,6 +10,11 @@
 //   EPI_RESID Y bf16 = bf16(acc) + R (residual add fused, rounded like GEMM-then-add)
 //   EPI_BIAS / EPI_BIAS_GELU  Y bf16 = bf16(acc + bias[n]) [-> exact-erf GELU], R = the bias: the
 //             bge encoder's QKV / O / fc2 and its GELU-MLP fc1 (no separate GELU pass)
+//   EPI_SAMPLE the LM head fused with the K12 sampler: W = the [V, K] vocabulary projection, and
+//             no logits reach HBM -- each lane scores its bf16-rounded logits (greedy, or
+//             logit / T + Gumbel noise of (row seed, token id), sampler.hip's draw) and the
+//             workgroup leaves one (best score, token) pair per (token row, 128-column wave half);
+//             lm_sample_final_kernel reduces the V / 128 pairs of a row to the sampled token
 //   EPI_ROPE  the fused QKV projection (K3+K4+K5): a wave's 128 output columns are exactly one
 //             head, so the rotate-half RoPE pair (d, d+64) sits in one lane (accumulators f, f+4);
 //             q heads -> rotated q [M, Hq, 128]; k heads -> rotated, v heads -> as is, both
@@ -53,7 +58,7 @@ constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
 constexpr int GM = 4;                // token tiles per L2 group
 enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
 enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6,
-       EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8 };
+       EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8, EPI_SAMPLE = 9 };
 
 // Grouped fp8 MoE GEMM (penny_moe_gemm_prefill_fp8): rows sorted by expert, bucket bounds on the
 // DEVICE (offsets [E+1]), so tiles are found without a host round trip.
@@ -64,6 +69,14 @@ struct MoeArgs {
   const float* ws;        // [E, N] per-output-row weight scales
   const float* route_w;   // [P] routing weight of each sorted row (EPI_MOE_ROUTE)
   int E;
+};
+
+// EPI_SAMPLE: per-row temperature (<= 0: greedy) and seed; pv / pi [M, 2 * N / 256] partial bests
+struct SampleArgs {
+  const float* temps;
+  const unsigned long long* seeds;
+  float* pv;
+  int* pi;
 };
 
 struct RopeArgs {
@@ -177,7 +190,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
                                                            const void* __restrict__ Wv, int K,
                                                            void* __restrict__ Y, int ldy,
                                                            const bf16* __restrict__ R, int ldr,
-                                                           int M, int N, int S, RopeArgs ra, MoeArgs ma) {
+                                                           int M, int N, int S, RopeArgs ra, MoeArgs ma,
+                                                           SampleArgs sa) {
   constexpr int ESZ = FP8 ? 1 : 2;        // bytes per element
   constexpr int BKE = 128 / ESZ;          // elements per K-tile row (128 bytes)
   const char* __restrict__ X = static_cast<const char*>(Xv);
@@ -418,6 +432,35 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
           *reinterpret_cast<uint4*>(y + 16 * f) = pair16(lo, hi);
         }
       }
+    } else if constexpr (EPI == EPI_SAMPLE) {
+      // lanes col, col + 16, col + 32, col + 48 hold this row's 128 columns of the wave: each scores
+      // its 32, then two xor-shuffles inside the same-row lane set (all active or all skipped)
+      const float temp = sa.temps[m];
+      const bool greedy = !(temp > 0.f);
+      const float inv_t = greedy ? 1.f : 1.f / temp;
+      const unsigned long long seed = sa.seeds[m];
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int f = 0; f < 8; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int idx = n0 + wa * 128 + f * 16 + 4 * g + r;
+          float v = (float)(bf16)acc[f][t][r];          // the bf16 logit the unfused path samples
+          if (!greedy) v = v * inv_t + gumbel_noise(seed, idx);
+          better(bv, bi, v, idx);
+        }
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        better(bv, bi, ov, oi);
+      }
+      if (g == 0) {
+        const long slot = (long)m * (2 * Nt) + 2 * tn + wa;
+        sa.pv[slot] = bv;
+        sa.pi[slot] = bi;
+      }
     } else if constexpr (EPI == EPI_ROPE) {
       constexpr int D = 128;
       const int hd = (n0 + wa * 128) >> 7;     // this wave's head (q heads, then k, then v)
@@ -518,7 +561,7 @@ template <int EPI, int ABL = 0, int BAL = 1>
 static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
                    const void* R, int ldr, int M, int N, int S, const RopeArgs& ra) {
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy,
-                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{});
+                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{});
 }
 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
@@ -597,9 +640,55 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
   const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
   if (epi == EPI_MOE_SILU)
     hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_SILU, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma);
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{});
   else
     hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_ROUTE, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma);
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{});
+  return (int)hipGetLastError();
+}
+
+// Reduce a row's (score, token) partials of the fused LM head (EPI_SAMPLE) to its sampled token:
+// one 256-thread workgroup per row, ties to the smallest token id (sample_final_kernel's rule).
+__global__ void __launch_bounds__(256) lm_sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                              int P, int* __restrict__ out) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int j = threadIdx.x; j < P; j += 256) better(bv, bi, pv[(long)row * P + j], pi[(long)row * P + j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    better(bv, bi, ov, oi);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sv[w] = bv;
+    si[w] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k) better(bv, bi, sv[k], si[k]);
+    out[row] = bi;
+  }
+}
+
+// LM head + sampler fused (K11 + K12): out[m] = Gumbel-max / argmax sample of row m of
+// X [M, K] bf16 x W [V, K]^T, temps [M] f32 (<= 0: greedy), seeds [M] u64 -- the [M, V] logits are
+// never written.  workspace: M * 2 * (V / 256) floats, then as many ints.
+// Contract (checked): V % 256 == 0, K % 64 == 0, ldx % 8 == 0, M >= 1.
+PENNY_API int penny_lm_head_sample(const void* X, int ldx, const void* W, int K, int M, int V, const float* temps,
+                                   const unsigned long long* seeds, void* workspace, int* out, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (V % TN || K % BK || ldx % 8 || !temps || !seeds || !workspace || !out) return (int)hipErrorInvalidValue;
+  const int P = 2 * (V / TN);
+  float* pv = static_cast<float*>(workspace);
+  int* pi = reinterpret_cast<int*>(pv + (long)M * P);
+  const SampleArgs sa{temps, seeds, pv, pi};
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI_SAMPLE>), grid_for(M, V, 1), dim3(512), 0, stream, X, ldx, W, K,
+                     nullptr, 0, (const bf16*)nullptr, 0, M, V, 1, RopeArgs{}, MoeArgs{}, sa);
+  hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, out);
   return (int)hipGetLastError();
 }

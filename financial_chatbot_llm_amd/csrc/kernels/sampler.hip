@@ -29,13 +29,6 @@ __device__ __forceinline__ void load8<float>(const float* p, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-__device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
-  if (v > bv || (v == bv && i < bi)) {
-    bv = v;
-    bi = i;
-  }
-}
-
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -234,8 +227,7 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
       float v = f[k];
       if (v < floor_l) continue;
       if (!greedy) {
-        const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
-        v = v * inv_t - __logf(-__logf(u01_from_bits((uint32_t)r)));
+        v = v * inv_t + gumbel_noise(seed, idx);
       }
       better(bv, bi, v, idx);
     }
@@ -245,8 +237,7 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
       float v = (float)lr[idx];
       if (v < floor_l) continue;
       if (!greedy) {
-        const uint64_t r = mix64(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(idx + 1)));
-        v = v * inv_t - __logf(-__logf(u01_from_bits((uint32_t)r)));
+        v = v * inv_t + gumbel_noise(seed, idx);
       }
       better(bv, bi, v, idx);
     }

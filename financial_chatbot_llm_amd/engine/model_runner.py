@@ -211,8 +211,9 @@ class PendingStep:
 
 
 class _DecodeGraph:
-    def __init__(self, graph, B: int, out: torch.Tensor):
-        self.graph, self.B, self.out = graph, B, out
+    def __init__(self, graph, B: int, out: torch.Tensor, fused: bool = False):
+        # fused: the graph samples inside the LM head (no top-k / top-p support)
+        self.graph, self.B, self.out, self.fused = graph, B, out, fused
 
 
 class ModelRunner:
@@ -396,10 +397,30 @@ class ModelRunner:
         idx = self._to_dev(si.logits_idx)
         return self.model.logits(h.index_select(0, idx))
 
+    def _fused_sampling(self, h: torch.Tensor) -> bool:
+        """Does sampling the rows ``h`` run inside the LM head (fused K11 + K12)?  TP=1 only: under TP
+        the vocabulary is sharded and the logits are all-gathered before sampling."""
+        m = self.model
+        return getattr(m, "tp_size", 1) == 1 and hasattr(m, "lm_weight") and ops.fused_lm_head_ok(h, m.lm_weight())
+
+    @staticmethod
+    def _has_filters(si: StepInputs) -> bool:
+        return bool((si.top_k > 0).any() or (si.top_p < 1).any())
+
+    def logits_and_sample(self, si: StepInputs) -> torch.Tensor:
+        """Forward the step, then sample one token per ``si.logits_idx`` row: fused into the LM head
+        where it applies (no top-k / top-p rows), else logits -> sampler."""
+        h = self._hidden(si)
+        hs = h.index_select(0, self._to_dev(si.logits_idx))
+        if not self._has_filters(si) and self._fused_sampling(hs):
+            self.stats["fused_lm_head_steps"] = self.stats.get("fused_lm_head_steps", 0) + 1
+            return ops.lm_head_sample(hs, self.model.lm_weight(), self._to_dev(si.temps), self._to_dev(si.seeds))
+        return self.sample(self.model.logits(hs), si)
+
     def sample(self, logits: torch.Tensor, si: StepInputs) -> torch.Tensor:
         temps = self._to_dev(si.temps)
         seeds = self._to_dev(si.seeds)
-        if (si.top_k > 0).any() or (si.top_p < 1).any():   # device-side top-k/top-p threshold
+        if self._has_filters(si):   # device-side top-k/top-p threshold
             return ops.sample(logits.contiguous(), temps, seeds, top_k=self._to_dev(si.top_k),
                               top_p=self._to_dev(si.top_p))
         return ops.sample(logits.contiguous(), temps, seeds)
@@ -428,7 +449,8 @@ class ModelRunner:
             start_ev = torch.cuda.Event(enable_timing=True)
             start_ev.record()
         graph = False
-        if self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch:
+        if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
+                and not self._fused_graph_needs_eager(si)):
             with marker(f"decode.graph[{si.num_decode}]"):
                 out = self._graph_decode(si)
             graph = True
@@ -438,7 +460,7 @@ class ModelRunner:
                     si.pwork = prefill_work_list(si.cu_q, si.ctx_p, self.G)
                 self._stage_inputs(si)
                 try:
-                    out = self.sample(self.forward_logits(si), si)
+                    out = self.logits_and_sample(si)
                 finally:
                     self._staged = None
         n = len(si.logits_idx)
@@ -504,6 +526,8 @@ class ModelRunner:
                                  ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
                                  cascade=s["cascade"])
         h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
+        if self._fused_sampling(h):
+            return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B])
         logits = self.model.logits(h)
         # the top-k/top-p threshold kernel is always in the graph: unfiltered rows (k=0, p=1) exit
         # after reading their parameters
@@ -525,9 +549,21 @@ class ModelRunner:
                 out = self._run_static(B)
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
-            self.graphs[B] = _DecodeGraph(g, B, out)
+            fused = self._fused_sampling(torch.empty((B, self.model.cfg.hidden_size), dtype=torch.bfloat16,
+                                                     device=self.device))
+            self.graphs[B] = _DecodeGraph(g, B, out, fused)
         torch.cuda.synchronize()
         logger.info(f"captured decode hipGraphs for batch sizes {sorted(self.graphs)}")
+
+    def _fused_graph_needs_eager(self, si: StepInputs) -> bool:
+        """A decode step with top-k / top-p rows whose bucket's graph samples inside the LM head runs
+        eagerly (logits -> filtered sampler) instead of replaying that graph."""
+        if not self._has_filters(si):
+            return False
+        if not self.graphs:
+            self.capture_graphs()
+        G = self.graphs.get(self._bucket(si.num_decode))
+        return G is not None and G.fused
 
     def _bucket(self, n: int) -> int:
         for b in self.graph_sizes:

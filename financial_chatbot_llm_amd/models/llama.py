@@ -328,9 +328,12 @@ class DecoderModel:
             x = self.mlp(i, h)
         return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
 
+    def lm_weight(self) -> torch.Tensor:
+        """The (local shard of the) [V, H] vocabulary projection."""
+        return self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
+
     def logits(self, h: torch.Tensor) -> torch.Tensor:
-        w = self.w["embed"] if self.cfg.tie_embeddings else self.w["lm_head"]
-        out = linear(h, w)
+        out = linear(h, self.lm_weight())
         return comm.tp_all_gather_last(out) if self.tp_size > 1 else out
 
 

@@ -47,6 +47,7 @@ _SIGS = {
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P],
     "penny_sample": [P, c_int, c_long, P, P, P, P, P, P, c_int, c_int, P],
+    "penny_lm_head_sample": [P, c_int, P, c_int, c_int, c_int, P, P, P, P, P],
     "penny_topk_topp_threshold": [P, c_int, c_long, P, P, P, P, c_int, c_int, P],
     "penny_moe_route": [P, c_int, c_int, c_int, P, P, P, P, P],
     "penny_quant_rows_fp8": [P, c_int, c_int, c_int, P, P, P],

@@ -53,6 +53,50 @@ def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor
     return res.to(logits.device)
 
 
+# Fused LM head + sampler (K11 + K12, ``gemm_prefill.hip`` EPI_SAMPLE): the vocabulary projection
+# runs on the 256x256 MFMA tile kernel and every lane Gumbel-max-scores its logits in registers,
+# so the [M, V] logits never reach HBM and the separate sampler pass disappears.  Its cost is
+# nearly flat in M (two rounds of 501 vocab tiles over 256 CUs for Llama-3: 243-265 us at M = 1-160,
+# 306 us at 256), while hipBLASLt + the sampler grows with M (190 us at M = 1, 266 at 128, 355 at
+# 256): the fused path is taken from FUSED_LM_HEAD_MIN_M rows, where it ties (M = 128) or wins
+# 8-16 % (M = 160-256) (bench/kernels.py lm_head_fused, profiles/r3_lm_head_fused_vs_hipblaslt.jsonl).
+# Below that the 256-row tile's MFMA work and the 1.05 GB weight stream share each CU's time
+# (4.2 TB/s) and the library's streaming GEMM wins.  ``PENNY_FUSED_LM_HEAD=0`` disables it,
+# ``=force`` takes it at every M.
+FUSED_LM_HEAD_MIN_M = 128
+
+
+def fused_lm_head_ok(h: torch.Tensor, w: torch.Tensor) -> bool:
+    import os
+    mode = os.environ.get("PENNY_FUSED_LM_HEAD", "1")
+    if mode == "0" or not N.use_native(h):
+        return False
+    M, K = h.shape
+    V = w.shape[0]
+    if V % 256 or K % 64 or h.stride(1) != 1 or h.stride(0) % 8 or not w.is_contiguous():
+        return False
+    return mode == "force" or M >= FUSED_LM_HEAD_MIN_M
+
+
+def lm_head_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sample one token per row of ``h`` [M, K] from softmax((h @ w.T) / T) (T <= 0: greedy) without
+    materialising the logits.  Same noise as :func:`sample` (counter-based on (seed, token id)),
+    scored on the bf16-rounded logits, so for equal logits both paths pick the same token.  No
+    top-k / top-p (those rows need the whole distribution: use ``sample`` on the logits)."""
+    M, K = h.shape
+    V = w.shape[0]
+    if not N.use_native(h):
+        import torch.nn.functional as F
+        return sample(F.linear(h.float(), w.float()).to(h.dtype), temperatures, seeds, out=out)
+    out = torch.empty((M,), dtype=torch.int32, device=h.device) if out is None else out
+    ws = torch.empty((2 * M * 2 * (V // 256),), dtype=torch.float32, device=h.device)
+    N.call("penny_lm_head_sample", N.ptr(h), h.stride(0), N.ptr(w), K, M, V,
+           N.ptr(temperatures.to(torch.float32).contiguous()), N.ptr(seeds.contiguous()), N.ptr(ws), N.ptr(out),
+           N.stream())
+    return out
+
+
 def topk_topp_threshold(logits: torch.Tensor, temperatures: torch.Tensor, top_k: torch.Tensor,
                         top_p: torch.Tensor) -> torch.Tensor:
     """The HIP filter's per-row logit threshold (-inf: keep all) -- diagnostics/tests."""

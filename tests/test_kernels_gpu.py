@@ -774,3 +774,55 @@ def test_topp_threshold_is_bitwise_repeatable():
     ths = [topk_topp_threshold(lg, t, k, p).cpu() for _ in range(20)]
     ref = ths[0][0]
     assert all(bool((th == ref).all()) for th in ths)
+
+
+# ------------------------------------------------------------------------------------------------
+# fused LM head + sampler (gemm_prefill.hip EPI_SAMPLE): no logits in HBM
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M,V,K", [(1, 2048, 512), (37, 4096, 1024), (256, 2048, 512), (300, 1024, 256),
+                                   (128, 128256, 4096)])
+def test_fused_lm_head_sampler_matches_logits_then_sampler(M, V, K):
+    """Same tile accumulation as the bf16 tile GEMM -> identical bf16 logits -> the fused sample must
+    equal ops.sample on those logits bit for bit (greedy and Gumbel rows); greedy rows also hold
+    the fp32 reference's max logit up to bf16 rounding."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + V)
+    x, w = rnd(M, K, gen=g).to(DEV), rnd(V, K, scale=0.05, gen=g).to(DEV)
+    temps = torch.tensor([0.0 if i % 3 == 0 else (0.7 if i % 3 == 1 else 1.3) for i in range(M)], device=DEV)
+    seeds = (torch.arange(M, dtype=torch.int64) * 7919 + 11).to(DEV)
+    got = ops.lm_head_sample(x, w, temps, seeds)
+    logits = gemm.prefill_gemm(x, w)
+    want = ops.sample(logits, temps, seeds)
+    assert torch.equal(got.cpu(), want.cpu())
+    ref = (x.float() @ w.float().t())
+    greedy = (temps <= 0).nonzero().flatten()
+    picked = ref[greedy, got[greedy].long()]
+    assert bool((picked >= ref[greedy].max(-1).values - 2e-2 * ref.abs().max()).all())
+    # batch invariance: a row's sample does not depend on the other rows
+    if M > 1:
+        one = ops.lm_head_sample(x[1:2].contiguous(), w, temps[1:2].contiguous(), seeds[1:2].contiguous())
+        assert int(one[0]) == int(got[1])
+
+
+def test_fused_lm_head_graph_decode_falls_back_for_top_p(monkeypatch):
+    """A hipGraph decode bucket captured with the fused sampler still honours top-k / top-p rows
+    (those steps run eagerly through the logits + filtered sampler)."""
+    monkeypatch.setenv("PENNY_FUSED_LM_HEAD", "force")
+    from financial_chatbot_llm_amd.config import EngineConfig
+    from financial_chatbot_llm_amd.engine import LLMEngine, SamplingParams
+    cfg = EngineConfig(model="llama-tiny", device="cuda", num_kv_blocks=64, max_model_len=1024,
+                       max_num_seqs=4, graph_batch_sizes=(1, 2, 4))
+    eng = LLMEngine(cfg)
+    eng.warmup()
+    prompts = [list(range(100, 160)), list(range(7, 30))]
+    greedy = eng.generate(prompts, SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
+    assert eng.runner.stats.get("fused_lm_head_steps", 0) > 0 or any(G.fused for G in eng.runner.graphs.values())
+    filt = eng.generate(prompts, SamplingParams(temperature=0.8, top_p=0.5, top_k=5, max_tokens=6, ignore_eos=True,
+                                                seed=3))
+    assert all(len(o) == 6 for o in greedy + filt)
+    monkeypatch.setenv("PENNY_FUSED_LM_HEAD", "0")
+    eng2 = LLMEngine(cfg)
+    eng2.warmup()
+    # filtered rows take the unfused sampler on both engines (eager fallback vs the unfused graph)
+    assert eng2.generate(prompts, SamplingParams(temperature=0.8, top_p=0.5, top_k=5, max_tokens=6,
+                                                 ignore_eos=True, seed=3)) == filt
