@@ -407,6 +407,32 @@ def bench_lm_head_fused(dev) -> List[Dict]:
     return out
 
 
+def bench_bge_query(dev) -> List[Dict]:
+    """bge-base encoder latency on retrieval-size query batches (the per-turn critical path): the
+    four projections on hipBLASLt (+ the GELU pass) vs the tile kernel with the bias / bias+GELU
+    epilogues (PENNY_PREFILL_GEMM=0 / 1 / force)."""
+    import os
+    from ..models.bert import BertEncoder
+    from ..models.configs import get_model_config
+    enc = BertEncoder.build(get_model_config("bge-base-en"), device=dev)
+    out = []
+    for nq, L in ((1, 16), (8, 16), (24, 20), (64, 24), (128, 32)):
+        ids = [[101] + [(1000 + 7 * q + 13 * j) % 30000 for j in range(L - 2)] + [102] for q in range(nq)]
+        row = {"op": "bge_query", "queries": nq, "tokens": nq * L}
+        fns = {}
+        for mode in ("0", "1", "force"):
+            def f(mode=mode):
+                os.environ["PENNY_PREFILL_GEMM"] = mode
+                enc.encode(ids)
+            fns[f"mode_{mode}"] = f
+        t = interleaved(fns, rounds=5, iters=5)
+        os.environ.pop("PENNY_PREFILL_GEMM", None)
+        row.update({k + "_us": round(v, 1) for k, v in t.items()})
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    return out
+
+
 def bench_gemm_tune_sweep(dev) -> List[Dict]:
     """Prefill GEMMs at every M = 256k: hipBLASLt default heuristic vs a TunableOp-tuned solution
     (tuned here, written to ``PENNY_TUNE_OUT``): is a padded-M + tuned-solution policy worth it?"""
@@ -731,6 +757,7 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
     step of M rows, under every available choice (microseconds; same random operands):
       qkv:     hipBLASLt + rope_kv_write | fused QKV+RoPE+KV-write tile kernel
       o, down: hipBLASLt + add&RMSNorm   | tile kernel bf16 + add&RMSNorm | split-K S slabs + slab RMSNorm
+               | tile kernel adding the residual in place + RMSNorm (hipR)
       gate_up: hipBLASLt + silu_mul      | tile kernel with the SiLU epilogue
     -> the table ops/gemm.py PREFILL_POLICY is written from."""
     from ..ops import gemm
@@ -763,6 +790,10 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
                                                                        1e-5, residual=res))
             fns[f"{name}_hip1"] = (lambda a=a, name=name: ops.rms_norm(gemm.prefill_gemm(a, w[name]), nw, 1e-5,
                                                                         residual=res))
+            # residual added in the GEMM epilogue over the residual stream (in place), then a plain
+            # RMSNorm: the decoder's fuse_residual path (ops.gemm.ResidualSum)
+            fns[f"{name}_hipR"] = (lambda a=a, name=name: ops.rms_norm(gemm.ResidualSum(gemm.prefill_gemm(
+                a, w[name], "residual", residual=res, out=res)), nw, 1e-5, residual=res))
             for S in (2, 4):
                 if K % (64 * S) == 0:
                     P = torch.empty((S, M, H), dtype=torch.float32, device=dev)
@@ -918,10 +949,10 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused,
+                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
-                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "gemm_ablate": bench_gemm_ablate,
+                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]), "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),

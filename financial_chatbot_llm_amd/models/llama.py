@@ -157,15 +157,18 @@ class DecoderModel:
         x = ops.embedding(ids, self.w["embed"], self.vocab_start, self.vocab_end)
         return comm.tp_all_reduce(x) if self.tp_size > 1 else x
 
-    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True) -> torch.Tensor:
+    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True,
+            fuse_residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         p = f"layers.{i}."
         a = linear(h, self.w[p + "gate_up"], epilogue="silu", wt=self.wt.get(p + "gate_up"))  # fused SiLU(gate)*up
-        # TP=1: decode-size batches return split-K slabs, reduced by the next add+RMSNorm
-        out = linear(a, self.w[p + "down"], wt=self.wt.get(p + "down"), slabs=self.tp_size == 1)
+        # TP=1: decode-size batches return split-K slabs, reduced by the next add+RMSNorm; prefill
+        # sizes may add the residual stream in the GEMM epilogue (fuse_residual -> ResidualSum)
+        out = linear(a, self.w[p + "down"], wt=self.wt.get(p + "down"), slabs=self.tp_size == 1,
+                     fuse_residual=fuse_residual)
         return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
 
     def attention(self, i: int, h: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata,
-                  kv: KVCache, reduce: bool = True) -> torch.Tensor:
+                  kv: KVCache, reduce: bool = True, fuse_residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         p = f"layers.{i}."
         T = h.shape[0]
         kc, vc = kv.k(i), kv.v(i)
@@ -199,7 +202,7 @@ class DecoderModel:
             ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
                        workspace=meta.decode_ws, out=attn[tp:], cascade=meta.cascade)
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"),
-                     slabs=self.tp_size == 1)
+                     slabs=self.tp_size == 1, fuse_residual=fuse_residual)
         return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out
 
     def uses_sp(self, T: int) -> bool:
@@ -323,9 +326,11 @@ class DecoderModel:
             p = f"layers.{i}."
             if i > 0:
                 h = ops.rms_norm(x, self.w[p + "in_norm"], c.norm_eps, residual=residual)
-            a = self.attention(i, h, positions, meta, kv)
+            # TP=1: the O / down projections may add the residual stream in their epilogue (in place)
+            fr = residual if self.tp_size == 1 else None
+            a = self.attention(i, h, positions, meta, kv, fuse_residual=fr)
             h = ops.rms_norm(a, self.w[p + "post_norm"], c.norm_eps, residual=residual)
-            x = self.mlp(i, h)
+            x = self.mlp(i, h, fuse_residual=fr)
         return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
 
     def lm_weight(self) -> torch.Tensor:

@@ -154,7 +154,7 @@ class MixtralModel(DecoderModel):
             return F.linear(act, self._dequant(p, "w2", e))
         return F.linear(ops.silu_mul(F.linear(rows, self.w[p + "w13"][e])), self.w[p + "w2"][e])
 
-    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True) -> torch.Tensor:
+    def mlp(self, i: int, h: torch.Tensor, reduce: bool = True, fuse_residual=None) -> torch.Tensor:
         """``reduce=False``: return the TP partial sum (the overlapped forward all-reduces it);
         expert-parallel outputs are already complete (all-gathered) either way."""
         p = f"layers.{i}."

@@ -71,17 +71,24 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
 
 def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
            residual: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
-           slabs: bool = False) -> Union[torch.Tensor, "Slabs"]:
+           slabs: bool = False, fuse_residual: Optional[torch.Tensor] = None) -> Union[torch.Tensor, "Slabs",
+                                                                                     "ResidualSum"]:
     """y = x @ w.T with an optional fused epilogue ("silu": w is gate|up 16-interleaved).
 
     ``wt`` is the fragment-tiled copy of ``w`` (``tile_weight``); when given, decode-sized
     batches run the hand-written MFMA kernels on it.  ``slabs=True`` lets the caller receive the
     split-K GEMM's unreduced :class:`Slabs` (the consumer -- ``ops.rms_norm`` /
-    ``ops.rope_kv_write`` -- sums them in its own pass)."""
+    ``ops.rope_kv_write`` -- sums them in its own pass).  ``fuse_residual`` (the residual stream the
+    consumer's add + RMSNorm would add this output to) lets a prefill-size GEMM add it in its
+    epilogue, in place, returning :class:`ResidualSum` (the norm then only normalises)."""
     M, K = x.shape
     N_ = w.shape[0]
     if M > 256 and prefill_ok(x, w) and epilogue in (None, "silu", "residual"):
-        c = prefill_choice(M, N_, K, epilogue, slabs and residual is None)
+        fr = fuse_residual is not None and epilogue is None and residual is None
+        c = prefill_choice(M, N_, K, epilogue, slabs and residual is None, fused_residual=fr)
+        if c == "R":
+            prefill_gemm(x, w, "residual", residual=fuse_residual, out=fuse_residual)
+            return ResidualSum(fuse_residual)
         if c == "hip":
             return prefill_gemm(x, w, epilogue, residual=residual)
         if c.startswith("S"):
@@ -249,6 +256,22 @@ def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
     return y
 
 
+class ResidualSum:
+    """A row-parallel projection whose residual add already happened: the tile kernel's residual
+    epilogue wrote ``x @ w.T + residual`` over the residual stream in place.  ``ops.rms_norm``
+    given it (with that same residual) only normalises -- one HBM pass less than GEMM -> bf16 ->
+    add&norm, and no [M, N] projection output."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+    @property
+    def shape(self):
+        return self.t.shape
+
+
 class Slabs:
     """A split-K GEMM output left unreduced: f32 partial sums ``P`` [S, M, N].  Consumers that
     read the activation anyway (``ops.rms_norm``, ``ops.rope_kv_write``) sum the slabs inside
@@ -307,10 +330,13 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 #   "lib"  hipBLASLt (+ the separate epilogue pass)       "hip"  tile kernel, fused epilogue
 #   "S<n>" tile kernel split-K into n f32 slabs (only where the consumer reads slabs)
 #   "fused" (QKV only) tile kernel with RoPE + paged-KV-write epilogue (prefill_qkv_rope)
+#   "R"    tile kernel adding the residual stream in place (ResidualSum; the consumer's RMSNorm
+#          then skips the add): O at M >= 3072 is 3-7 % faster than hipBLASLt + add&norm
+#          (profiles/r3_prefill_policy_v4_residual.jsonl); only where the caller passes fuse_residual
 # Shapes without an entry use ``_default_choice``.
 PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (6144, 4096): [(1536, "lib"), (2816, "fused"), (3840, "lib"), (1 << 30, "fused")],     # QKV
-    (4096, 4096): [(1 << 30, "lib")],                                                     # O
+    (4096, 4096): [(2816, "lib"), (1 << 30, "R")],                                        # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
     (4096, 14336): [(1024, "S4"), (2048, "S2"), (1 << 30, "lib")],                        # down
 }
@@ -324,7 +350,8 @@ def _default_choice(M: int, N_: int, K: int, epilogue: Optional[str]) -> str:
     return "hip" if tiles >= 224 or (epilogue in ("silu", "bias_gelu") and tiles >= 112) else "lib"
 
 
-def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slabs: bool = False) -> str:
+def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slabs: bool = False,
+                   fused_residual: bool = False) -> str:
     if os.environ.get("PENNY_PREFILL_GEMM", "1") == "0":
         return "lib"
     force = os.environ.get("PENNY_PREFILL_GEMM") == "force"
@@ -337,7 +364,11 @@ def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slab
                 break
     if choice is None:
         choice = "hip" if force else _default_choice(M, N_, K, epilogue)
+    if force and fused_residual and epilogue is None:
+        choice = "R"
     if choice.startswith("S") and not (slabs and epilogue is None and K % (64 * int(choice[1:])) == 0):
+        choice = "hip" if force else "lib"
+    if choice == "R" and not fused_residual:
         choice = "hip" if force else "lib"
     if choice == "fused":           # only the QKV entry point (qkv_rope_choice) fuses RoPE
         choice = "hip"
@@ -385,12 +416,12 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
             return torch.einsum("smk,snk->smn", xs, w.float().view(N_, S, K // S).transpose(0, 1))
         y = F.linear(x.float(), w.float(), bias.float() if bias is not None else None).to(x.dtype)
         if epilogue == "bias_gelu":
-            return F.gelu(y.float()).to(x.dtype)
-        if epilogue == "silu":
-            return silu_mul(y, interleave16=True)
-        if epilogue == "residual":
-            return (y.float() + residual.float()).to(x.dtype)
-        return y
+            y = F.gelu(y.float()).to(x.dtype)
+        elif epilogue == "silu":
+            y = silu_mul(y, interleave16=True)
+        elif epilogue == "residual":
+            y = (y.float() + residual.float()).to(x.dtype)
+        return out.copy_(y) if out is not None else y
     if epilogue == "slabs":
         y = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
         ldy = N_
@@ -405,13 +436,24 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
     return y
 
 
+# bge query batches up to this many tokens run every projection on the tile kernel: the encoder is
+# launch-bound there (~2 ms for 12 layers) and the fused bias / bias+GELU epilogues save launches and
+# passes -- 1.72 vs 2.15 ms for 1 query, 2.12 vs 2.24 ms for 24, 2.18 vs 2.26 ms for 64 (1.5k tokens)
+# against hipBLASLt + the GELU pass; at 4k tokens the per-shape policy decides
+# (profiles/r3_bge_query_tile_vs_hipblaslt.jsonl)
+BGE_TILE_MAX_M = 2048
+
+
 def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = False) -> torch.Tensor:
-    """Encoder projection bf16(x @ w.T + b) [-> exact GELU]: the tile kernel with the bias (+GELU)
-    epilogue once its tiles fill the chip (bulk ingest), hipBLASLt's bias GEMM + the HIP GELU pass
-    for query-size batches (``PENNY_PREFILL_GEMM=0``: always the library)."""
+    """Encoder projection bf16(x @ w.T + b) [-> exact GELU] on the tile kernel with the bias (+GELU)
+    epilogue: always for query-size batches (<= BGE_TILE_MAX_M tokens), by the measured per-shape
+    policy for bulk ingest; hipBLASLt's bias GEMM + the HIP GELU pass otherwise
+    (``PENNY_PREFILL_GEMM=0``: always the library)."""
     M, K = x.shape
     N_ = w.shape[0]
-    if M > 256 and prefill_ok(x, w) and prefill_choice(M, N_, K, "bias_gelu" if gelu else "bias") == "hip":
+    mode = os.environ.get("PENNY_PREFILL_GEMM", "1")
+    if mode != "0" and prefill_ok(x, w) and (M <= BGE_TILE_MAX_M or mode == "force" or
+                                            prefill_choice(M, N_, K, "bias_gelu" if gelu else "bias") == "hip"):
         return prefill_gemm(x, w, "bias_gelu" if gelu else "bias", bias=b)
     y = F.linear(x, w, b)
     if gelu:

@@ -6,7 +6,7 @@ from typing import Optional, Tuple, Union
 import torch
 
 from . import _native as N
-from .gemm import Slabs
+from .gemm import ResidualSum, Slabs
 
 
 def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
@@ -20,6 +20,9 @@ def rms_norm(x: Union[torch.Tensor, Slabs], w: torch.Tensor, eps: float, residua
     """``residual is None``: y = rms(x).  Otherwise residual <- x + residual (in place, bf16) and
     y = rms(residual) -- the Llama pre-norm pattern, one HBM pass.  ``x`` may be the unreduced
     :class:`~.gemm.Slabs` of a split-K GEMM: the slabs are summed in the same pass."""
+    if isinstance(x, ResidualSum):    # the GEMM epilogue already added x into the residual stream
+        assert residual is None or residual is x.t
+        return rms_norm(x.t, w, eps, None, out)
     if isinstance(x, Slabs):
         S, T, H = x.P.shape
         if N.use_native(x.P):
