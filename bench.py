@@ -185,6 +185,23 @@ async def run(args, ps):
             "plots_ok": sum(r.plots_ok for r in results), "plots_failed": sum(r.plots_failed for r in results)}
 
 
+def _share_host_cpus() -> None:
+    """One process per GPU on a shared host: give each local rank an equal share of the CPUs for
+    its intra-op thread pools (torch / OpenMP default to every core, so 8 ranks would each start
+    one thread per core).  PENNY_PIN_CPUS=1 also pins each rank to its own contiguous CPU slice."""
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if lws <= 1:
+        return
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    cpus = sorted(os.sched_getaffinity(0))
+    per = max(1, len(cpus) // lws)
+    os.environ.setdefault("OMP_NUM_THREADS", str(min(per, 16)))
+    if os.environ.get("PENNY_PIN_CPUS") == "1" and per >= 2:
+        os.sched_setaffinity(0, cpus[lr * per:(lr + 1) * per])
+    import torch
+    torch.set_num_threads(min(per, 16))
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     if args.max_batched_tokens is None:
@@ -192,6 +209,7 @@ def main(argv=None) -> int:
     os.environ.setdefault("LOG_LEVEL", "WARNING")
     if args.decide_always_limit:
         os.environ["PENNY_DECIDE_ALWAYS_LIMIT"] = "1"
+    _share_host_cpus()
     import torch
     import torch.distributed as dist
 

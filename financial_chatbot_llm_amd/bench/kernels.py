@@ -433,6 +433,35 @@ def bench_bge_query(dev) -> List[Dict]:
     return out
 
 
+def bench_gemm_tail(dev, Ms=None) -> List[Dict]:
+    """Tile GEMM with vs without the wave-quantisation tail (K-split tail tiles on idle CUs),
+    interleaved A/B per (projection, M), each with its fused epilogue."""
+    import os
+    from ..ops import gemm
+    shapes = {"qkv": (6144, 4096, None), "o": (4096, 4096, None), "gate_up": (28672, 4096, "silu"),
+              "down": (4096, 14336, None)}
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    ws = {n: rnd(N, K) for n, (N, K, _) in shapes.items()}
+    out = []
+    for M in Ms or [512, 1024, 1536, 2048, 2304, 2560, 3072, 3584]:
+        row = {"op": "gemm_tail", "M": M}
+        for n, (N, K, epi) in shapes.items():
+            x = rnd(M, K)
+            fns = {}
+            for mode in ("0", "1"):
+                def f(mode=mode, x=x, n=n, epi=epi):
+                    os.environ["PENNY_GEMM_TAIL"] = mode
+                    gemm.prefill_gemm(x, ws[n], epi)
+                fns[mode] = f
+            t = interleaved(fns, rounds=5, iters=5)
+            os.environ.pop("PENNY_GEMM_TAIL", None)
+            row[f"{n}_whole_us"] = round(t["0"], 1)
+            row[f"{n}_tail_us"] = round(t["1"], 1)
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    return out
+
+
 def bench_gemm_tune_sweep(dev) -> List[Dict]:
     """Prefill GEMMs at every M = 256k: hipBLASLt default heuristic vs a TunableOp-tuned solution
     (tuned here, written to ``PENNY_TUNE_OUT``): is a padded-M + tuned-solution policy worth it?"""
@@ -949,7 +978,7 @@ def main(argv=None) -> int:
     res = []
     for name in args.only.split(","):
         res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
-                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query,
+                "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query, "gemm_tail": bench_gemm_tail,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]), "gemm_ablate": bench_gemm_ablate,

@@ -43,6 +43,14 @@
 //     is a COUNTED vmcnt(6) once per K-tile (never 0 in the steady state).
 //   * blockIdx is remapped bijectively so each XCD owns a contiguous range of tiles, grouped
 //     4 token-tiles x N so the XCD's 32 concurrent tiles share X and W panels in its L2.
+//   * wave quantisation (TailArgs): when the tile count T is not a multiple of the CU count C, the
+//     first T - L tiles (L = T mod C) run whole, one per workgroup, and each of the L tail tiles is
+//     split over s = C / L workgroups along K -- the last partial round costs 1/s of a tile
+//     instead of a whole one (at M = 512 the QKV GEMM's 48 tiles become 240 workgroups).  Each
+//     split stores its f32 accumulators, releases them (agent fence) and draws a ticket from the
+//     tile's counter; the workgroup drawing s - 1 acquires, adds the other splits' partials into
+//     its registers (in split order: bitwise repeatable), resets the counter and runs the tile's
+//     ordinary epilogue.  No workgroup ever waits on another.
 #include "common.h"
 #include "kv_layout.h"
 
@@ -77,6 +85,14 @@ struct SampleArgs {
   const unsigned long long* seeds;
   float* pv;
   int* pi;
+};
+
+// wave-quantisation tail (above): dpn whole tiles, then L tail tiles x s K-splits; part =
+// [L, s, 256*256] f32, cnt = [L] zero-initialised tickets (self-resetting); s <= 1: no tail
+struct TailArgs {
+  int dpn, L, s;
+  float* part;
+  int* cnt;
 };
 
 struct RopeArgs {
@@ -191,7 +207,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
                                                            void* __restrict__ Y, int ldy,
                                                            const bf16* __restrict__ R, int ldr,
                                                            int M, int N, int S, RopeArgs ra, MoeArgs ma,
-                                                           SampleArgs sa) {
+                                                           SampleArgs sa, TailArgs ta) {
   constexpr int ESZ = FP8 ? 1 : 2;        // bytes per element
   constexpr int BKE = 128 / ESZ;          // elements per K-tile row (128 bytes)
   const char* __restrict__ X = static_cast<const char*>(Xv);
@@ -203,13 +219,22 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   const int g = lane >> 4, col = lane & 15;
 
   // ---- tile of this workgroup: bijective XCD remap, then L2 groups of GM token tiles ----
-  const int Mt = (M + TM - 1) / TM + (FP8 ? ma.E : 0), Nt = N / TN, tiles = Mt * Nt, nwg = tiles * S;
-  int id = blockIdx.x;
-  {
+  const int Mt = (M + TM - 1) / TM + (FP8 ? ma.E : 0), Nt = N / TN, tiles = Mt * Nt;
+  const bool tail = !FP8 && ta.s > 1 && (int)blockIdx.x >= ta.dpn;   // workgroup-uniform
+  int s = 0, tile, tu = 0, tj = 0;
+  if (tail) {
+    const int u = blockIdx.x - ta.dpn;        // tail workgroups are dispatched last, round robin
+    tu = u % ta.L;
+    tj = u / ta.L;
+    tile = ta.dpn + tu;
+  } else {
+    const int nwg = ta.s > 1 ? ta.dpn : tiles * S;
+    int id = blockIdx.x;
     const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
     id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+    s = id / tiles;
+    tile = id - s * tiles;
   }
-  const int s = id / tiles, tile = id - s * tiles;
   const int grp = tile / (GM * Nt), first = grp * GM, gm = min(Mt - first, GM);
   const int within = tile - grp * GM * Nt;
   const int tm = first + within % gm, tn = within / gm;
@@ -230,8 +255,17 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     if (e == ma.E) return;                 // surplus tile of the upper-bound grid: whole WG exits
     W += (long)e * N * K;
   }
-  const int kc = K / S, k0 = s * kc, nt = kc / BKE;
-  PENNY_DASSERT(N % TN == 0 && kc % BKE == 0 && tm < Mt && tn < Nt);
+  int k0, nt;
+  if (tail) {                                 // K-tiles [tj * ntot / s, (tj + 1) * ntot / s)
+    const int ntot = K / BKE, kb = tj * ntot / ta.s, ke = (tj + 1) * ntot / ta.s;
+    k0 = kb * BKE;
+    nt = ke - kb;
+  } else {
+    const int kc = K / S;
+    k0 = s * kc;
+    nt = kc / BKE;
+  }
+  PENNY_DASSERT(N % TN == 0 && nt >= 1 && tm < Mt && tn < Nt);
 
   // ---- per-lane LDS-DMA sources: half h, piece i -> LDS rows 16w + 8i .. +7 of that half ----
   const char* src[4][2];
@@ -388,6 +422,47 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     }
   }
   if (wa == 0) bar();
+
+  if (!FP8 && tail) {
+    // ---- wave-quantisation tail: publish this K-split's accumulators; the last split combines ----
+    // partial layout [wave][f][t][lane] f32x4: every store / load instruction moves 1 KiB contiguous
+    float* mine = ta.part + ((long)tu * ta.s + tj) * (TM * TN);
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<f32x4*>(mine + ((((w * 8 + f) * 4 + t) * 64 + lane) << 2)) = acc[f][t];
+    wait_vm<0>();
+    __syncthreads();                          // every wave's stores issued and retired
+    int* flag = reinterpret_cast<int*>(smem); // LDS is free: the K loop is over for all waves
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      wait_vm<0>();
+      const int old = __hip_atomic_fetch_add(&ta.cnt[tu], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == ta.s - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        wait_vm<0>();
+        __hip_atomic_store(&ta.cnt[tu], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+      }
+      *reinterpret_cast<volatile int*>(flag) = last;
+    }
+    __syncthreads();
+    if (!*reinterpret_cast<volatile int*>(flag)) return;
+    // sum every split (its own included, re-read) in split order whichever drew the last ticket, so
+    // the result is bitwise repeatable; each pass issues its 32 independent 16-B loads at once
+    const float* base = ta.part + (long)tu * ta.s * (TM * TN) + ((w * 32 * 64 + lane) << 2);
+    for (int j = 0; j < ta.s; ++j) {
+      const float* pj = base + (long)j * (TM * TN);
+#pragma unroll
+      for (int f = 0; f < 8; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(pj + ((f * 4 + t) * 64 << 2));
+          acc[f][t] = j == 0 ? v : acc[f][t] + v;
+        }
+    }
+  }
 
   // ---- epilogue: lane holds Y[m0 + wb*64 + 16t + col][n0 + wa*128 + 16f + 4g + r], r = 0..3 ----
   // bf16 outputs leave as 16-B stores: pair16 swaps 8-B halves between lane rows g and g^1 (same
@@ -559,19 +634,42 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
 
 template <int EPI, int ABL = 0, int BAL = 1>
 static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
-                   const void* R, int ldr, int M, int N, int S, const RopeArgs& ra) {
+                   const void* R, int ldr, int M, int N, int S, const RopeArgs& ra, const TailArgs& ta = TailArgs{}) {
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy,
-                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{});
+                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{}, ta);
 }
 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
+
+// Tail plan for T tiles on `cus` CUs (S == 1 launches): L = T mod cus tiles split s = cus / L ways
+// (>= 2, each split >= 16 K-tiles), workspace permitting (ws_floats >= L * s * 256 * 256, ncnt >= L).
+// Returns the grid; ta.s <= 1 means no tail.
+static dim3 tail_plan(int M, int N, int K, int cus, float* ws, long ws_floats, int* cnt, int ncnt, TailArgs& ta) {
+  ta = TailArgs{};
+  const int T = ((M + TM - 1) / TM) * (N / TN);
+  if (cus > 0 && ws && cnt) {
+    const int L = T % cus, ntot = K / BK;
+    int s = L ? cus / L : 0;
+    s = min(s, ntot / 16);          // >= 16 K-tiles per split: the f32 partial store + combine of a
+                                    // 256x256 tile costs ~ a few K-tiles' time (bench/kernels.py gemm_tail)
+    if (L && s >= 2 && L <= ncnt && (long)L * s * TM * TN <= ws_floats) {
+      ta = TailArgs{T - L, L, s, ws, cnt};
+      return dim3((unsigned)(T - L + L * s));
+    }
+  }
+  return dim3((unsigned)T);
+}
 
 // Contract (checked): N % 256 == 0, K % (64*S) == 0, ldx % 8 == 0, rows 16-B aligned; EPI_SILU
 // needs S == 1 and ldy % 8 == 0 (Y is [M, N/2]); EPI_SLAB writes P [S, M, N] f32 (ldy unused);
 // EPI_RESID needs R (row stride ldr, ldr % 8 == 0) and S == 1; EPI_BIAS(_GELU) take the bias [N]
 // as R.
+// tail_ws / tail_cnt / cus (optional, null / 0: off): the wave-quantisation tail's workspace (f32
+// [tail_ws_floats]), its zero-initialised ticket counters [tail_ncnt] and the device's CU count;
+// one workspace per stream (launches on one stream run in order, the counters reset themselves).
 PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, void* Y, int ldy, const void* R,
-                                 int ldr, int M, int N, int S, int epi, hipStream_t stream) {
+                                 int ldr, int M, int N, int S, int epi, float* tail_ws, long tail_ws_floats,
+                                 int* tail_cnt, int tail_ncnt, int cus, hipStream_t stream) {
   if (M <= 0) return 0;
   if (N % TN || S < 1 || K % (BK * S) || ldx % 8 || epi < 0 || epi > 6 || epi == EPI_ROPE)
     return (int)hipErrorInvalidValue;
@@ -579,15 +677,17 @@ PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, v
   if (epi == EPI_RESID && (!R || ldr % 8)) return (int)hipErrorInvalidValue;
   if ((epi == EPI_BIAS || epi == EPI_BIAS_GELU) && !R) return (int)hipErrorInvalidValue;
   if ((long)((M + TM - 1) / TM) * (N / TN) * S > (1L << 30)) return (int)hipErrorInvalidValue;
-  const dim3 grid = grid_for(M, N, S);
+  TailArgs ta{};
+  const dim3 grid = S == 1 ? tail_plan(M, N, K, cus, tail_ws, tail_ws_floats, tail_cnt, tail_ncnt, ta)
+                           : grid_for(M, N, S);
   const RopeArgs ra{};
   switch (epi) {
-    case EPI_BF16: launch<EPI_BF16>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
-    case EPI_SILU: launch<EPI_SILU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    case EPI_BF16: launch<EPI_BF16>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
+    case EPI_SILU: launch<EPI_SILU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
     case EPI_SLAB: launch<EPI_SLAB>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
-    case EPI_BIAS: launch<EPI_BIAS>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
-    case EPI_BIAS_GELU: launch<EPI_BIAS_GELU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra); break;
-    default: launch<EPI_RESID>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra);
+    case EPI_BIAS: launch<EPI_BIAS>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
+    case EPI_BIAS_GELU: launch<EPI_BIAS_GELU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
+    default: launch<EPI_RESID>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta);
   }
   return (int)hipGetLastError();
 }
@@ -597,13 +697,16 @@ PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, v
 // Contract (checked): N == (Hq + 2*Hkv)*128, N % 256 == 0, K % 64 == 0, ldx % 8 == 0.
 PENNY_API int penny_gemm_prefill_qkv_rope(const void* X, int ldx, const void* W, int K, int M, const int* positions,
                                           const float* cos_sin, const int* slots, void* q_out, void* k_cache,
-                                          void* v_cache, int Hq, int Hkv, hipStream_t stream) {
+                                          void* v_cache, int Hq, int Hkv, float* tail_ws, long tail_ws_floats,
+                                          int* tail_cnt, int tail_ncnt, int cus, hipStream_t stream) {
   if (M <= 0) return 0;
   const int N = (Hq + 2 * Hkv) * 128;
   if (Hq <= 0 || Hkv <= 0 || N % TN || K % BK || ldx % 8 || !positions || !cos_sin || !slots || !q_out)
     return (int)hipErrorInvalidValue;
   const RopeArgs ra{positions, cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv};
-  launch<EPI_ROPE>(grid_for(M, N, 1), stream, X, ldx, W, K, nullptr, 0, nullptr, 0, M, N, 1, ra);
+  TailArgs ta{};
+  const dim3 grid = tail_plan(M, N, K, cus, tail_ws, tail_ws_floats, tail_cnt, tail_ncnt, ta);
+  launch<EPI_ROPE>(grid, stream, X, ldx, W, K, nullptr, 0, nullptr, 0, M, N, 1, ra, ta);
   return (int)hipGetLastError();
 }
 
@@ -640,10 +743,10 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
   const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
   if (epi == EPI_MOE_SILU)
     hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_SILU, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{});
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
   else
     hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_ROUTE, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{});
+                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
   return (int)hipGetLastError();
 }
 
@@ -688,7 +791,7 @@ PENNY_API int penny_lm_head_sample(const void* X, int ldx, const void* W, int K,
   int* pi = reinterpret_cast<int*>(pv + (long)M * P);
   const SampleArgs sa{temps, seeds, pv, pi};
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI_SAMPLE>), grid_for(M, V, 1), dim3(512), 0, stream, X, ldx, W, K,
-                     nullptr, 0, (const bf16*)nullptr, 0, M, V, 1, RopeArgs{}, MoeArgs{}, sa);
+                     nullptr, 0, (const bf16*)nullptr, 0, M, V, 1, RopeArgs{}, MoeArgs{}, sa, TailArgs{});
   hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, out);
   return (int)hipGetLastError();
 }

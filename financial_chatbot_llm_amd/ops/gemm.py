@@ -432,8 +432,29 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
         ldy = y.stride(0)
     R = bias if epilogue in ("bias", "bias_gelu") else residual
     N.call("penny_gemm_prefill", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), ldy, N.ptr(R),
-           residual.stride(0) if residual is not None else 0, M, N_, S, PREFILL_EPI[epilogue], N.stream())
+           residual.stride(0) if residual is not None else 0, M, N_, S, PREFILL_EPI[epilogue],
+           *tail_workspace(x.device), N.stream())
     return y
+
+
+# Wave-quantisation tail of the tile kernel (gemm_prefill.hip TailArgs): one workspace per
+# (device, stream) -- f32 partial tiles of at most one round of tail workgroups (64 MB) and
+# self-resetting ticket counters.  PENNY_GEMM_TAIL=0 launches whole tiles only (A/B).
+_TAIL_WS: Dict[Tuple[int, int], Tuple[torch.Tensor, torch.Tensor, int]] = {}
+
+
+def tail_workspace(dev: torch.device) -> Tuple:
+    if os.environ.get("PENNY_GEMM_TAIL", "1") == "0":
+        return (None, 0, None, 0, 0)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), torch.cuda.current_stream(dev).cuda_stream)
+    ent = _TAIL_WS.get(key)
+    if ent is None:
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        part = torch.empty((cus * 256 * 256,), dtype=torch.float32, device=dev)
+        cnt = torch.zeros((cus,), dtype=torch.int32, device=dev)
+        ent = _TAIL_WS[key] = (part, cnt, cus)
+    part, cnt, cus = ent
+    return (N.ptr(part), part.numel(), N.ptr(cnt), cnt.numel(), cus)
 
 
 # bge query batches up to this many tokens run every projection on the tile kernel: the encoder is
@@ -474,7 +495,7 @@ def prefill_qkv_rope(x: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, 
                              v_cache, Hq, Hkv, 128)
     q = torch.empty((M, Hq, 128), dtype=x.dtype, device=x.device)
     N.call("penny_gemm_prefill_qkv_rope", N.ptr(x), x.stride(0), N.ptr(w), K, M, N.ptr(positions), N.ptr(cos_sin),
-           N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache), Hq, Hkv, N.stream())
+           N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache), Hq, Hkv, *tail_workspace(x.device), N.stream())
     return q
 
 

@@ -826,3 +826,25 @@ def test_fused_lm_head_graph_decode_falls_back_for_top_p(monkeypatch):
     # filtered rows take the unfused sampler on both engines (eager fallback vs the unfused graph)
     assert eng2.generate(prompts, SamplingParams(temperature=0.8, top_p=0.5, top_k=5, max_tokens=6,
                                                  ignore_eos=True, seed=3)) == filt
+
+
+@pytest.mark.parametrize("M,N_,K,epi", [(512, 6144, 4096, None), (2560, 1024, 2048, "silu"), (300, 512, 1024, "residual"),
+                                        (1000, 768, 768, "bias_gelu")])
+def test_prefill_gemm_wave_quantisation_tail(M, N_, K, epi, monkeypatch):
+    """Tail tiles split along K over idle CUs (last split combines in registers) equal the whole-tile
+    launch up to f32 summation order, every call (the ticket counters reset themselves)."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + N_)
+    x, w = rnd(M, K, gen=g).to(DEV), rnd(N_, K, scale=0.05, gen=g).to(DEV)
+    kw = {}
+    if epi == "residual":
+        kw["residual"] = rnd(M, N_, gen=g).to(DEV)
+    if epi == "bias_gelu":
+        kw["bias"] = rnd(N_, gen=g).to(DEV)
+    monkeypatch.setenv("PENNY_GEMM_TAIL", "0")
+    whole = gemm.prefill_gemm(x, w, epi, **kw)
+    monkeypatch.setenv("PENNY_GEMM_TAIL", "1")
+    outs = [gemm.prefill_gemm(x, w, epi, **kw) for _ in range(3)]
+    for y in outs:
+        close(y, whole, atol=1e-2 * whole.float().abs().max().item())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
