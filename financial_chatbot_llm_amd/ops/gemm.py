@@ -325,20 +325,22 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 
 
 # Which path each Llama-3-8B projection takes at a prefill step of M rows (M > 256), measured with
-# its consumer on MI355X, interleaved A/B (bench/kernels.py prefill_policy,
-# profiles/r3_prefill_policy_v2.jsonl): (N, K) -> [(max M, choice), ...], first match wins.
+# its consumer on MI355X, interleaved A/B (bench/kernels.py prefill_policy), with the tile kernel's
+# wave-quantisation tail (profiles/r3_prefill_policy_v5_tail.jsonl; before the tail:
+# r3_prefill_policy_v3_widestores.jsonl, the residual epilogue: r3_prefill_policy_v4_residual.jsonl):
+# (N, K) -> [(max M, choice), ...], first match wins.
 #   "lib"  hipBLASLt (+ the separate epilogue pass)       "hip"  tile kernel, fused epilogue
 #   "S<n>" tile kernel split-K into n f32 slabs (only where the consumer reads slabs)
 #   "fused" (QKV only) tile kernel with RoPE + paged-KV-write epilogue (prefill_qkv_rope)
 #   "R"    tile kernel adding the residual stream in place (ResidualSum; the consumer's RMSNorm
-#          then skips the add): O at M >= 3072 is 3-7 % faster than hipBLASLt + add&norm
-#          (profiles/r3_prefill_policy_v4_residual.jsonl); only where the caller passes fuse_residual
+#          then skips the add): O from M = 2816 is 3-5 % faster than hipBLASLt + add&norm; only
+#          where the caller passes fuse_residual
 # Shapes without an entry use ``_default_choice``.
 PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
-    (6144, 4096): [(1536, "lib"), (2816, "fused"), (3840, "lib"), (1 << 30, "fused")],     # QKV
-    (4096, 4096): [(2816, "lib"), (1 << 30, "R")],                                        # O
+    (6144, 4096): [(1280, "lib"), (1 << 30, "fused")],                                    # QKV
+    (4096, 4096): [(2560, "lib"), (1 << 30, "R")],                                        # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
-    (4096, 14336): [(1024, "S4"), (2048, "S2"), (1 << 30, "lib")],                        # down
+    (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "lib")],         # down
 }
 
 
