@@ -16,7 +16,9 @@
 
 // SLAB: the QKV activation arrives as the S f32 split-K slabs [S, T, width] of the QKV GEMM
 // (gemm_splitk.hip) and is reduced here, in the same pass that rotates and scatters it.
-template <int D, bool SLAB>
+// QK: no paged cache -- rotated q AND k heads go to q_out [T, Hq + Hkv, D] (k heads after the q
+// heads), v is left in qkv: the context-parallel prefill, whose K/V travel the ring as tensors.
+template <int D, bool SLAB, bool QK = false>
 __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restrict__ positions,
                                const float* __restrict__ cos_sin, const int* __restrict__ slots,
                                bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
@@ -26,7 +28,7 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
   constexpr int VU = D / 8;     // copy units per v head
   const int t = blockIdx.x;
   const int pos = positions[t];
-  const int slot = slots[t];
+  const int slot = QK ? -1 : slots[t];
   PENNY_DASSERT(pos >= 0 && slot >= -1);
   const int width = (Hq + 2 * Hkv) * D;
   const bf16* row = qkv + (long)t * width;
@@ -62,7 +64,11 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
         }
       }
       const uint4 p1 = pack8(x1), p2 = pack8(x2);
-      if (h < Hq) {
+      if (QK) {
+        bf16* dst = q_out + ((long)t * (Hq + Hkv) + h) * D;
+        *reinterpret_cast<uint4*>(dst + c * 8) = p1;
+        *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
+      } else if (h < Hq) {
         bf16* dst = q_out + ((long)t * Hq + h) * D;
         *reinterpret_cast<uint4*>(dst + c * 8) = p1;
         *reinterpret_cast<uint4*>(dst + HALF + c * 8) = p2;
@@ -72,7 +78,7 @@ __global__ void rope_kv_kernel(const bf16* __restrict__ qkv, const int* __restri
         *reinterpret_cast<uint4*>(dst + k_index(off, c * 8, D)) = p1;
         *reinterpret_cast<uint4*>(dst + k_index(off, HALF + c * 8, D)) = p2;
       }
-    } else if (slot >= 0) {
+    } else if (!QK && slot >= 0) {
       const int v = u - n_rot;
       const int h = v / VU, c = v % VU;
       float x[8];
@@ -117,4 +123,24 @@ PENNY_API int penny_rope_kv_write_slabs(const void* P, int S, const int* positio
   if (S < 1) return (int)hipErrorInvalidValue;
   return launch_rope_kv<true>(nullptr, (const float*)P, S, positions, cos_sin, slots, q_out, k_cache, v_cache, T, Hq,
                               Hkv, D, apply_rope, stream);
+}
+
+// Context-parallel form: rotated q and k heads of qkv [T, (Hq + 2*Hkv) * D] -> qk [T, Hq + Hkv, D]
+// (no KV-cache write; v stays in qkv).  positions [T] are the zig-zag shard's global positions.
+PENNY_API int penny_rope_qk(const void* qkv, const int* positions, const float* cos_sin, void* qk, int T, int Hq,
+                            int Hkv, int D, hipStream_t stream) {
+  if (T <= 0) return 0;
+  const dim3 grid(T, T <= 512 ? 2 : 1);
+  if (D == 128) {
+    hipLaunchKernelGGL((rope_kv_kernel<128, false, true>), grid, dim3(256), 0, stream, (const bf16*)qkv, positions,
+                       cos_sin, (const int*)nullptr, (bf16*)qk, (bf16*)nullptr, (bf16*)nullptr, Hq, Hkv, 1,
+                       (const float*)nullptr, 0, T);
+  } else if (D == 64) {
+    hipLaunchKernelGGL((rope_kv_kernel<64, false, true>), grid, dim3(256), 0, stream, (const bf16*)qkv, positions,
+                       cos_sin, (const int*)nullptr, (bf16*)qk, (bf16*)nullptr, (bf16*)nullptr, Hq, Hkv, 1,
+                       (const float*)nullptr, 0, T);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
 }

@@ -287,7 +287,8 @@ class DecoderModel:
         prefill kernel on the GPU), then O / MLP on the local rows.  Returns the final hidden
         states of the local rows.  ``kv_sink(layer, k, v)`` receives each layer's local K/V shard
         (``zigzag_unshard`` of every rank's shards is the full cache for the decode rank)."""
-        from ..ops.attention import _rope_ref
+        from ..ops.attention import rope_qk
+        from ..ops.gemm import Slabs
         from ..parallel import context as cpx
         import torch.distributed as dist
         c = self.cfg
@@ -303,10 +304,14 @@ class DecoderModel:
             p = f"layers.{i}."
             if i > 0:
                 h = ops.rms_norm(x, self.w[p + "in_norm"], c.norm_eps, residual=residual)
-            qkv = linear(h, self.w[p + "qkv"]).view(T, self.hq + 2 * self.hkv, self.D)
-            q = _rope_ref(qkv[:, :self.hq], pos, self.cos_sin).to(h.dtype).contiguous()
-            k = _rope_ref(qkv[:, self.hq:self.hq + self.hkv], pos, self.cos_sin).to(h.dtype).contiguous()
-            v = qkv[:, self.hq + self.hkv:].contiguous()
+            qkv = linear(h, self.w[p + "qkv"])
+            if isinstance(qkv, Slabs):
+                qkv = qkv.materialize()
+            # RoPE of q and k heads in one HIP pass at the shard's zig-zag positions (no cache write)
+            qk = rope_qk(qkv, pos, self.cos_sin, self.hq, self.hkv, self.D)
+            q = qk[:, :self.hq].contiguous()
+            k = qk[:, self.hq:].contiguous()
+            v = qkv.view(T, self.hq + 2 * self.hkv, self.D)[:, self.hq + self.hkv:].contiguous()
             if kv_sink is not None:
                 kv_sink(i, k, v)
             a = cpx.ring_attention(q, k, v, total_len, scale=self.scale, causal=True, group=group, block_fn=block)

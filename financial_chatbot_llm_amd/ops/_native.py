@@ -42,6 +42,7 @@ _SIGS = {
     "penny_moe_gemm_prefill_fp8": [P, c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gelu": [P, c_long, P],
     "penny_embedding": [P, P, P, c_int, c_int, c_int, c_int, P],
+    "penny_rope_qk": [P, P, P, P, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_rope_kv_write_slabs": [P, c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P,

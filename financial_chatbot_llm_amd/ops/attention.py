@@ -130,6 +130,20 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[
 # --------------------------------------------------------------------------------------------
 # Attention
 # --------------------------------------------------------------------------------------------
+def rope_qk(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor, Hq: int, Hkv: int,
+            D: int) -> torch.Tensor:
+    """Rotated q and k heads of the fused QKV activation, no KV-cache write: [T, Hq + Hkv, D] (the
+    context-parallel prefill passes K/V around the ring as tensors).  HIP (``penny_rope_qk``) on
+    the GPU, the fp32 reference on CPU."""
+    T = qkv.shape[0]
+    if N.use_native(qkv):
+        qk = torch.empty((T, Hq + Hkv, D), dtype=qkv.dtype, device=qkv.device)
+        N.call("penny_rope_qk", N.ptr(qkv.contiguous()), N.ptr(positions.to(torch.int32).contiguous()),
+               N.ptr(cos_sin), N.ptr(qk), T, Hq, Hkv, D, N.stream())
+        return qk
+    return _rope_ref(qkv.view(T, -1, D)[:, :Hq + Hkv], positions, cos_sin).to(qkv.dtype)
+
+
 def gather_kv_ref(k_cache: torch.Tensor, v_cache: torch.Tensor, blocks: torch.Tensor, n: int):
     """-> K, V [n, Hkv, D] for one sequence (inverse of the paged layout)."""
     Hkv = k_cache.shape[1]

@@ -848,3 +848,19 @@ def test_prefill_gemm_wave_quantisation_tail(M, N_, K, epi, monkeypatch):
     for y in outs:
         close(y, whole, atol=1e-2 * whole.float().abs().max().item())
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_rope_qk_matches_reference(D):
+    """Context-parallel RoPE (penny_rope_qk): rotated q and k heads at arbitrary (zig-zag) positions,
+    no cache write, vs the fp32 reference."""
+    from financial_chatbot_llm_amd.ops.attention import _rope_ref, rope_cos_sin, rope_qk
+    g = torch.Generator().manual_seed(D)
+    T, Hq, Hkv = 300, 8, 2
+    qkv = rnd(T, (Hq + 2 * Hkv) * D, gen=g)
+    pos = torch.randperm(4096, generator=g)[:T].to(torch.int32)
+    cs = rope_cos_sin(D, 4096, 500000.0)
+    got = rope_qk(qkv.to(DEV), pos.to(DEV), cs.to(DEV), Hq, Hkv, D)
+    ref = _rope_ref(qkv.view(T, -1, D)[:, :Hq + Hkv].float(), pos, cs)
+    assert got.shape == (T, Hq + Hkv, D)
+    close(got, ref, atol=2e-2)
