@@ -38,6 +38,10 @@ def log(msg: str) -> None:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree per replica (config 4: --model llama3-70b --tp 8 --tool-steps 3); "
+                         "WORLD_SIZE / tp replicas, each TP leader serves --convs conversations, the other ranks "
+                         "replay its steps")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--convs", type=int, default=128, help="concurrent conversations per GPU")
@@ -85,11 +89,39 @@ async def run(args, ps):
     from financial_chatbot_llm_amd.config import EngineConfig
     from financial_chatbot_llm_amd.engine.async_engine import AsyncEngine
     from financial_chatbot_llm_amd.engine.backend import EngineLLM
-    from financial_chatbot_llm_amd.parallel.dist import barrier
+    from financial_chatbot_llm_amd.parallel.dist import barrier as world_barrier
+
+    def barrier() -> None:
+        """Timing barrier of the replicas: the TP leaders only (followers sit in their step loop)."""
+        if args.tp == 1:
+            world_barrier()
+        elif ps.dp_group is not None:
+            import torch.distributed as dist
+            if ps.backend == "nccl":
+                dist.barrier(group=ps.dp_group, device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier(group=ps.dp_group)
     from financial_chatbot_llm_amd.retrieval import BgeEmbedder, DeviceVectorStore, RetrievalService
 
     on_gpu = args.device == "cuda"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
+    ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
+                        max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
+                        graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype, tp_size=args.tp,
+                        # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
+                        kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
+                        sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)),
+                        step_time_target_ms=float(os.environ.get("PENNY_STEP_TIME_TARGET_MS",
+                                                                 EngineConfig.step_time_target_ms)))
+    if args.tp > 1 and not ps.is_tp_leader:
+        # TP follower: the same engine shard, warmed up (graph capture) in lockstep with its leader,
+        # then replays every step the leader broadcasts until the leader's engine shuts down
+        from financial_chatbot_llm_amd.engine.llm_engine import LLMEngine
+        eng = LLMEngine(ecfg)
+        eng.warmup()
+        eng.follower_loop()
+        return None
 
     def sync() -> None:
         if on_gpu:
@@ -101,16 +133,12 @@ async def run(args, ps):
     retrieval = RetrievalService(embedder, store)
     log(f"retrieval ready ({args.corpus} vectors) in {time.perf_counter() - t0:.1f}s")
 
-    sizes = tuple(s for s in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256) if s <= max(2 * args.convs, 1))
-    ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
-                        max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
-                        graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype,
-                        # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
-                        kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
-                        sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)),
-                        step_time_target_ms=float(os.environ.get("PENNY_STEP_TIME_TARGET_MS",
-                                                                 EngineConfig.step_time_target_ms)))
-    if args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
+    if args.tp > 1:     # leader of a TP group: its followers warm up (capture graphs) alongside it
+        from financial_chatbot_llm_amd.engine.llm_engine import LLMEngine
+        core = LLMEngine(ecfg)
+        core.warmup()
+        engine = AsyncEngine(engine=core, warmup=False)
+    elif args.engine == "process":   # engine core in its own interpreter: no GIL shared with serving
         from financial_chatbot_llm_amd.engine.process_engine import ProcessAsyncEngine
         engine = ProcessAsyncEngine(ecfg, device_index=torch.cuda.current_device() if on_gpu else None)
     else:
@@ -214,13 +242,15 @@ def main(argv=None) -> int:
     import torch.distributed as dist
 
     from financial_chatbot_llm_amd.parallel.dist import init_distributed
-    ps = init_distributed(tp_size=1, device_type=args.device)
+    ps = init_distributed(tp_size=args.tp, device_type=args.device)
     if ps.world_size != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ps.world_size}")
     res = asyncio.run(run(args, ps))
     if ps.world_size > 1:
+        # every rank joins (TP followers contribute None); the replicas' results are the leaders'
         allr = [None] * ps.world_size
         dist.all_gather_object(allr, res)
+        allr = [r for r in allr if r is not None]
     else:
         allr = [res]
     if ps.rank == 0:
@@ -237,7 +267,7 @@ def main(argv=None) -> int:
             "dtype": "bf16" if args.dtype == "bf16" else "bf16 (fp8 e4m3 MoE experts)",
             "data": f"synthetic conversations + {args.corpus:,}-vector synthetic corpus per GPU; "
                     "random-init weights of the real architectures",
-            "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": args.embed_model, "global_batch": args.convs * ps.world_size,
+            "config": {"model": MODEL_LABELS.get(args.model, args.model), "embedder": args.embed_model, "global_batch": args.convs * ps.dp_size,
                        "convs_per_gpu": args.convs, "respond_tokens": args.respond_tokens,
                        "arrival": "closed-loop per conversation" if args.arrival == "closed" else "lock-step waves",
                        "tool_steps": 0 if args.no_tools else args.tool_steps,
@@ -246,7 +276,7 @@ def main(argv=None) -> int:
                                          "reference few-shot: time windows send no limit (10000 -> token clamp)"),
                        "agent": "single-chain chat (no tools)" if args.no_tools else "tool-calling RAG agent",
                        "corpus_vectors": args.corpus, "seq_len": args.max_model_len,
-                       "parallelism": f"dp{ps.world_size}"},
+                       "parallelism": f"dp{ps.dp_size}" if args.tp == 1 else f"dp{ps.dp_size}tp{args.tp}"},
             "p50_ttft_ms": None if p50 is None else round(p50, 1),
             "p99_ttft_ms": None if p99 is None else round(p99, 1),
             "turn_errors": sum(r["errors"] for r in allr),

@@ -71,3 +71,37 @@ def test_bench_two_ranks_on_one_gpu_json_contract():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 2)
+
+
+@pytest.mark.timeout(400)
+def test_bench_tensor_parallel_replica_gloo_json_contract():
+    """--tp 2 over 2 ranks (config 4's process model at small scale): one replica whose TP follower
+    replays the leader's steps; the JSON counts both GPUs and the replica's conversations."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--tp", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=380, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp1tp2" and d["config"]["global_batch"] == 3
+    assert d["turn_errors"] == 0 and d["value"] > 0
+    assert abs(d["ms_per_step"] - 1e3 * 3 / d["value"]) / d["ms_per_step"] < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_tensor_parallel_replica_on_one_gpu_json_contract():
+    """--tp 2 on the device: leader and follower share cuda:0 (gloo control plane, the TP all-reduces
+    on the custom IPC kernels inside the captured decode graphs)."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", PENNY_DIST_BACKEND="gloo", PENNY_KV_FRACTION="0.05")
+    gpu_args = ["--device" if a == "--device" else ("cuda" if a == "cpu" else a) for a in ARGS]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--tp", "2", *gpu_args]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["config"]["parallelism"] == "dp1tp2" and d["turn_errors"] == 0 and d["value"] > 0
