@@ -275,6 +275,48 @@ def bench_prefill_mixed(dev) -> List[Dict]:
     return out
 
 
+def bench_prefill_spec_split(dev) -> List[Dict]:
+    """Mixed steps with speculative chunks (9 query tokens behind 5k-token contexts): one launch of
+    the 8-wave kernel over every sequence (LPT work list; a spec chunk's 36 rows fill one 256-row
+    tile) vs the long chunks on the 8-wave kernel + the spec chunks on the 4-wave 128-row kernel."""
+    out = []
+    g = torch.Generator(device=dev).manual_seed(3)
+    Hq, Hkv, D = 32, 8, 128
+    steps = {"respond+4decides+16spec": [(1500, 3600)] + [(220, 4600)] * 4 + [(9, 5200)] * 16,
+             "2decides+32spec": [(220, 4600)] * 2 + [(9, 5200)] * 32,
+             "respond+64spec": [(1500, 3600)] + [(9, 4800)] * 64}
+    for name, shape in steps.items():
+        tables, kc, vc = _paged_varlen(shape, Hkv, D, dev, g)
+        qlens = [q for q, _ in shape]
+        nb = sum(1 for q in qlens if q * (Hq // Hkv) > 128)
+        T, T1 = sum(qlens), sum(qlens[:nb])
+        q = torch.randn((T, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=dev)
+        lens = torch.tensor([c for _, c in shape], dtype=torch.int32, device=dev)
+        o = torch.empty_like(q)
+        wl = ops.attention.prefill_work_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv)
+        wd = torch.from_numpy(wl).to(dev)
+        cu1, lens1, tb1 = cu[:nb + 1], lens[:nb], tables[:nb]
+        wl1 = ops.attention.prefill_work_list(cu1.cpu().numpy(), lens1.cpu().numpy(), Hq // Hkv)
+        wd1 = torch.from_numpy(wl1).to(dev)
+        cu2, lens2, tb2 = (cu[nb:] - T1).contiguous(), lens[nb:].contiguous(), tables[nb:].contiguous()
+        q2, o2 = q[T1:], o[T1:]
+
+        def split():
+            ops.prefill(q[:T1], cu1, lens1, tb1, kc, vc, 0.088, True, max(qlens[:nb]), out=o[:T1], work=wd1)
+            ops.prefill(q2, cu2, lens2, tb2, kc, vc, 0.088, True, max(qlens[nb:]), out=o2)
+        ref = ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), work=wd).clone()
+        split()
+        err = float((o.float() - ref.float()).abs().max())
+        ts = interleaved({"one": lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
+                                                     work=wd), "split": split}, rounds=7, iters=5)
+        row = {"op": "prefill_spec_split", "step": name, "T": T, "one_launch_us": round(ts["one"], 1),
+               "split_us": round(ts["split"], 1), "max_abs_diff": err}
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
 def bench_elementwise(dev) -> List[Dict]:
     out = []
     for T, H in [(64, 4096), (8192, 4096)]:
@@ -977,7 +1019,7 @@ def main(argv=None) -> int:
     dev = torch.device("cuda")
     res = []
     for name in args.only.split(","):
-        res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "elementwise": bench_elementwise,
+        res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "prefill_spec_split": bench_prefill_spec_split, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query, "gemm_tail": bench_gemm_tail,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
