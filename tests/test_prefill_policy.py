@@ -1,0 +1,43 @@
+"""Host-side logic of the prefill GEMM policy (ops/gemm.py) and its fused-residual path, on CPU."""
+import torch
+
+from financial_chatbot_llm_amd import ops
+from financial_chatbot_llm_amd.ops import gemm
+
+
+def test_policy_table_choices(monkeypatch):
+    monkeypatch.delenv("PENNY_PREFILL_GEMM", raising=False)
+    # O: the residual epilogue only where the caller can take it, else the library
+    assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=True) == "R"
+    assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=False) == "lib"
+    assert gemm.prefill_choice(2048, 4096, 4096, None, True, fused_residual=True) == "lib"
+    # down: split-K slabs only when the consumer reads slabs
+    assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=True) == "S4"
+    assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=False) == "lib"
+    assert gemm.prefill_choice(1280, 4096, 14336, None, slabs=True) == "hip"
+    # gate|up + SiLU on the tile kernel from 512 rows
+    assert gemm.prefill_choice(512, 28672, 4096, "silu") == "hip"
+    assert gemm.prefill_choice(256, 28672, 4096, "silu") == "lib"
+    # force: every tile path, the residual epilogue where offered
+    monkeypatch.setenv("PENNY_PREFILL_GEMM", "force")
+    assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "R"
+    assert gemm.prefill_choice(512, 4096, 4096, None, False) == "hip"
+    monkeypatch.setenv("PENNY_PREFILL_GEMM", "0")
+    assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=True) == "lib"
+
+
+def test_residual_sum_norm_equals_add_then_norm():
+    """GEMM adding the residual in place + plain RMSNorm == GEMM -> add&RMSNorm (CPU reference path)."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(300, 128, generator=g).bfloat16()
+    w = (torch.randn(256, 128, generator=g) * 0.05).bfloat16()
+    nw = torch.rand(256, generator=g).bfloat16() + 0.5
+    r1 = torch.randn(300, 256, generator=g).bfloat16()
+    r2 = r1.clone()
+    y = gemm.prefill_gemm(x, w)
+    h_ref = ops.rms_norm(y, nw, 1e-5, residual=r1)                 # r1 <- y + r1
+    rs = gemm.ResidualSum(gemm.prefill_gemm(x, w, "residual", residual=r2, out=r2))
+    h = ops.rms_norm(rs, nw, 1e-5, residual=r2)
+    assert rs.t is r2
+    assert torch.allclose(r2.float(), r1.float(), atol=2e-2)
+    assert torch.allclose(h.float(), h_ref.float(), atol=3e-2)
