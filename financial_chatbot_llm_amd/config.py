@@ -111,6 +111,12 @@ class EngineConfig:
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
+    # context parallelism (SURVEY §5.7 stretch): cp_size ranks, each with the full weights, form one
+    # replica; its leader serves, and a prompt with >= cp_min_tokens uncomputed tokens is prefilled
+    # by all of them at once (zig-zag shards, ring attention over xGMI), its K/V gathered into the
+    # leader's paged pool (engine/context_prefill.py)
+    cp_size: int = 1
+    cp_min_tokens: int = 16384
     kv_block_size: int = 64                 # tokens per KV block (one MFMA KV tile)
     # of (free HBM after weights - 6 GiB); 0.92 leaves ~20 GiB of the 288 GiB unused at the end of
     # the 20/5 bench (engine stats hbm_used_gib: 8B 264.5, Mixtral fp8 267.9; 0.95 measured no
@@ -146,6 +152,8 @@ class EngineConfig:
             weights=os.getenv("PENNY_WEIGHTS") or None,
             tokenizer=os.getenv("PENNY_TOKENIZER") or None,
             tp_size=_env_int("PENNY_TP", cls.tp_size),
+            cp_size=_env_int("PENNY_CP", cls.cp_size),
+            cp_min_tokens=_env_int("PENNY_CP_MIN_TOKENS", cls.cp_min_tokens),
             kv_block_size=_env_int("PENNY_KV_BLOCK", cls.kv_block_size),
             kv_mem_fraction=_env_float("PENNY_KV_FRACTION", cls.kv_mem_fraction),
             max_num_seqs=_env_int("PENNY_MAX_SEQS", cls.max_num_seqs),

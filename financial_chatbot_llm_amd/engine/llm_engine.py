@@ -92,6 +92,11 @@ class LLMEngine:
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
         self.profiler = StepProfiler(rank=self.ps.rank)
+        # context parallelism: long prompts prefilled by the whole CP replica (engine/context_prefill.py)
+        self.cp = None
+        if getattr(cfg, "cp_size", 1) > 1 and self.ps.cp_size > 1:
+            from .context_prefill import ContextParallelPrefill
+            self.cp = ContextParallelPrefill(self)
         logger.info(f"engine ready: model={self.model.cfg.name} tp={self.model.tp_size} kv_blocks={nblocks} "
                     f"({nblocks * KV_BS} tokens) weights={self.model.num_bytes() / 2**30:.1f} GiB "
                     f"init={time.perf_counter() - t0:.1f}s")
@@ -103,7 +108,10 @@ class LLMEngine:
         max_prompt = self.cfg.max_model_len - 1
         seq = Sequence(request_id, list(prompt_ids)[-max_prompt:], params)
         self.requests[request_id] = seq
-        self.scheduler.add(seq)
+        if self.cp is not None and self.cp.wants(seq):
+            self.cp.queue.append(seq)          # prefilled context-parallel before the next step
+        else:
+            self.scheduler.add(seq)
         return seq
 
     def abort(self, request_id: str) -> None:
@@ -113,7 +121,7 @@ class LLMEngine:
             seq.finish_reason = "abort"
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work() or self._inflight is not None
+        return self.scheduler.has_work() or self._inflight is not None or bool(self.cp and self.cp.queue)
 
     def warmup(self) -> None:
         """Capture decode graphs (all TP ranks must call this together)."""
@@ -125,6 +133,9 @@ class LLMEngine:
         while step N is still on the GPU, then collect N -- the host's scheduling, input packing
         and token bookkeeping hide behind the device instead of idling it between steps."""
         self.profiler.on_step()
+        if self.cp is not None and self.cp.queue:
+            with marker("engine.cp_prefill"):
+                self.cp.run_pending()
         with marker("engine.step"):
             return self._step_overlap() if self.async_scheduling else self._step_sync()
 
@@ -487,6 +498,14 @@ class LLMEngine:
     def stop_followers(self) -> None:
         if self.ps.tp_size > 1 and self.ps.is_tp_leader:
             comm.broadcast_step(None)
+        if self.cp is not None:
+            self.cp.stop()
+
+    def cp_follower_loop(self) -> None:
+        """Context-parallel follower ranks: join the leader's long-prompt prefills until it stops."""
+        if self.cp is None:
+            raise RuntimeError("cp_follower_loop needs cp_size > 1 and init_cp_groups")
+        self.cp.follower_loop()
 
     # -- convenience --------------------------------------------------------------------
     def generate(self, prompts: Seq[Seq[int]], params: SamplingParams) -> List[List[int]]:
@@ -508,6 +527,7 @@ class LLMEngine:
                 "cascade_steps": self.runner.stats["cascade_steps"],
                 "cascade_rows": self.runner.stats["cascade_rows"],
                 "prefill_steps": self.runner.stats["prefill_steps"],
+                **(self.cp.stats if self.cp is not None else {}),
                 "prefill_step_tokens_mean": round(self.runner.stats["prefill_step_tokens"]
                                                   / max(1, self.runner.stats["prefill_steps"]), 1),
                 # device time per step (PENNY_STEP_GPU_TIMING=1): compare with step_p50_ms (host cadence)

@@ -31,6 +31,10 @@ class ParallelState:
     dp_group: Optional[object] = None
     tp_cpu_group: Optional[object] = None   # gloo twin of tp_group: host control messages (C4)
     backend: str = "none"
+    cp_size: int = 1                        # context-parallel replica (init_cp_groups)
+    cp_rank: int = 0
+    cp_group: Optional[object] = None
+    cp_cpu_group: Optional[object] = None
 
     @property
     def is_tp_leader(self) -> bool:
@@ -92,6 +96,28 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None, device_typ
             if rank in ranks:
                 s.dp_group = g
     set_state(s)
+    return s
+
+
+def init_cp_groups(cp_size: int) -> ParallelState:
+    """Context-parallel replicas (TP = 1): consecutive ranks [g*cp, (g+1)*cp) form replica g, whose
+    rank g*cp leads.  cp_group carries the ring attention's K/V hops and the K/V gather (RCCL on
+    the GPU), cp_cpu_group (gloo) the leader's prefill commands."""
+    s = _STATE
+    if cp_size <= 1:
+        return s
+    if s.tp_size != 1:
+        raise ValueError("context parallelism runs with tp_size 1 (every CP rank holds the full weights)")
+    if s.world_size % cp_size:
+        raise ValueError(f"world size {s.world_size} not divisible by cp {cp_size}")
+    for gi in range(s.world_size // cp_size):
+        ranks = list(range(gi * cp_size, (gi + 1) * cp_size))
+        g = dist.new_group(ranks)
+        gc = g if s.backend == "gloo" else dist.new_group(ranks, backend="gloo")
+        if s.rank in ranks:
+            s.cp_group, s.cp_cpu_group = g, gc
+    s.cp_size, s.cp_rank = cp_size, s.rank % cp_size
+    s.dp_size, s.dp_rank = s.world_size // cp_size, s.rank // cp_size
     return s
 
 

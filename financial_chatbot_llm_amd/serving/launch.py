@@ -31,6 +31,9 @@ logger = get_logger(__name__)
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, default=int(os.environ.get("PENNY_TP", "1")))
+    ap.add_argument("--cp", type=int, default=int(os.environ.get("PENNY_CP", "1")),
+                    help="context-parallel replicas of cp ranks (full weights each): the leader serves, "
+                         "prompts >= PENNY_CP_MIN_TOKENS are prefilled by the whole replica")
     ap.add_argument("--model", default=os.environ.get("PENNY_MODEL", "llama3-8b"))
     ap.add_argument("--embed-model", default=os.environ.get("PENNY_EMBED_MODEL", "bge-base-en"))
     ap.add_argument("--corpus", type=int, default=int(os.environ.get("PENNY_CORPUS_SIZE", "0")))
@@ -107,14 +110,23 @@ def main(argv=None) -> int:
 
     from ..engine.async_engine import AsyncEngine
     from ..engine.llm_engine import LLMEngine
-    from ..parallel.dist import init_distributed, shutdown
+    from ..parallel.dist import init_cp_groups, init_distributed, shutdown
 
     ps = init_distributed(tp_size=args.tp)
+    if args.cp > 1:
+        ps = init_cp_groups(args.cp)
     dev_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
     device = torch.device(dev_type, torch.cuda.current_device()) if dev_type == "cuda" else torch.device("cpu")
+    cp_follower = ps.cp_size > 1 and ps.cp_rank != 0
     ecfg = config.EngineConfig.from_env(model=args.model, tp_size=args.tp, max_model_len=args.max_model_len,
-                                        device=dev_type, use_cuda_graph=dev_type == "cuda")
+                                        device=dev_type, use_cuda_graph=dev_type == "cuda", cp_size=args.cp,
+                                        # a CP follower never decodes: a token KV pool, no graphs
+                                        **({"num_kv_blocks": 16} if cp_follower else {}))
     engine = LLMEngine(ecfg)
+    if cp_follower:
+        engine.cp_follower_loop()
+        shutdown()
+        return 0
     engine.warmup()   # every TP rank captures the same decode graphs (collectives inside)
     if not ps.is_tp_leader:
         engine.follower_loop()
