@@ -855,6 +855,10 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
         fns["qkv_lib"] = lambda: rope_kv_write(torch.nn.functional.linear(x, w["qkv"]), pos, cs, slots, kc, vc,
                                                Hq, Hkv, 128)
         fns["qkv_fused"] = lambda: gemm.prefill_qkv_rope(x, w["qkv"], pos, cs, slots, kc, vc, Hq, Hkv)
+        for S in (2, 4):   # split-K slabs summed by the RoPE / KV-write pass
+            Pq = torch.empty((S, M, 6144), dtype=torch.float32, device=dev)
+            fns[f"qkv_hipS{S}"] = (lambda S=S, Pq=Pq: rope_kv_write(gemm.Slabs(gemm.prefill_gemm(
+                x, w["qkv"], "slabs", S, out=Pq)), pos, cs, slots, kc, vc, Hq, Hkv, 128))
         for name, a in (("o", x), ("down", xf)):
             K = a.shape[1]
             fns[f"{name}_lib"] = (lambda a=a, name=name: ops.rms_norm(torch.nn.functional.linear(a, w[name]), nw,
@@ -1023,7 +1027,8 @@ def main(argv=None) -> int:
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query, "gemm_tail": bench_gemm_tail,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
-                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]), "gemm_ablate": bench_gemm_ablate,
+                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]),
+                "prefill_policy_small": lambda d: bench_prefill_policy(d, [512, 768, 1024, 1280, 1536]), "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
