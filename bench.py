@@ -113,7 +113,9 @@ async def run(args, ps):
                         kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
                         sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)),
                         step_time_target_ms=float(os.environ.get("PENNY_STEP_TIME_TARGET_MS",
-                                                                 EngineConfig.step_time_target_ms)))
+                                                                 EngineConfig.step_time_target_ms)),
+                        sched_burst_tokens=int(os.environ.get("PENNY_BURST_TOKENS", EngineConfig.sched_burst_tokens)),
+                        sched_burst_age_s=float(os.environ.get("PENNY_BURST_AGE_S", EngineConfig.sched_burst_age_s)))
     if args.tp > 1 and not ps.is_tp_leader:
         # TP follower: the same engine shard, warmed up (graph capture) in lockstep with its leader,
         # then replays every step the leader broadcasts until the leader's engine shuts down

@@ -133,6 +133,10 @@ class EngineConfig:
     # 0 = off).  Cost model: base + per decode row + per prefill token (engine/scheduler.py)
     step_time_target_ms: float = 0.0
     step_cost_ms: tuple = (3.0, 0.07, 0.013)
+    # burst drain: steps take up to this many prefill tokens while the oldest pending prefill's turn
+    # has waited >= sched_burst_age_s (0 = off)
+    sched_burst_tokens: int = 0
+    sched_burst_age_s: float = 0.5
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
     # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
@@ -162,6 +166,8 @@ class EngineConfig:
             step_token_quantum=_env_int("PENNY_STEP_TOKEN_QUANTUM", cls.step_token_quantum),
             sched_aging_s=_env_float("PENNY_SCHED_AGING_S", cls.sched_aging_s),
             step_time_target_ms=_env_float("PENNY_STEP_TIME_TARGET_MS", cls.step_time_target_ms),
+            sched_burst_tokens=_env_int("PENNY_BURST_TOKENS", cls.sched_burst_tokens),
+            sched_burst_age_s=_env_float("PENNY_BURST_AGE_S", cls.sched_burst_age_s),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),

@@ -76,7 +76,9 @@ class LLMEngine:
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
                                    token_quantum=cfg.step_token_quantum if device.type == "cuda" else 0,
                                    aging_s=cfg.sched_aging_s,
-                                   cost_model=StepCostModel(cfg.step_time_target_ms, base, per_row, per_tok))
+                                   cost_model=StepCostModel(cfg.step_time_target_ms, base, per_row, per_tok),
+                                   burst_tokens=getattr(cfg, "sched_burst_tokens", 0),
+                                   burst_age_s=getattr(cfg, "sched_burst_age_s", 0.5))
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)
@@ -520,6 +522,7 @@ class LLMEngine:
                 "kv_blocks": self.bm.num_blocks, "kv_evictions": int(getattr(self.bm, "evictions", 0)),
                 "preemptions": self.scheduler.num_preemptions,
                 "time_capped_steps": self.scheduler.num_capped_steps,
+                "burst_steps": self.scheduler.num_burst_steps,
                 "spec_draft_tokens": self.spec_stats["proposed"], "spec_accepted_tokens": self.spec_stats["accepted"],
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},

@@ -73,7 +73,7 @@ class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
                  aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
-                 cost_model: "StepCostModel" = None):
+                 cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -87,6 +87,11 @@ class Scheduler:
         self.token_quantum = token_quantum
         self.cost = cost_model if cost_model is not None else StepCostModel()
         self.num_capped_steps = 0
+        # burst drain (TTFT tail): when the oldest pending prefill's turn has waited burst_age_s, the
+        # step takes up to burst_tokens prefill tokens instead of max_num_batched_tokens (0 = off)
+        self.burst_tokens = burst_tokens
+        self.burst_age_s = burst_age_s
+        self.num_burst_steps = 0
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
@@ -127,9 +132,22 @@ class Scheduler:
         self.waiting.appendleft(seq)
         batch.preempted.append(seq)
 
+    def _burst(self) -> bool:
+        if self.burst_tokens <= self.max_num_batched_tokens:
+            return False
+        now = self.clock()
+        oldest = min((s.priority_time for s in self.waiting), default=None)
+        cont = [s.priority_time for s in self.running if s.remaining_prefill > 1 and not s.spec_rows]
+        if cont:
+            oldest = min(cont) if oldest is None else min(oldest, min(cont))
+        return oldest is not None and now - oldest >= self.burst_age_s
+
     def schedule(self) -> ScheduledBatch:
         batch = ScheduledBatch()
         budget = self.max_num_batched_tokens
+        if self._burst():
+            budget = self.burst_tokens
+            self.num_burst_steps += 1
         # 1) decodes (oldest first); preempt youngest when blocks run out
         decodes = [s for s in self.running if s.remaining_prefill == 1 and not s.awaiting]
         for seq in sorted(decodes, key=lambda s: s.arrival):
