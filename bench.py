@@ -216,20 +216,22 @@ async def run(args, ps):
 
 
 def _share_host_cpus() -> None:
-    """One process per GPU on a shared host: give each local rank an equal share of the CPUs for
-    its intra-op thread pools (torch / OpenMP default to every core, so 8 ranks would each start
-    one thread per core).  PENNY_PIN_CPUS=1 also pins each rank to its own contiguous CPU slice."""
+    """One process per GPU on a shared host: without an OMP_NUM_THREADS from the launcher, give each
+    local rank an equal share of the CPUs for its intra-op thread pools (torch / OpenMP default to
+    every core, so 8 ranks would each start one thread per core).  PENNY_PIN_CPUS=1 also pins each
+    rank to its own contiguous CPU slice."""
     lws = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
     if lws <= 1:
         return
     lr = int(os.environ.get("LOCAL_RANK", "0"))
     cpus = sorted(os.sched_getaffinity(0))
     per = max(1, len(cpus) // lws)
-    os.environ.setdefault("OMP_NUM_THREADS", str(min(per, 16)))
     if os.environ.get("PENNY_PIN_CPUS") == "1" and per >= 2:
         os.sched_setaffinity(0, cpus[lr * per:(lr + 1) * per])
-    import torch
-    torch.set_num_threads(min(per, 16))
+    if "OMP_NUM_THREADS" not in os.environ:     # torchrun sets it (to 1) unless the caller did
+        os.environ["OMP_NUM_THREADS"] = str(min(per, 16))
+        import torch
+        torch.set_num_threads(min(per, 16))
 
 
 def main(argv=None) -> int:
