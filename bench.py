@@ -167,6 +167,9 @@ async def run(args, ps):
     sync()
     barrier()
     tok0 = {p: dict(v) for p, v in llm.token_stats.items()}
+    for lat in llm.latency.values():      # engine latency anatomy of the timed turns only
+        for v in lat.values():
+            v.clear()
     stats0 = engine.stats()
     prof = None
     if os.environ.get("PENNY_PYPROFILE"):   # host-side cProfile of the serving event loop
@@ -209,9 +212,15 @@ async def run(args, ps):
     tokens["kv_evictions"] = stats.get("kv_evictions", 0) - stats0.get("kv_evictions", 0)
     tokens["preemptions"] = stats.get("preemptions", 0) - stats0.get("preemptions", 0)
     stages = {k: [v for r in results for v in r.stages.get(k, [])] for k in ("decide", "retrieval", "respond_first_token")}
+
+    def pct(v, q):
+        v = sorted(v)
+        return round(1e3 * v[min(len(v) - 1, int(q * len(v)))], 1) if v else None
+    latency = {p: {k: {"p50": pct(v, 0.5), "p99": pct(v, 0.99)} for k, v in lat.items()}
+               for p, lat in llm.latency.items()}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
             "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
-            "stages": stages, "engine": stats, "tokens": tokens,
+            "stages": stages, "engine": stats, "tokens": tokens, "latency": latency,
             "plots_ok": sum(r.plots_ok for r in results), "plots_failed": sum(r.plots_failed for r in results)}
 
 
@@ -293,6 +302,8 @@ def main(argv=None) -> int:
             "ttft_stage_p99_ms": {k: round(1e3 * sorted(v)[min(len(v) - 1, int(0.99 * len(v)))], 1) if v else None
                                   for k, v in allr[0]["stages"].items()},
             "prompt_tokens_rank0": allr[0]["tokens"],
+            # per LLM call, engine side: queued before admission / admission -> first token / total
+            "engine_call_latency_ms_rank0": allr[0]["latency"],
             "engine_rank0": allr[0]["engine"],
         }
         line = json.dumps(out)

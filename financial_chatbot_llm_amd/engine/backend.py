@@ -60,6 +60,9 @@ class EngineLLM(LLMBackend):
         # (prompt - prefix-cache hits + preemption recomputes), generated tokens
         self.token_stats = {p: {"calls": 0, "prompt": 0, "prefilled": 0, "generated": 0}
                             for p in ("decide", "respond")}
+        # engine-side latency anatomy per call (seconds): queued before admission, admission to the
+        # first sampled token, and arrival to the last token
+        self.latency = {p: {"queue": [], "to_first": [], "total": []} for p in ("decide", "respond")}
 
     def _account(self, purpose: str, prompt_len: int, seq) -> None:
         st = self.token_stats.setdefault(purpose, {"calls": 0, "prompt": 0, "prefilled": 0, "generated": 0})
@@ -68,6 +71,13 @@ class EngineLLM(LLMBackend):
         # prefill chunks also cover forced tokens appended after the prompt (jump-forward)
         st["prefilled"] += min(getattr(seq, "num_prefilled", 0), prompt_len)
         st["generated"] += len(seq.output_ids)
+        lat = self.latency.setdefault(purpose, {"queue": [], "to_first": [], "total": []})
+        import time as _t
+        if getattr(seq, "admit_time", None) is not None:
+            lat["queue"].append(seq.admit_time - seq.arrival)
+            if seq.first_token_time is not None:
+                lat["to_first"].append(seq.first_token_time - seq.admit_time)
+        lat["total"].append(_t.perf_counter() - seq.arrival)
 
     def count_tokens(self, text: str) -> int:
         return self.encoder.count(text)

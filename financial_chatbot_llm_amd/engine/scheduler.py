@@ -206,6 +206,8 @@ class Scheduler:
                     raise MemoryError("KV pool too small for a single prompt")
                 break
             self.waiting.popleft()
+            if seq.admit_time is None:
+                seq.admit_time = self.clock()
             seq.status = SeqStatus.RUNNING
             self.running.append(seq)
             batch.prefill.append((seq, seq.num_computed, n))

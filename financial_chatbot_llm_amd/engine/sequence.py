@@ -66,6 +66,7 @@ class Sequence:
         self.num_prefilled = 0         # tokens run through prefill chunks (recomputes included)
         self.arrival = time.perf_counter() if arrival is None else arrival
         self.first_token_time: Optional[float] = None
+        self.admit_time: Optional[float] = None   # first admitted into a step (scheduler clock)
         self.finish_reason: Optional[str] = None
         self.seed = params.seed if params.seed is not None else (hash((request_id, self.seq_id)) & 0x7FFFFFFF)
         self.num_preemptions = 0
