@@ -115,7 +115,8 @@ async def run(args, ps):
                         step_time_target_ms=float(os.environ.get("PENNY_STEP_TIME_TARGET_MS",
                                                                  EngineConfig.step_time_target_ms)),
                         sched_burst_tokens=int(os.environ.get("PENNY_BURST_TOKENS", EngineConfig.sched_burst_tokens)),
-                        sched_burst_age_s=float(os.environ.get("PENNY_BURST_AGE_S", EngineConfig.sched_burst_age_s)))
+                        sched_burst_age_s=float(os.environ.get("PENNY_BURST_AGE_S", EngineConfig.sched_burst_age_s)),
+                        sched_sjf_tokens=int(os.environ.get("PENNY_SJF_TOKENS", EngineConfig.sched_sjf_tokens)))
     if args.tp > 1 and not ps.is_tp_leader:
         # TP follower: the same engine shard, warmed up (graph capture) in lockstep with its leader,
         # then replays every step the leader broadcasts until the leader's engine shuts down
@@ -268,7 +269,7 @@ def main(argv=None) -> int:
         allr = [res]
     if ps.rank == 0:
         tmax = max(r["elapsed"] for r in allr)
-        turns = sum(r["turns"] for r in allr)
+        turns = sum(r["turns"] - r["errors"] for r in allr)    # completed turns: errored ones do not count
         ttfts = sorted(t for r in allr for t in r["ttfts"])
         p50 = statistics.median(ttfts) * 1e3 if ttfts else None
         p99 = ttfts[min(len(ttfts) - 1, int(0.99 * len(ttfts)))] * 1e3 if ttfts else None

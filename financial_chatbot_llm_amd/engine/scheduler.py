@@ -73,7 +73,8 @@ class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
                  aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
-                 cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5):
+                 cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5,
+                 sjf_tokens: int = 0):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -92,6 +93,10 @@ class Scheduler:
         self.burst_tokens = burst_tokens
         self.burst_age_s = burst_age_s
         self.num_burst_steps = 0
+        # short-job-first admission (TTFT tail): a waiting request whose uncached prompt is at most
+        # sjf_tokens is admitted ahead of the continuing chunks of long prefills (0 = off)
+        self.sjf_tokens = sjf_tokens
+        self.num_sjf_admits = 0
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
@@ -179,9 +184,15 @@ class Scheduler:
             if cap < budget:
                 budget = cap
                 self.num_capped_steps += 1
-        # 2) continuing prefills
+        # 2a) short-job-first: short uncached prompts (an agent decide call: ~200 new tokens behind a
+        # cached few-shot prefix) go before the continuing chunks of long prefills
+        if self.sjf_tokens > 0 and self.waiting and budget > 0:
+            budget = self._admit_short(batch, budget)
+        # 2) continuing prefills (not the sequences 2a just admitted: their computed count moves only
+        # when this step resolves)
+        taken = {id(q) for q, _, _ in batch.prefill}
         for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting
-                           and not s.spec_rows), key=lambda s: s.priority_time):
+                           and not s.spec_rows and id(s) not in taken), key=lambda s: s.priority_time):
             if budget <= 0:
                 break
             n = min(seq.remaining_prefill, budget)
@@ -215,6 +226,31 @@ class Scheduler:
             budget -= n
         self._quantise(batch)
         return batch
+
+    def _admit_short(self, batch: ScheduledBatch, budget: int) -> int:
+        now = self.clock()
+        for seq in sorted(self.waiting, key=lambda q: self._priority(q, now)):
+            if budget <= 0 or len(self.running) >= self.max_num_seqs:
+                break
+            if seq.pending_src >= 0 or seq.awaiting or seq.num_preemptions:
+                continue
+            if not seq.block_table:
+                self.bm.match_prefix(seq)
+            n = seq.remaining_prefill
+            if n > self.sjf_tokens or n > budget:
+                continue
+            if not self.bm.grow(seq, seq.num_computed + n):
+                break
+            self.waiting.remove(seq)
+            if seq.admit_time is None:
+                seq.admit_time = now
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+            batch.prefill.append((seq, seq.num_computed, n))
+            seq.num_prefilled += n
+            budget -= n
+            self.num_sjf_admits += 1
+        return budget
 
     def _quantise(self, batch: ScheduledBatch) -> None:
         """Round the step's row count DOWN to a multiple of ``token_quantum`` by shortening its last

@@ -256,3 +256,24 @@ def test_step_time_bound_off_by_default():
     from financial_chatbot_llm_amd.config import EngineConfig
     from financial_chatbot_llm_amd.engine.scheduler import StepCostModel
     assert EngineConfig().step_time_target_ms == 0.0 and StepCostModel().target_ms == 0.0
+
+
+def test_short_job_first_admits_short_prompt_once_ahead_of_long_prefill():
+    """sjf_tokens: a short waiting prompt is admitted ahead of a long prefill's next chunk, and a
+    sequence admitted that way is not scheduled a second time by the continuing-prefill pass."""
+    from financial_chatbot_llm_amd.engine.block_manager import make_block_manager
+    from financial_chatbot_llm_amd.engine.scheduler import Scheduler
+    from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
+    bm = make_block_manager(256, 64, False)
+    sch = Scheduler(bm, max_num_batched_tokens=512, sjf_tokens=128)
+    long = Sequence("long", list(range(2000)), SamplingParams(max_tokens=8))
+    sch.add(long)
+    b1 = sch.schedule()
+    assert [(q.request_id, n) for q, _, n in b1.prefill] == [("long", 512)]
+    long.num_computed = 512
+    short = Sequence("short", list(range(100)), SamplingParams(max_tokens=8))
+    sch.add(short)
+    b2 = sch.schedule()
+    ids = [q.request_id for q, _, _ in b2.prefill]
+    assert ids == ["short", "long"] and len(set(ids)) == len(ids)
+    assert sum(n for _, _, n in b2.prefill) == 512 and sch.num_sjf_admits == 1
