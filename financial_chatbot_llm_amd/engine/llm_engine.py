@@ -79,7 +79,8 @@ class LLMEngine:
                                    cost_model=StepCostModel(cfg.step_time_target_ms, base, per_row, per_tok),
                                    burst_tokens=getattr(cfg, "sched_burst_tokens", 0),
                                    burst_age_s=getattr(cfg, "sched_burst_age_s", 0.5),
-                                   sjf_tokens=getattr(cfg, "sched_sjf_tokens", 0))
+                                   sjf_tokens=getattr(cfg, "sched_sjf_tokens", 0),
+                                   sjf_step_cap=getattr(cfg, "sched_sjf_step_cap", 0))
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)

@@ -74,7 +74,7 @@ class Scheduler:
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
                  aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
                  cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5,
-                 sjf_tokens: int = 0):
+                 sjf_tokens: int = 0, sjf_step_cap: int = 0):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -96,6 +96,7 @@ class Scheduler:
         # short-job-first admission (TTFT tail): a waiting request whose uncached prompt is at most
         # sjf_tokens is admitted ahead of the continuing chunks of long prefills (0 = off)
         self.sjf_tokens = sjf_tokens
+        self.sjf_step_cap = sjf_step_cap      # at most this many tokens of a step go to 2a (0: budget)
         self.num_sjf_admits = 0
 
     def _priority(self, seq: Sequence, now: float):
@@ -229,6 +230,7 @@ class Scheduler:
 
     def _admit_short(self, batch: ScheduledBatch, budget: int) -> int:
         now = self.clock()
+        cap = self.sjf_step_cap if self.sjf_step_cap > 0 else budget
         for seq in sorted(self.waiting, key=lambda q: self._priority(q, now)):
             if budget <= 0 or len(self.running) >= self.max_num_seqs:
                 break
@@ -237,7 +239,7 @@ class Scheduler:
             if not seq.block_table:
                 self.bm.match_prefix(seq)
             n = seq.remaining_prefill
-            if n > self.sjf_tokens or n > budget:
+            if n > self.sjf_tokens or n > budget or n > cap:
                 continue
             if not self.bm.grow(seq, seq.num_computed + n):
                 break
@@ -249,6 +251,7 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
+            cap -= n
             self.num_sjf_admits += 1
         return budget
 
