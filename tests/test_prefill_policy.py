@@ -41,3 +41,30 @@ def test_residual_sum_norm_equals_add_then_norm():
     assert rs.t is r2
     assert torch.allclose(r2.float(), r1.float(), atol=2e-2)
     assert torch.allclose(h.float(), h_ref.float(), atol=3e-2)
+
+
+def test_fused_lm_head_gating(monkeypatch):
+    """The fused LM head + sampler is taken on the device only, from FUSED_LM_HEAD_MIN_M rows, for a
+    vocabulary that tiles by 256 (PENNY_FUSED_LM_HEAD=0 / force override)."""
+    from financial_chatbot_llm_amd.ops import sampling
+    w = torch.zeros(512, 128, dtype=torch.bfloat16)
+    h = torch.zeros(200, 128, dtype=torch.bfloat16)
+    monkeypatch.delenv("PENNY_FUSED_LM_HEAD", raising=False)
+    assert not sampling.fused_lm_head_ok(h, w)                 # CPU tensors: no native kernel
+    monkeypatch.setattr(sampling.N, "use_native", lambda t: True)
+    assert sampling.fused_lm_head_ok(h, w)
+    assert not sampling.fused_lm_head_ok(h[:sampling.FUSED_LM_HEAD_MIN_M - 1], w)
+    assert not sampling.fused_lm_head_ok(h, torch.zeros(500, 128, dtype=torch.bfloat16))   # V % 256
+    monkeypatch.setenv("PENNY_FUSED_LM_HEAD", "force")
+    assert sampling.fused_lm_head_ok(h[:1], w)
+    monkeypatch.setenv("PENNY_FUSED_LM_HEAD", "0")
+    assert not sampling.fused_lm_head_ok(h, w)
+
+
+def test_context_parallel_prefix_length():
+    """CP prefills all but the prompt's last token, rounded down to whole zig-zag chunk pairs."""
+    from financial_chatbot_llm_amd.engine.context_prefill import cp_prefix_len
+    assert cp_prefix_len(301, 2) == 300
+    assert cp_prefix_len(300, 2) == 296
+    assert cp_prefix_len(100_001, 8) == 100_000
+    assert cp_prefix_len(5, 4) == 0
