@@ -249,6 +249,23 @@ class LLMEngine:
                 if t in stops:
                     draft = draft[:i]
                     break
+        if draft and p.grammar is not None and p.forced_output is None:
+            draft = self._grammar_cut(seq, list(after), draft)
+        return draft
+
+    def _grammar_cut(self, seq: Sequence, after: List[int], draft: List[int]) -> List[int]:
+        """Longest draft prefix d[:k] such that the output grammar forces nothing after any of
+        d[:1] .. d[:k]: one-token-per-step decoding would jump forward (override the sample) at
+        the first such position, so the chunk's samples there -- an accepted draft token's
+        successor or the bonus -- are not what it would emit.  With the cut, every sampled
+        position of the chunk is one where the grammar is free, and ``_stage_grammar`` after the
+        bonus resumes exactly as without speculation."""
+        g = seq.params.grammar
+        base = [t for t in seq.output_ids if t != PENDING] + after
+        for k in range(len(draft)):
+            forced, ends = g.forced(self.tokenizer.decode(base + draft[:k + 1]))
+            if forced or ends:
+                return draft[:k]
         return draft
 
     def _model_tokens(self, seq: Sequence, base: int, toks: Seq[int], m: int) -> List[int]:
@@ -301,9 +318,11 @@ class LLMEngine:
             if seq.finished:
                 continue
             if seq.spec_rows > 1:              # sampled draft in flight: verified on resolve
+                # no commit here: num_computed counts the unverified draft, and a full block
+                # holding draft positions must not enter the prefix cache under the draft's token
+                # ids (a rejection rewrites that KV); _resolve commits after _verify
                 seq.awaiting = True
                 seq.jump_tail = []
-                self.bm.commit(seq)
                 continue
             run = self._known_run(seq)
             tok = run[-1] if run else None
@@ -362,6 +381,7 @@ class LLMEngine:
                 sat_out = True
                 if seq.spec_rows > 1:          # sampled draft: keep the accepted prefix + bonus
                     acc, bonus = self._verify(seq, toks)
+                    self.bm.commit(seq)        # verified positions only (num_computed clamped)
                     seq.output_ids.append(bonus)
                     new = acc + [bonus]
                     was_sampled = True

@@ -174,7 +174,11 @@ class Scheduler:
         for seq in sorted((s for s in self.running if s.spec_rows and not s.awaiting
                            and s.remaining_prefill >= s.spec_rows), key=lambda s: s.arrival):
             n = seq.remaining_prefill
-            if not self.bm.grow(seq, seq.num_tokens):
+            if n > max(budget, 0) or not self.bm.grow(seq, seq.num_tokens):
+                # no room for the chunk: forget the draft, so the sequence is an ordinary row
+                # again (a 1-token decode, or the rest of a forced run) and next step's decode
+                # pass -- which preempts when the pool is dry -- schedules it
+                seq.drop_draft()
                 continue
             batch.prefill.append((seq, seq.num_computed, n))
             budget -= n

@@ -143,6 +143,25 @@ def test_scheduler_chunked_prefill_and_preemption():
     assert bm.num_free() >= 0
 
 
+def test_scheduler_drops_a_draft_it_cannot_grow():
+    """A speculative chunk whose blocks do not fit gives up its draft: the sequence
+    is an ordinary decode row again and the next step's decode pass (which preempts when the pool
+    is dry) schedules it -- steps never come out empty with has_work() true."""
+    bm = PyBlockManager(2, BS, True)
+    sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=256, max_model_len=1024)
+    a = mk(list(range(BS * 2 - 1)), "a")
+    sch.add(a)
+    batch = sch.schedule()
+    a.num_computed = BS * 2 - 1
+    a.output_ids.append(5)                     # the sampled token: KV not computed yet
+    a.output_ids.extend([6, 7, 8])             # a draft that needs a third block
+    a.spec_rows = 4
+    batch = sch.schedule()
+    assert batch.empty() and a.spec_rows == 0 and a.output_ids == [5]
+    batch = sch.schedule()
+    assert batch.decode == [a]
+
+
 def _mk_params(prompt, rid, max_tokens, arrival):
     from financial_chatbot_llm_amd.engine.sequence import SamplingParams, Sequence
     return Sequence(rid, prompt, SamplingParams(max_tokens=max_tokens), arrival=arrival)

@@ -90,6 +90,77 @@ def test_sampled_outputs_identical_with_speculation(mode, temperature):
         assert eb.spec_stats["accepted"] > 0            # greedy loops get copied
 
 
+class _EveryFifthChar:
+    """Output grammar stub that forces " the" whenever the output text's length is a multiple of
+    5: jump-forward fires often on a random model's text, inside drafted spans too."""
+    def __init__(self):
+        self.forcing = 0
+
+    def forced(self, text):
+        if text and len(text) % 5 == 0:
+            self.forcing += 1
+            return " the", False
+        return "", False
+
+
+@pytest.mark.parametrize("mode", [True, False])
+@pytest.mark.parametrize("temperature", [0.0, 0.8])
+def test_sampled_outputs_identical_with_speculation_under_grammar(mode, temperature):
+    """Jump-forward inside a draft: the draft is cut before the first position where the grammar
+    forces, so speculation emits exactly the one-token-per-step output."""
+    prompts = [[400 + (i * 13) % 50 for i in range(60)] + [900 + i for i in range(20)],
+               [700 + (i * 7) % 30 for i in range(90)]]
+
+    def run(lookup):
+        g = _EveryFifthChar()
+        ps = [SamplingParams(temperature=temperature, max_tokens=40, ignore_eos=True, seed=5 + i, grammar=g,
+                             prompt_lookup=lookup) for i in range(len(prompts))]
+        seqs, eng = _run(ps, prompts, mode)
+        return [s.output_ids for s in seqs], eng, g
+    a, _, ga = run(0)
+    b, eb, gb = run(8)
+    assert a == b
+    assert ga.forcing > 0 and gb.forcing > 0
+
+
+def test_rejected_sampled_draft_never_enters_prefix_cache():
+    """A sampled draft crossing a 64-token block boundary is rejected: the block holding draft
+    positions must not be registered under the draft's token ids, since the bonus token then
+    rewrites that KV.  A second request whose prompt carries the rejected draft must
+    miss the prefix cache and compute what the uncached engine computes."""
+    from financial_chatbot_llm_amd.ops.attention import KV_BS
+    prompt = [500 + (i * 3) % 40 for i in range(KV_BS - 3)]
+    bad = [7, 8, 9, 10, 11, 12]      # positions 63..68: d0 lands in block 0, the rest in block 1
+
+    def engine(caching):
+        return LLMEngine(EngineConfig(async_scheduling=True, seed=0, **{**BASE, "enable_prefix_caching": caching}))
+
+    eng = engine(True)
+    used = {"n": 0}
+
+    def propose(seq, after=(), min_ngram=0):     # inject the draft once, after output token 2
+        k = len(seq.output_ids) + len(after)
+        if used["n"] == 0 and k in (1, 2):
+            used["n"] = k == 2
+            return list(bad)
+        return []
+    eng._propose = propose
+    seq = eng.add_request("a", prompt, SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True, prompt_lookup=8))
+    while eng.has_work():
+        eng.step()
+    assert used["n"] and eng.spec_stats["proposed"] == len(bad)
+    assert seq.output_ids[2] != bad[0]            # rejected at its first token (bonus differs)
+    p2 = prompt + seq.output_ids[:2] + bad + [42, 43, 44]
+    outs = []
+    for e in (eng, engine(False)):
+        s = e.add_request("b", p2, SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
+        while e.has_work():
+            e.step()
+        outs.append((s.num_cached_prompt, s.output_ids))
+    assert outs[0][0] == 0, "block 0 was cached under the rejected draft"
+    assert outs[0][1] == outs[1][1]
+
+
 def test_draft_respects_max_tokens_and_stops():
     eng = LLMEngine(EngineConfig(async_scheduling=False, seed=0, **BASE))
     seq = eng.add_request("r", [9, 1, 2, 3, EOT, 7, 4, 5, 6, 7, 8, 9, 10], SamplingParams(max_tokens=6, prompt_lookup=8))
