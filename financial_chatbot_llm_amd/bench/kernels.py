@@ -262,14 +262,26 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         o = torch.empty_like(q)
         wl = ops.attention.prefill_work_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv)
         wd = torch.from_numpy(wl).to(dev) if wl is not None else None
-        ts = interleaved({"grid": lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o),
-                          "lpt": lambda: ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
-                                                     work=wd)}, rounds=7, iters=5)
+        def run(v):
+            def f():
+                ops.attention.prefill_variant(v)
+                ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
+            return f
+        variants = {"pf2": 0, "pp": 1, "pp_valu": 2, "pp_prio": 3}
+        old = ops.attention.prefill_variant()
+        outs = {}
+        for k, v in variants.items():
+            run(v)()
+            outs[k] = o.clone()
+        ts = interleaved({k: run(v) for k, v in variants.items()}, rounds=7, iters=5)
+        ops.attention.prefill_variant(old)
         keys = sum(ql * (c - ql) + ql * (ql + 1) / 2 for ql, c in shape)
         flops = 4 * keys * Hq * D
-        row = {"op": "prefill_attn_mixed", "step": name, "T": T, "us": round(ts["lpt"], 1),
-               "TFLOPs": round(flops / ts["lpt"] / 1e6, 1), "grid_us": round(ts["grid"], 1),
-               "grid_TFLOPs": round(flops / ts["grid"] / 1e6, 1)}
+        row = {"op": "prefill_attn_mixed", "step": name, "T": T}
+        for k in variants:
+            row[f"{k}_us"] = round(ts[k], 1)
+            row[f"{k}_TFLOPs"] = round(flops / ts[k] / 1e6, 1)
+            row[f"{k}_maxdiff_vs_pf2"] = round(float((outs[k].float() - outs["pf2"].float()).abs().max()), 5)
         print(json.dumps(row), flush=True)
         out.append(row)
     return out

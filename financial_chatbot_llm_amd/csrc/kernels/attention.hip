@@ -949,6 +949,285 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Ping-pong prefill (prefill3_kernel): the 8-wave tile of prefill2 with its two SIMD partners
+// half a block apart.
+// ------------------------------------------------------------------------------------------
+// In prefill2 every wave runs {QK^T MFMAs, softmax VALU, P.V MFMAs} per block between the same
+// two barriers, so the two waves sharing a SIMD (w and w + 4) reach their softmax together and
+// the matrix pipe idles through it (about half of every block: ~1.0 PF/s).  Here a block is two
+// barrier-separated halves and the waves 4-7 (group B) run one half behind waves 0-3 (group A):
+//   half 1 of block i: A = QKS(i) (K frags, 32 MFMAs, softmax) | B = PV(i-1) (32 MFMAs)
+//   half 2 of block i: A = PV(i)                               | B = QKS(i)
+// so on every SIMD one wave's softmax runs beside its partner's P.V MFMAs.  Both groups execute
+// the same barrier sequence (2 per block + 1), so the LDS protocol is written in barrier indices:
+// block i is published by barrier 2i (each wave's counted vmcnt for its own pieces before it).
+// The last reader of block i's buffer is B's PV(i) (between barriers 2i+2 and 2i+3; an
+// lgkmcnt(0) precedes every barrier), and block i+3 refills it after barrier 2i+3.  VPRE: V(i)
+// is read into registers inside QKS(i) instead (its LDS latency under the softmax; costs 64
+// VGPRs across the softmax -- spills at D = 128).
+// LSUM: the softmax row sums come from 4 extra MFMAs against an all-ones A fragment (the P.V
+// product with a V column of ones) instead of 32 VALU adds per lane and block.
+template <int D, bool LSUM, bool VPRE>
+__device__ __forceinline__ void pp_qks(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
+                                       const Frag (&qf)[2][D / 32], Frag (&vf)[D / 8], f32x4 (&o)[2][D / 16],
+                                       float (&m)[2], float (&l)[2], f32x4 (&lacc)[2], Frag (&pf)[2][2], bool causal,
+                                       int j, int ctx, const int (&qpos)[2], float scale_log2, int lane, int g,
+                                       bool need_mask) {
+  constexpr int KC = D / 32, DT = D / 16;
+  f32x4 sc[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    Frag kf[KC];          // one 16-key row group at a time: 16 VGPRs, not 64
+#pragma unroll
+    for (int c = 0; c < KC; ++c) kf[c].u = kl[(t * KC + c) * 64 + lane];
+    sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      sc[0][t] = mfma16(kf[c].v, qf[0][c].v, sc[0][t]);
+      sc[1][t] = mfma16(kf[c].v, qf[1][c].v, sc[1][t]);
+    }
+  }
+  // V fragments for PV: in flight during the softmax (read after the K fragments are consumed, so
+  // the two sets are never live together -- the scheduling barrier keeps hipcc from hoisting them)
+  if constexpr (VPRE) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 2 * DT; ++f) vf[f].u = vl[f * 64 + lane];
+  }
+  if (need_mask) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = j * KV_BS + 16 * t + 4 * g + r;
+          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));
+          sc[ct][t][r] = ok ? sc[ct][t][r] : -INFINITY;
+        }
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[ct][t][r]);
+    mt = rowgroup_max(mt) * scale_log2;
+    const bool grow = mt > m[ct] + 8.f;      // deferred rescale, as attend_block
+    if (__any(grow)) {
+      const float mn = grow ? mt : m[ct];
+      const float alpha = grow ? fast_exp2(m[ct] - mn) : 1.f;
+      if constexpr (LSUM) lacc[ct] *= alpha;
+      else l[ct] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+      m[ct] = mn;
+    }
+    const float mref = (m[ct] == -INFINITY) ? 0.f : m[ct];
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = fast_exp2(fmaf(sc[ct][t][r], scale_log2, -mref));
+        sc[ct][t][r] = p;
+        if constexpr (!LSUM) ls += p;
+      }
+    if constexpr (!LSUM) l[ct] += ls;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
+        pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
+      }
+  }
+}
+
+template <int D, bool LSUM, bool VPRE>
+__device__ __forceinline__ void pp_pv(const uint4* __restrict__ vl, Frag (&vf)[D / 8], f32x4 (&o)[2][D / 16],
+                                      f32x4 (&lacc)[2], const Frag (&pf)[2][2], int lane) {
+  constexpr int DT = D / 16;
+  if constexpr (!VPRE) {
+#pragma unroll
+    for (int f = 0; f < 2 * DT; ++f) vf[f].u = vl[f * 64 + lane];
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      o[0][dt] = mfma16(vf[dt * 2 + st].v, pf[0][st].v, o[0][dt]);
+      o[1][dt] = mfma16(vf[dt * 2 + st].v, pf[1][st].v, o[1][dt]);
+    }
+  if constexpr (LSUM) {
+    Frag ones;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones.v[i] = (bf16)1.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      lacc[0] = mfma16(ones.v, pf[0][st].v, lacc[0]);
+      lacc[1] = mfma16(ones.v, pf[1][st].v, lacc[1]);
+    }
+  }
+}
+
+__device__ __forceinline__ void lgkm0_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int D, bool HEAD_FAST, bool LSUM, bool PRIO, bool VPRE = false>
+__global__ void __launch_bounds__(512, 1) prefill3_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
+    float* __restrict__ lse, const int* __restrict__ work) {
+  constexpr int NW = 8, NBUF = 3;
+  constexpr int KC = D / 32, DT = D / 16;
+  constexpr int TILE = KV_BS * D * 2;
+  constexpr int PIECES = TILE / 1024 / NW;
+  constexpr int LOADS = 2 * PIECES;
+  static_assert(PIECES >= 1 && TILE % (1024 * NW) == 0, "tile must split evenly over the waves");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
+
+  const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
+  const int s = work ? work[2 * item] : blockIdx.z;
+  const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
+  const int tile = work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item;
+  const int G = Hq / Hkv;
+  const int TQ = NW * 32 / G;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  const int tok0 = tile * TQ;
+  if (tok0 >= qlen) return;
+  const int ctx = ctx_lens[s];
+  const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool grpB = w >= 4;                   // SIMD partners: waves w and w + 4
+  if (PRIO && grpB) __builtin_amdgcn_s_setprio(1);   // the younger half wins VALU arbitration
+
+  const int last_tok = min(tok0 + TQ, qlen) - 1;
+  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
+  const int nblk = (kv_end + KV_BS - 1) / KV_BS;
+  const int* bt = block_tables + (long)s * max_blocks;
+
+  auto stage = [&](int j) {
+    const long phys = bt[j];
+    PENNY_DASSERT(phys >= 0);
+    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
+    char* kl = smem + (j % NBUF) * 2 * TILE;
+    char* vl = kl + TILE;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int piece = w * PIECES + i;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kl + piece * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vl + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+  stage(0);
+  if (nblk > 1) stage(1);
+
+  int tok[2], head[2], qpos[2];
+  Frag qf[2][KC];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int r = w * 32 + ct * 16 + col;
+    tok[ct] = tok0 + r / G;
+    head[ct] = h * G + r % G;
+    const bool valid = tok[ct] < qlen;
+    qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
+    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): Q and the prologue blocks (visible wait)
+
+  f32x4 o[2][DT], lacc[2];
+  float m[2], l[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    m[ct] = -INFINITY;
+    l[ct] = 0.f;
+    lacc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  Frag vf[2 * DT], pf[2][2];
+
+  const int wave_tok0 = tok0 + (w * 32) / G;
+  const bool wave_live = wave_tok0 < qlen;
+  const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
+  const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
+  auto act = [&](int j) { return wave_live && j * KV_BS < wave_kv_end; };
+  auto qks = [&](int j) {
+    const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
+    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
+    pp_qks<D, LSUM, VPRE>(kl, kl + TILE / 16, qf, vf, o, m, l, lacc, pf, causal, j, ctx, qpos, scale_log2, lane, g,
+                          __builtin_amdgcn_readfirstlane((int)!full) != 0);
+  };
+
+  // One op per barrier, the same op sequence QKS(0), PV(0), QKS(1), ... on every wave; group B
+  // passes barrier 0 before its first op (one half behind) and group A one extra barrier at the
+  // end, so both execute barriers 0 .. 2*nblk.  b = the barrier this wave passes before op k.
+  const int boff = grpB ? 1 : 0;
+  if (grpB) lgkm0_bar();                     // barrier 0 (the prologue already waited vmcnt(0))
+  for (int k = 0; k < 2 * nblk; ++k) {
+    const int b = k + boff;
+    if ((b & 1) == 0) {                      // barrier b publishes block b/2
+      if ((b >> 1) + 1 < nblk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lgkm0_bar();
+    if ((b & 1) && (b >> 1) + 2 < nblk) stage((b >> 1) + 2);   // the buffer block b/2 - 1 used
+    const int j = k >> 1;
+    if (act(j)) {
+      if ((k & 1) == 0) qks(j);
+      else pp_pv<D, LSUM, VPRE>(reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE), vf, o, lacc, pf,
+                                lane);
+    }
+  }
+  if (!grpB) lgkm0_bar();                    // barrier 2*nblk
+
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float lt;
+    if constexpr (LSUM) lt = lacc[ct][0];     // every output row of the ones-MFMA holds the full sum
+    else lt = rowgroup_sum(l[ct]);
+    if (tok[ct] >= qlen) continue;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x4 v4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
+    }
+    if (lse != nullptr && g == 0)
+      lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
+  }
+}
+
+// Big-tile prefill variant: 1 (default) ping-pong prefill3 with ones-MFMA row sums, 2 ping-pong
+// with VALU row sums, 3 = 1 + static priority for waves 4-7, 0 prefill2 (PENNY_PREFILL_PP, or
+// penny_attention_prefill_variant for in-process A/B runs)
+static int g_prefill_variant = -1;
+static int prefill_variant() {
+  if (g_prefill_variant < 0) {
+    const char* v = getenv("PENNY_PREFILL_PP");
+    g_prefill_variant = v ? atoi(v) : 0;
+  }
+  return g_prefill_variant;
+}
+PENNY_API int penny_attention_prefill_variant(int v) {
+  const int old = prefill_variant();
+  if (v >= 0) g_prefill_variant = v;
+  return old;
+}
+
 PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                       const void* k_cache, const void* v_cache, void* out, int num_seqs,
                                       int max_q_len, int Hq, int Hkv, int D, int max_blocks, float scale, int causal,
@@ -961,6 +1240,7 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   // > 128 rows per (sequence, kv head): the 8-wave pipelined kernel; short chunks keep the
   // 4-wave tile (a 256-row tile would be mostly padding)
   const bool big = (long)max_q_len * G > 128;
+  const int pp_env = prefill_variant();
   const int TQ = (big ? 256 : 128) / G;
   const int ntiles = (max_q_len + TQ - 1) / TQ;
   // XCD-per-kv-head order measured +5-47 % TF/s (profiles/r1_prefill_head_fast.txt: 457 -> 672 at
@@ -977,7 +1257,19 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
                         : (head_fast ? dim3(Hkv, ntiles, num_seqs) : grid);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && head_fast)                                                                                          \
+  if (big && head_fast && pp_env == 1)                                                                                      \
+    hipLaunchKernelGGL((prefill3_kernel<DD, true, true, false>), grid2, dim3(512), 0, stream,                    \
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+  else if (big && head_fast && pp_env == 2)                                                                                 \
+    hipLaunchKernelGGL((prefill3_kernel<DD, true, false, false>), grid2, dim3(512), 0, stream,                   \
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+  else if (big && head_fast && pp_env == 3)                                                                                 \
+    hipLaunchKernelGGL((prefill3_kernel<DD, true, true, true>), grid2, dim3(512), 0, stream,                     \
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+  else if (big && head_fast)                                                                                     \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), grid2, dim3(512), 0, stream,                           \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \

@@ -79,12 +79,15 @@ struct MoeArgs {
   int E;
 };
 
-// EPI_SAMPLE: per-row temperature (<= 0: greedy) and seed; pv / pi [M, 2 * N / 256] partial bests
+// EPI_SAMPLE: per-row temperature (<= 0: greedy) and seed; pv / pi [M, 2 * N / 256] partial bests.
+// Vocabulary-parallel (a TP rank's shard): token ids are voff + local row, and local rows >= vvalid
+// (the shard's padding up to a multiple of 256) never win.
 struct SampleArgs {
   const float* temps;
   const unsigned long long* seeds;
   float* pv;
   int* pi;
+  int voff, vvalid;
 };
 
 // wave-quantisation tail (above): dpn whole tiles, then L tail tiles x s K-splits; part =
@@ -520,9 +523,10 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       for (int f = 0; f < 8; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int idx = n0 + wa * 128 + f * 16 + 4 * g + r;
+          const int loc = n0 + wa * 128 + f * 16 + 4 * g + r, idx = sa.voff + loc;
           float v = (float)(bf16)acc[f][t][r];          // the bf16 logit the unfused path samples
           if (!greedy) v = v * inv_t + gumbel_noise(seed, idx);
+          if (loc >= sa.vvalid) v = -INFINITY;
           better(bv, bi, v, idx);
         }
 #pragma unroll
@@ -753,7 +757,7 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
 // Reduce a row's (score, token) partials of the fused LM head (EPI_SAMPLE) to its sampled token:
 // one 256-thread workgroup per row, ties to the smallest token id (sample_final_kernel's rule).
 __global__ void __launch_bounds__(256) lm_sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                              int P, int* __restrict__ out) {
+                                                              int P, int* __restrict__ out, int* __restrict__ pairs) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int row = blockIdx.x;
@@ -774,7 +778,11 @@ __global__ void __launch_bounds__(256) lm_sample_final_kernel(const float* __res
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int k = 1; k < 4; ++k) better(bv, bi, sv[k], si[k]);
-    out[row] = bi;
+    if (out) out[row] = bi;
+    if (pairs) {   // (score bits, token id): a vocab shard's candidate for the cross-rank pick
+      pairs[2 * row] = __float_as_int(bv);
+      pairs[2 * row + 1] = bi;
+    }
   }
 }
 
@@ -789,9 +797,31 @@ PENNY_API int penny_lm_head_sample(const void* X, int ldx, const void* W, int K,
   const int P = 2 * (V / TN);
   float* pv = static_cast<float*>(workspace);
   int* pi = reinterpret_cast<int*>(pv + (long)M * P);
-  const SampleArgs sa{temps, seeds, pv, pi};
+  const SampleArgs sa{temps, seeds, pv, pi, 0, V};
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI_SAMPLE>), grid_for(M, V, 1), dim3(512), 0, stream, X, ldx, W, K,
                      nullptr, 0, (const bf16*)nullptr, 0, M, V, 1, RopeArgs{}, MoeArgs{}, sa, TailArgs{});
-  hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, out);
+  hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, out, (int*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Vocabulary-parallel form (a TP rank's LM-head shard, SURVEY C2 "per-rank top-k then gather"):
+// W [Vpad, K] holds vocabulary rows voff .. voff + vvalid - 1 (rows vvalid .. Vpad - 1 padding),
+// and pairs [M, 2] int32 receives each row's best (score bits, GLOBAL token id) -- the noise is
+// keyed by the global id, so the best pair over the shards is exactly the TP = 1 sample.
+// Contract (checked): Vpad % 256 == 0, 0 < vvalid <= Vpad, K % 64 == 0, ldx % 8 == 0.
+PENNY_API int penny_lm_head_sample_shard(const void* X, int ldx, const void* W, int K, int M, int Vpad, int vvalid,
+                                         int voff, const float* temps, const unsigned long long* seeds,
+                                         void* workspace, int* pairs, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (Vpad % TN || vvalid <= 0 || vvalid > Vpad || voff < 0 || K % BK || ldx % 8 || !temps || !seeds ||
+      !workspace || !pairs)
+    return (int)hipErrorInvalidValue;
+  const int P = 2 * (Vpad / TN);
+  float* pv = static_cast<float*>(workspace);
+  int* pi = reinterpret_cast<int*>(pv + (long)M * P);
+  const SampleArgs sa{temps, seeds, pv, pi, voff, vvalid};
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI_SAMPLE>), grid_for(M, Vpad, 1), dim3(512), 0, stream, X, ldx, W, K,
+                     nullptr, 0, (const bf16*)nullptr, 0, M, Vpad, 1, RopeArgs{}, MoeArgs{}, sa, TailArgs{});
+  hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, (int*)nullptr, pairs);
   return (int)hipGetLastError();
 }

@@ -203,7 +203,8 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
                                                              const float* __restrict__ temps,
                                                              const unsigned long long* __restrict__ seeds,
                                                              const float* __restrict__ thresh,
-                                                             float* __restrict__ pv, int* __restrict__ pi, int V) {
+                                                             float* __restrict__ pv, int* __restrict__ pi, int V,
+                                                             int voff) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int row = blockIdx.x, split = blockIdx.y;
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
     load8<T>(lr + c * 8, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int idx = c * 8 + k;
+      const int idx = voff + c * 8 + k;     // global token id (vocab shard offset)
       float v = f[k];
       if (v < floor_l) continue;
       if (!greedy) {
@@ -233,8 +234,9 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
     }
   }
   if (split == SAMPLE_SPLITS - 1) {  // tail (V not a multiple of 8)
-    for (int idx = (V & ~7) + threadIdx.x; idx < V; idx += blockDim.x) {
-      float v = (float)lr[idx];
+    for (int loc = (V & ~7) + threadIdx.x; loc < V; loc += blockDim.x) {
+      const int idx = voff + loc;
+      float v = (float)lr[loc];
       if (v < floor_l) continue;
       if (!greedy) {
         v = v * inv_t + gumbel_noise(seed, idx);
@@ -261,7 +263,8 @@ __global__ void __launch_bounds__(256) sample_partial_kernel(const T* __restrict
   }
 }
 
-__global__ void sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi, int* __restrict__ out) {
+__global__ void sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi, int* __restrict__ out,
+                                    int* __restrict__ pairs) {
   const int row = blockIdx.x, lane = threadIdx.x;
   float bv = lane < SAMPLE_SPLITS ? pv[row * SAMPLE_SPLITS + lane] : -INFINITY;
   int bi = lane < SAMPLE_SPLITS ? pi[row * SAMPLE_SPLITS + lane] : 0x7fffffff;
@@ -271,7 +274,13 @@ __global__ void sample_final_kernel(const float* __restrict__ pv, const int* __r
     const int oi = __shfl_xor(bi, o, 64);
     better(bv, bi, ov, oi);
   }
-  if (lane == 0) out[row] = bi;
+  if (lane == 0) {
+    if (out) out[row] = bi;
+    if (pairs) {
+      pairs[2 * row] = __float_as_int(bv);
+      pairs[2 * row + 1] = bi;
+    }
+  }
 }
 
 // workspace: B * SAMPLE_SPLITS floats + B * SAMPLE_SPLITS ints + B floats (thresholds)
@@ -296,12 +305,36 @@ PENNY_API int penny_sample(const void* logits, int is_fp32, long row_stride, con
   dim3 grid(B, SAMPLE_SPLITS);
   if (is_fp32) {
     hipLaunchKernelGGL(sample_partial_kernel<float>, grid, dim3(256), 0, stream, (const float*)logits, row_stride,
-                       temps, seeds, th, pv, pi, V);
+                       temps, seeds, th, pv, pi, V, 0);
   } else {
     hipLaunchKernelGGL(sample_partial_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)logits, row_stride,
-                       temps, seeds, th, pv, pi, V);
+                       temps, seeds, th, pv, pi, V, 0);
   }
-  hipLaunchKernelGGL(sample_final_kernel, dim3(B), dim3(64), 0, stream, pv, pi, out);
+  hipLaunchKernelGGL(sample_final_kernel, dim3(B), dim3(64), 0, stream, pv, pi, out, (int*)nullptr);
+  PENNY_RETURN_LAUNCH();
+}
+
+// Vocabulary-parallel sampling of one TP rank's logit shard [B, V] (global ids voff .. voff+V-1):
+// pairs [B, 2] int32 = each row's best (score bits, global token id); the ranks' pairs are then
+// all-gathered and the best taken (ops.sampling.pick_pairs) -- [B, 2] on the wire instead of the
+// [B, V*tp] logits.  No top-k / top-p (they need the whole distribution).
+// workspace: B * SAMPLE_SPLITS floats + as many ints.
+PENNY_API int penny_sample_shard(const void* logits, int is_fp32, long row_stride, const float* temps,
+                                 const unsigned long long* seeds, int* pairs, void* workspace, int B, int V, int voff,
+                                 hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (!pairs || !workspace || V <= 0 || voff < 0) return (int)hipErrorInvalidValue;
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + (long)B * SAMPLE_SPLITS);
+  dim3 grid(B, SAMPLE_SPLITS);
+  if (is_fp32) {
+    hipLaunchKernelGGL(sample_partial_kernel<float>, grid, dim3(256), 0, stream, (const float*)logits, row_stride,
+                       temps, seeds, (const float*)nullptr, pv, pi, V, voff);
+  } else {
+    hipLaunchKernelGGL(sample_partial_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)logits, row_stride,
+                       temps, seeds, (const float*)nullptr, pv, pi, V, voff);
+  }
+  hipLaunchKernelGGL(sample_final_kernel, dim3(B), dim3(64), 0, stream, pv, pi, (int*)nullptr, pairs);
   PENNY_RETURN_LAUNCH();
 }
 

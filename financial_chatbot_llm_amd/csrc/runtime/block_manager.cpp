@@ -1,16 +1,22 @@
-// pybind11 binding of the native paged-KV block allocator (block_allocator.h): module
-// _penny_runtime, class BlockAllocator; the engine-facing wrapper is
-// engine/native_block_manager.py.
+// pybind11 bindings of the native host runtime, module _penny_runtime:
+//   BlockAllocator -- the paged-KV block allocator (block_allocator.h; engine-facing wrapper
+//                     engine/native_block_manager.py)
+//   StepRing       -- the shared-memory TP step-broadcast ring (step_ring.h; parallel/step_ring.py)
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <vector>
+
 #include "block_allocator.h"
+#include "step_ring.h"
 
 namespace py = pybind11;
 using penny::BlockAllocator;
+using penny::StepRing;
 
 PYBIND11_MODULE(_penny_runtime, m) {
-  m.doc() = "Native host runtime for the MI355X serving engine (paged-KV block allocator)";
+  m.doc() = "Native host runtime for the MI355X serving engine (paged-KV block allocator, TP step ring)";
   py::class_<BlockAllocator>(m, "BlockAllocator")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("prefix_caching"))
       .def("num_blocks", &BlockAllocator::num_blocks)
@@ -28,4 +34,40 @@ PYBIND11_MODULE(_penny_runtime, m) {
       .def_property_readonly("hits", &BlockAllocator::hits)
       .def_property_readonly("queries", &BlockAllocator::queries)
       .def_property_readonly("evictions", &BlockAllocator::evictions);
+
+  py::class_<StepRing>(m, "StepRing")
+      .def(py::init<const std::string&, bool, uint64_t, uint64_t, uint64_t>(), py::arg("name"), py::arg("create"),
+           py::arg("nslots") = 8, py::arg("slot_bytes") = 1 << 20, py::arg("nreaders") = 1)
+      .def_property_readonly("name", &StepRing::name)
+      .def_property_readonly("slot_bytes", &StepRing::slot_bytes)
+      .def_property_readonly("nslots", &StepRing::nslots)
+      .def_property_readonly("nreaders", &StepRing::nreaders)
+      .def_property_readonly("closed", &StepRing::closed)
+      .def_property_readonly("head", &StepRing::head)
+      // writer: False if the message exceeds a slot (send it another way); raises on timeout
+      .def("put",
+           [](StepRing& r, py::buffer b, double timeout_s) {
+             py::buffer_info info = b.request();
+             const uint64_t len = (uint64_t)info.size * (uint64_t)info.itemsize;
+             const void* ptr = info.ptr;
+             py::gil_scoped_release nogil;
+             return r.put(ptr, len, timeout_s);
+           },
+           py::arg("data"), py::arg("timeout_s") = 300.0)
+      // reader: the next message as a uint8 array, or None on timeout
+      .def("get",
+           [](StepRing& r, uint64_t reader, double timeout_s) -> py::object {
+             std::vector<uint8_t> buf;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = r.get(reader, buf, timeout_s);
+             }
+             if (!ok) return py::none();
+             py::array_t<uint8_t> out((py::ssize_t)buf.size());
+             if (!buf.empty()) std::memcpy(out.mutable_data(), buf.data(), buf.size());
+             return std::move(out);
+           },
+           py::arg("reader"), py::arg("timeout_s") = -1.0)
+      .def("close", &StepRing::close);
 }

@@ -95,6 +95,8 @@ class LLMEngine:
                 comm.enable_custom_all_reduce()
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
+        if self.ps.tp_size > 1 and getattr(cfg, "step_ring", True):
+            comm.enable_step_channel()      # collective too; None -> gloo C4
         self.profiler = StepProfiler(rank=self.ps.rank)
         # context parallelism: long prompts prefilled by the whole CP replica (engine/context_prefill.py)
         self.cp = None
@@ -512,12 +514,28 @@ class LLMEngine:
         return outs
 
     def follower_loop(self) -> None:
-        """Non-leader TP ranks: replay the leader's steps until it broadcasts None."""
+        """Non-leader TP ranks: replay the leader's steps until it broadcasts None -- with the
+        leader's own one-step-in-flight pipeline: step N+1 is launched before step N is collected,
+        so the follower's host (C4 receive, input staging) works while its GPU runs, and it never
+        adds a device sync between the leader's launches."""
+        prev = None
+        t = self.timing
         while True:
+            t0 = time.perf_counter()
             si = comm.broadcast_step(None)
+            t1 = time.perf_counter()
+            t["recv_s"] = t.get("recv_s", 0.0) + t1 - t0
             if si is None:
-                return
-            self.runner.execute(si)
+                break
+            cur = self.runner.launch(si)
+            t2 = time.perf_counter()
+            t["execute_s"] += t2 - t1
+            if prev is not None:
+                prev.result()
+            t["post_s"] += time.perf_counter() - t2
+            prev = cur
+        if prev is not None:
+            prev.result()
 
     def stop_followers(self) -> None:
         if self.ps.tp_size > 1 and self.ps.is_tp_leader:

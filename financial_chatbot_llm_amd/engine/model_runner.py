@@ -403,6 +403,14 @@ class ModelRunner:
         m = self.model
         return getattr(m, "tp_size", 1) == 1 and hasattr(m, "lm_weight") and ops.fused_lm_head_ok(h, m.lm_weight())
 
+    def _shard_sampling(self) -> bool:
+        """TP: rows without top-k / top-p are sampled vocab-parallel (``sample_vocab_parallel``:
+        [B, 2] candidates all-gathered instead of the [B, V] logits); ``PENNY_VOCAB_PARALLEL_SAMPLE=0``
+        restores logits all-gather + sampler."""
+        m = self.model
+        return (getattr(m, "tp_size", 1) > 1 and hasattr(m, "sample_vocab_parallel")
+                and os.environ.get("PENNY_VOCAB_PARALLEL_SAMPLE", "1") != "0")
+
     @staticmethod
     def _has_filters(si: StepInputs) -> bool:
         return bool((si.top_k > 0).any() or (si.top_p < 1).any())
@@ -412,6 +420,9 @@ class ModelRunner:
         where it applies (no top-k / top-p rows), else logits -> sampler."""
         h = self._hidden(si)
         hs = h.index_select(0, self._to_dev(si.logits_idx))
+        if not self._has_filters(si) and self._shard_sampling():
+            self.stats["vocab_parallel_sample_steps"] = self.stats.get("vocab_parallel_sample_steps", 0) + 1
+            return self.model.sample_vocab_parallel(hs, self._to_dev(si.temps), self._to_dev(si.seeds))
         if not self._has_filters(si) and self._fused_sampling(hs):
             self.stats["fused_lm_head_steps"] = self.stats.get("fused_lm_head_steps", 0) + 1
             return ops.lm_head_sample(hs, self.model.lm_weight(), self._to_dev(si.temps), self._to_dev(si.seeds))
@@ -526,6 +537,8 @@ class ModelRunner:
                                  ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
                                  cascade=s["cascade"])
         h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
+        if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
+            return self.model.sample_vocab_parallel(h, s["temps"][:B], s["seeds"][:B])
         if self._fused_sampling(h):
             return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B])
         logits = self.model.logits(h)
@@ -549,8 +562,8 @@ class ModelRunner:
                 out = self._run_static(B)
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
-            fused = self._fused_sampling(torch.empty((B, self.model.cfg.hidden_size), dtype=torch.bfloat16,
-                                                     device=self.device))
+            fused = self._shard_sampling() or self._fused_sampling(
+                torch.empty((B, self.model.cfg.hidden_size), dtype=torch.bfloat16, device=self.device))
             self.graphs[B] = _DecodeGraph(g, B, out, fused)
         torch.cuda.synchronize()
         logger.info(f"captured decode hipGraphs for batch sizes {sorted(self.graphs)}")

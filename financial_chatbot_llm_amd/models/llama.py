@@ -146,6 +146,22 @@ class DecoderModel:
                 continue
             if name.endswith((".qkv", ".o", ".down", ".gate_up")) and uses_tiled_weight(*t.shape):
                 self.wt[name] = tile_weight(t)
+        self._pad_vocab_shard()
+
+    def _pad_vocab_shard(self) -> None:
+        """Under TP the LM-head shard (V/tp rows: 16,032 for Llama-3 at TP=8) lives in a buffer padded
+        to a multiple of 256 rows, so the fused LM-head sampler's 256-row tiles can run on it
+        (``sample_vocab_parallel``); ``lm_weight()`` stays the exact-size view."""
+        name = "embed" if self.cfg.tie_embeddings else "lm_head"
+        t = self.w.get(name)
+        self._lm_pad = t
+        if t is None or self.tp_size == 1 or self.device.type != "cuda" or t.shape[0] % 256 == 0:
+            return
+        rows = t.shape[0]
+        buf = torch.zeros((-(-rows // 256) * 256, t.shape[1]), dtype=t.dtype, device=t.device)
+        buf[:rows].copy_(t)
+        self.w[name] = buf[:rows]
+        self._lm_pad = buf
 
     def num_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.w.values())
@@ -345,6 +361,20 @@ class DecoderModel:
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         out = linear(h, self.lm_weight())
         return comm.tp_all_gather_last(out) if self.tp_size > 1 else out
+
+    def sample_vocab_parallel(self, h: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor) -> torch.Tensor:
+        """TP sampling without the logits all-gather: each rank draws its vocab shard's
+        Gumbel-max candidate -- on the fused LM-head sampler from FUSED_LM_HEAD_MIN_M rows, else
+        local logits + the shard sampler -- and the [B, 2] candidates are all-gathered and the best
+        taken.  Same noise (keyed by the global token id) and tie rule as TP = 1: the TP = 1 token
+        whenever the shard logits equal the full ones bitwise (always on the fused path)."""
+        w = self.lm_weight()
+        pad = getattr(self, "_lm_pad", None)
+        if pad is not None and ops.fused_lm_head_ok(h, pad):
+            pairs = ops.lm_head_sample_shard(h, pad, w.shape[0], self.vocab_start, temps, seeds)
+        else:
+            pairs = ops.sample_shard(linear(h, w), temps, seeds, self.vocab_start, self.cfg.vocab_size)
+        return ops.pick_pairs(comm.tp_all_gather_pairs(pairs))
 
 
 class LlamaModel(DecoderModel):

@@ -10,7 +10,8 @@ from .attention import (KV_BS, CascadeInputs, DecodeWorkspace, decode, default_s
 from .embedding import embedding
 from .norm import layer_norm, rms_norm
 from .retrieval import filtered_topk
-from .sampling import apply_top_k_top_p, fused_lm_head_ok, lm_head_sample, sample
+from .sampling import (apply_top_k_top_p, fused_lm_head_ok, lm_head_sample, lm_head_sample_shard, pick_pairs, sample,
+                       sample_shard)
 
 __all__ = ["gelu_", "silu_mul", "KV_BS", "DecodeWorkspace", "decode", "default_scale", "prefill", "rope_cos_sin",
            "rope_kv_write", "write_kv_ref", "embedding", "layer_norm", "rms_norm", "filtered_topk",

@@ -47,10 +47,13 @@ _SIGS = {
     "penny_rope_kv_write_slabs": [P, c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P,
                                 c_int, P],
+    "penny_attention_prefill_variant": [c_int],
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_float, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P],
     "penny_sample": [P, c_int, c_long, P, P, P, P, P, P, c_int, c_int, P],
     "penny_lm_head_sample": [P, c_int, P, c_int, c_int, c_int, P, P, P, P, P],
+    "penny_lm_head_sample_shard": [P, c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P],
+    "penny_sample_shard": [P, c_int, c_long, P, P, P, P, c_int, c_int, c_int, P],
     "penny_topk_topp_threshold": [P, c_int, c_long, P, P, P, P, c_int, c_int, P],
     "penny_moe_route": [P, c_int, c_int, c_int, P, P, P, P, P],
     "penny_quant_rows_fp8": [P, c_int, c_int, c_int, P, P, P],

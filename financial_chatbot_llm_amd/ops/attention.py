@@ -204,6 +204,14 @@ def prefill_work_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, causal: bo
     return np.stack([np.asarray(seqs, np.int32)[order], np.asarray(tiles, np.int32)[order]], 1)
 
 
+def prefill_variant(v: int = -1) -> int:
+    """Select the big-tile prefill kernel for this process (returns the previous choice; -1 only
+    reads it): 1 = ping-pong prefill3 with ones-MFMA row sums (default), 2 = ping-pong with VALU
+    row sums, 3 = 1 + static priority for waves 4-7, 0 = prefill2 (``PENNY_PREFILL_PP`` sets the
+    initial value).  In-process A/B runs and tests only."""
+    return int(N.load().penny_attention_prefill_variant(int(v)))
+
+
 def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor,
             k_cache: torch.Tensor, v_cache: torch.Tensor, scale: float, causal: bool = True,
             max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None,

@@ -97,6 +97,67 @@ def lm_head_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor,
     return out
 
 
+# ----------------------------------------------------------------------------------------------
+# Vocabulary-parallel sampling (SURVEY C2 "per-rank top-k then gather"): under TP each rank scores
+# its own vocab shard -- Gumbel noise keyed by the GLOBAL token id -- and keeps one (score, id)
+# candidate per row; the candidates ([B, 2] int32 per rank) are all-gathered and the best taken.
+# Gumbel-max is exactly shard-decomposable, so this is the TP = 1 sample without the [B, V]
+# logits all-gather (33 MB per decode step at B = 128 for Llama-3 TP=8).
+# ----------------------------------------------------------------------------------------------
+def sample_shard(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor, voff: int,
+                 vocab_total: int) -> torch.Tensor:
+    """logits [B, Vs] of global vocabulary ids voff .. voff+Vs-1 -> pairs [B, 2] int32 (f32 score
+    bits, global id) of each row's Gumbel-max (T <= 0: argmax) winner within the shard."""
+    B, Vs = logits.shape
+    if N.use_native(logits):
+        assert logits.stride(1) == 1 and logits.stride(0) % 8 == 0
+        pairs = torch.empty((B, 2), dtype=torch.int32, device=logits.device)
+        ws = torch.empty((2 * B * SPLITS,), dtype=torch.float32, device=logits.device)
+        N.call("penny_sample_shard", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
+               N.ptr(temperatures), N.ptr(seeds), N.ptr(pairs), N.ptr(ws), B, Vs, int(voff), N.stream())
+        return pairs
+    lf = logits.float()
+    temps = temperatures.tolist()
+    sd = seeds.tolist()
+    sc = torch.empty(B, dtype=torch.float32)
+    ids = torch.empty(B, dtype=torch.int32)
+    for b in range(B):
+        if temps[b] <= 0:
+            v = lf[b]
+        else:   # the same per-row noise over the WHOLE vocabulary as ``sample``, sliced to the shard
+            g = torch.Generator().manual_seed(int(sd[b]) & 0x7FFFFFFFFFFFFFFF)
+            u = torch.rand(vocab_total, generator=g, dtype=torch.float64).clamp_(1e-12, 1 - 1e-12)[voff:voff + Vs]
+            v = (lf[b].double() / temps[b] - torch.log(-torch.log(u))).float()
+        j = int(torch.argmax(v).item())
+        sc[b] = v[j]
+        ids[b] = voff + j
+    return torch.stack([sc.view(torch.int32), ids], 1).to(logits.device)
+
+
+def lm_head_sample_shard(h: torch.Tensor, w_pad: torch.Tensor, vvalid: int, voff: int, temperatures: torch.Tensor,
+                         seeds: torch.Tensor) -> torch.Tensor:
+    """Fused LM head + sampler on one vocab shard: ``w_pad`` [Vpad, K] (Vpad % 256 == 0) holds global
+    rows voff .. voff+vvalid-1 then padding -> pairs [M, 2] as :func:`sample_shard`."""
+    M, K = h.shape
+    Vpad = w_pad.shape[0]
+    pairs = torch.empty((M, 2), dtype=torch.int32, device=h.device)
+    ws = torch.empty((2 * M * 2 * (Vpad // 256),), dtype=torch.float32, device=h.device)
+    N.call("penny_lm_head_sample_shard", N.ptr(h), h.stride(0), N.ptr(w_pad), K, M, Vpad, int(vvalid), int(voff),
+           N.ptr(temperatures.to(torch.float32).contiguous()), N.ptr(seeds.contiguous()), N.ptr(ws), N.ptr(pairs),
+           N.stream())
+    return pairs
+
+
+def pick_pairs(allp: torch.Tensor) -> torch.Tensor:
+    """[R, B, 2] candidates of R vocab shards -> [B] int32 tokens: the highest score, ties to the
+    smallest token id (the single-kernel sampler's rule).  Device ops only (graph-capturable)."""
+    sc = allp[..., 0].contiguous().view(torch.float32)
+    ids = allp[..., 1]
+    best = sc.max(0, keepdim=True).values
+    cand = torch.where(sc == best, ids, torch.full_like(ids, 0x7FFFFFFF))
+    return cand.min(0).values.to(torch.int32)
+
+
 def topk_topp_threshold(logits: torch.Tensor, temperatures: torch.Tensor, top_k: torch.Tensor,
                         top_p: torch.Tensor) -> torch.Tensor:
     """The HIP filter's per-row logit threshold (-inf: keep all) -- diagnostics/tests."""

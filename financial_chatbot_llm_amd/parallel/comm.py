@@ -5,15 +5,18 @@
   the prefill micro-batch pipeline (``DecoderModel.forward_overlap``) computes one half of the
   batch while the other half's all-reduce is on the wire.  In-place ``dist.all_reduce`` on the TP group; captured into
   the decode hipGraph together with the GEMMs.
-* C2 ``tp_all_gather_last``: vocab-parallel LM-head logits ([B, V/tp] -> [B, V]); embedding
-  partials are summed with C1.
+* C2 ``tp_all_gather_pairs``: vocab-parallel sampling -- each rank's per-row (score, token id)
+  candidate from its vocab shard ([B, 2] int32 -> [tp, B, 2]); ``tp_all_gather_last`` gathers the
+  full [B, V] logits only for rows with top-k / top-p filters.  Embedding partials are summed
+  with C1.
 * SP ``tp_reduce_scatter_rows`` / ``tp_all_gather_rows``: sequence-parallel prefill (Megatron
   SP) -- the residual stream is sharded by rows between the row-parallel and column-parallel
   GEMMs (reduce-scatter after O/down, all-gather before QKV/gate-up).
 * C4 ``broadcast_step``: the TP leader's scheduler decisions (token ids, positions, block
   tables, sampling params) for a step, so non-leader ranks replay the identical forward: ONE flat
-  byte buffer (``StepInputs.pack``), sent over a gloo twin of the TP group -- host memory to host
-  memory, no pickling and no device round trip (a header broadcast carries the length).
+  byte buffer (``StepInputs.pack``) -- through the node-local shared-memory ring
+  (``step_ring.py``, one release store per step) when enabled, else over a gloo twin of the TP
+  group (a header broadcast carries the length).  Host memory to host memory either way.
 
 xGMI is point-to-point (7 links per GPU): for 8-way TP the bandwidth-optimal ring is per-link
 bound, so large messages (prefill activations) use RCCL's ring/tree; decode messages are
@@ -103,6 +106,30 @@ def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts, dim=-1)
 
 
+def tp_all_gather_pairs(pairs: torch.Tensor) -> torch.Tensor:
+    """Vocab-parallel sampling candidates: every rank's [B, 2] int32 (score bits, token id) ->
+    [tp, B, 2] in rank order.  The custom xGMI gather moves the bytes as bf16 (graph-capturable);
+    RCCL / gloo otherwise."""
+    s = state()
+    if s.tp_size == 1:
+        return pairs[None]
+    B = pairs.shape[0]
+    x = pairs.contiguous()
+    if B % 2:                                    # the bf16 view must be a multiple of 8 elements
+        x = torch.cat([x, x[:1]], 0)
+    xb = x.view(torch.bfloat16)
+    if _CUSTOM_AR is not None and _CUSTOM_AR.gather_eligible(xb):
+        g = _CUSTOM_AR.all_gather(xb)            # [tp, B', 4] bf16
+        return g.view(torch.int32).view(s.tp_size, -1, 2)[:, :B]
+    if _is_gloo(s.tp_group):
+        parts = [torch.empty_like(x) for _ in range(s.tp_size)]
+        dist.all_gather(parts, x, group=s.tp_group)
+        return torch.stack(parts, 0)[:, :B]
+    out = torch.empty((s.tp_size * x.shape[0], 2), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    return out.view(s.tp_size, -1, 2)[:, :B]
+
+
 def _is_gloo(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
@@ -142,14 +169,47 @@ def tp_all_gather_rows(x: torch.Tensor) -> torch.Tensor:
 
 
 _STOP = -1
+_STEP_CHANNEL = None   # parallel.step_ring.StepChannel of the TP group (enable_step_channel)
+
+
+def enable_step_channel():
+    """C4 over the node-local shared-memory ring (``step_ring.py``) instead of two gloo
+    broadcasts per step.  Collective over the TP group; returns the channel or None (fallback)."""
+    global _STEP_CHANNEL
+    s = state()
+    if s.tp_size > 1 and _STEP_CHANNEL is None:
+        from .step_ring import make_step_channel
+        _STEP_CHANNEL = make_step_channel(s)
+    return _STEP_CHANNEL
+
+
+def step_channel():
+    return _STEP_CHANNEL
+
+
+def disable_step_channel() -> None:
+    global _STEP_CHANNEL
+    if _STEP_CHANNEL is not None:
+        _STEP_CHANNEL.close()
+    _STEP_CHANNEL = None
 
 
 def broadcast_step(si: Any) -> Any:
     """Leader: ``si`` (a StepInputs, or None = stop) -> followers; followers pass None and get
-    the leader's value back."""
+    the leader's value back.  Over the shared-memory ring when enabled, else gloo."""
     s = state()
     if s.tp_size == 1:
         return si
+    ch = _STEP_CHANNEL
+    if ch is not None:
+        if s.is_tp_leader:
+            ch.send(None if si is None else si.pack())
+            return si
+        buf = ch.recv()
+        if buf is None:
+            return None
+        from ..engine.model_runner import StepInputs
+        return StepInputs.unpack(buf)
     import numpy as np
     group = s.tp_cpu_group if s.tp_cpu_group is not None else s.tp_group
     head = torch.zeros(1, dtype=torch.int64)

@@ -130,6 +130,41 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     close(out, ref, atol=2e-2)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
+    # respond chunk behind a cached prefix + decide-like and spec-like chunks (dead waves: 17 x 4 rows)
+    (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
+    (32, 8, 128, True, [(257, 257), (64, 3000)], 12.0),      # rescale path, one block per op
+    (8, 1, 128, True, [(40, 40), (33, 500)], 1.0),            # G = 8
+    (12, 12, 64, False, [(200, 200), (33, 33)], 1.0),         # bidirectional, D = 64
+])
+def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, qscale):
+    """The ping-pong kernel (prefill3, variants 1-3) and prefill2 (0) vs the fp32 reference, with the
+    LPT work list and without (also the lse output)."""
+    g = torch.Generator().manual_seed(40 + variant)
+    qlens = [a for a, _ in lens]
+    ctx = [b for _, b in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    q = rnd(int(cu[-1]), Hq, D, scale=qscale, gen=g)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, causal)
+    lse_ref = torch.empty(q.shape[0], Hq)
+    ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, causal, lse=lse_ref)
+    wl = ops.attention.prefill_work_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, causal)
+    old = ops.attention.prefill_variant(variant)
+    try:
+        for work in (None, torch.from_numpy(wl).to(DEV) if wl is not None else None):
+            lse = torch.empty(q.shape[0], Hq, device=DEV)
+            out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale,
+                              causal, max_q_len=max(qlens), lse=lse, work=work)
+            close(out, ref, atol=2e-2)
+            close(lse, lse_ref, atol=2e-2, rtol=1e-3)
+    finally:
+        ops.attention.prefill_variant(old)
+
+
 @pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
                                          # B >= 96 / >= 192: longer partitions (pb 16 / 32)
                                          (32, 8, [(37 * i) % 3000 + 1 for i in range(100)]),

@@ -51,8 +51,15 @@ def _worker(rank, world, port, q):
         if rank == 0:
             out = eng.generate([list(range(10, 90)), list(range(200, 230))],
                                SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
+            # temperature sampling, vocab-parallel: per-shard Gumbel-max candidates gathered (C2)
+            out = (out, eng.generate([list(range(10, 90)), list(range(200, 230))],
+                                     SamplingParams(temperature=0.9, max_tokens=8, ignore_eos=True, seed=123)))
             eng.stop_followers()
             assert eng.runner.stats["overlap_steps"] >= 2, eng.runner.stats
+            assert eng.runner.stats.get("vocab_parallel_sample_steps", 0) > 0, eng.runner.stats
+            from financial_chatbot_llm_amd.parallel import comm
+            ch = comm.step_channel()        # C4 went through the shared-memory ring
+            assert ch is not None and ch.sent > 0 and ch.fallbacks == 0
         else:
             eng.follower_loop()
         q.put((rank, to_np(logits_tp), out))
@@ -97,4 +104,7 @@ def test_tp_matches_tp1(world):
     eng = LLMEngine(ecfg, model=ref, tokenizer=SyntheticLlamaTokenizer(cfg.vocab_size))
     want = eng.generate([list(range(10, 90)), list(range(200, 230))],
                         SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True))
-    assert res[0][1] == want
+    want_t = eng.generate([list(range(10, 90)), list(range(200, 230))],
+                          SamplingParams(temperature=0.9, max_tokens=8, ignore_eos=True, seed=123))
+    assert res[0][1][0] == want
+    assert res[0][1][1] == want_t          # the TP = 1 sampler's tokens, same seeds
