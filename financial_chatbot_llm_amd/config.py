@@ -142,6 +142,9 @@ class EngineConfig:
     # the continuing chunks of long prefills (0 = off)
     sched_sjf_tokens: int = 0
     sched_sjf_step_cap: int = 0             # tokens per step the short-first pass may take (0: all)
+    # per-step reservation for waiting short-output (decide) prompts against continuing long
+    # prefills (engine/scheduler.py; 0 = off)
+    sched_short_reserve_tokens: int = 0
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
     # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
@@ -175,6 +178,7 @@ class EngineConfig:
             sched_burst_age_s=_env_float("PENNY_BURST_AGE_S", cls.sched_burst_age_s),
             sched_sjf_tokens=_env_int("PENNY_SJF_TOKENS", cls.sched_sjf_tokens),
             sched_sjf_step_cap=_env_int("PENNY_SJF_STEP_CAP", cls.sched_sjf_step_cap),
+            sched_short_reserve_tokens=_env_int("PENNY_SHORT_RESERVE", cls.sched_short_reserve_tokens),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),

@@ -74,7 +74,7 @@ class Scheduler:
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
                  aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
                  cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5,
-                 sjf_tokens: int = 0, sjf_step_cap: int = 0):
+                 sjf_tokens: int = 0, sjf_step_cap: int = 0, short_reserve_tokens: int = 0):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -98,6 +98,13 @@ class Scheduler:
         self.sjf_tokens = sjf_tokens
         self.sjf_step_cap = sjf_step_cap      # at most this many tokens of a step go to 2a (0: budget)
         self.num_sjf_admits = 0
+        # per-step reservation for the short-output class (TTFT tail): while decide-class prompts
+        # wait, the continuing prefills of long prompts may take at most budget - reserve tokens of
+        # a step, so a burst of long respond prefills delays a decide call by at most one step
+        # instead of by the whole burst; the long prefills keep >= budget - reserve per step
+        # (starvation-free) and the reserve is only held while short prompts actually wait
+        self.short_reserve_tokens = short_reserve_tokens
+        self.num_reserved_steps = 0
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
@@ -193,6 +200,17 @@ class Scheduler:
         # cached few-shot prefix) go before the continuing chunks of long prefills
         if self.sjf_tokens > 0 and self.waiting and budget > 0:
             budget = self._admit_short(batch, budget)
+        # reservation: short-output prompts waiting for admission hold back up to
+        # short_reserve_tokens of this step from the continuing long prefills (pass 2); pass 3
+        # admits them first (class order) with whatever is left plus the reserve
+        reserve = 0
+        if self.short_reserve_tokens > 0 and self.waiting and budget > 0:
+            need = sum(q.remaining_prefill for q in self.waiting
+                       if q.params.max_tokens <= self.short_output_tokens and q.pending_src < 0 and not q.awaiting)
+            reserve = min(self.short_reserve_tokens, need, budget)
+            if reserve > 0:
+                self.num_reserved_steps += 1
+        budget -= reserve
         # 2) continuing prefills (not the sequences 2a just admitted: their computed count moves only
         # when this step resolves)
         taken = {id(q) for q, _, _ in batch.prefill}
@@ -206,6 +224,7 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
+        budget += reserve
         # 3) admit waiting sequences, by priority class (preempted, short-output/aged, rest)
         if len(self.waiting) > 1:
             now = self.clock()

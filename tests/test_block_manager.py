@@ -180,6 +180,49 @@ def test_scheduler_admits_short_output_requests_first():
     assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("decide", 0, 60), ("respond", 0, 68)]
 
 
+@pytest.mark.parametrize("reserve", [0, 96])
+def test_short_reserve_bounds_decide_wait_and_never_starves_long_prefills(reserve):
+    """A burst of long respond prefills already running takes whole steps; a decide prompt that
+    arrives meanwhile waits for the burst without a reservation, and is admitted in the very next
+    step with one -- while every step still gives the long prefills budget - reserve tokens, and
+    a stream of short prompts never stops them (starvation freedom)."""
+    clock = [100.0]
+    bm = PyBlockManager(512, BS, True)
+    sch = Scheduler(bm, max_num_seqs=64, max_num_batched_tokens=256, max_model_len=8192, clock=lambda: clock[0],
+                    short_reserve_tokens=reserve)
+    longs = [_mk_params(list(range(10000 * (i + 1), 10000 * (i + 1) + 900)), f"respond{i}", 512, arrival=99.0 + i * 0.01)
+             for i in range(4)]
+    for q in longs:
+        sch.add(q)
+    batch = sch.schedule()                                  # burst admitted: 256 tokens of respond0
+    for q, st, n in batch.prefill:
+        q.num_computed = st + n
+    decide = _mk_params(list(range(5000, 5060)), "decide", 96, arrival=99.5)
+    sch.add(decide)
+    admitted_at, long_tokens = None, []
+    for step in range(1, 40):
+        if step > 1 and step % 2 == 0:                      # a fresh decide every other step
+            sch.add(_mk_params(list(range(6000 + 100 * step, 6000 + 100 * step + 40)), f"d{step}", 96, arrival=99.6))
+        batch = sch.schedule()
+        long_tokens.append(sum(n for q, _, n in batch.prefill if q.request_id.startswith("respond")))
+        if admitted_at is None and any(q is decide for q, _, _ in batch.prefill):
+            admitted_at = step
+        for q, st, n in batch.prefill:
+            q.num_computed = st + n
+        for q in list(sch.running):
+            if q.num_computed >= q.num_tokens:               # prompt done: retire it (no decode here)
+                sch.finish(q, "stop")
+        if all(q.finished for q in longs):
+            break
+    if reserve:
+        assert admitted_at == 1
+        active = [t for t in long_tokens if t > 0]
+        assert min(active[:-1]) >= 256 - reserve             # long prefills keep budget - reserve
+    else:
+        assert admitted_at > 1                               # queued behind the burst's chunks
+    assert all(q.finished for q in longs)                   # never starved
+
+
 def test_scheduler_orders_a_class_by_turn_start():
     """Within a priority class the older TURN goes first: a respond call whose turn started
     before a newer turn's decide call is admitted ahead of it although it arrived later."""
