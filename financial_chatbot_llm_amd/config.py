@@ -118,6 +118,7 @@ class EngineConfig:
     # leader's paged pool (engine/context_prefill.py)
     cp_size: int = 1
     cp_min_tokens: int = 16384
+    cp_layers_per_step: int = 4             # CP prefill layers run per engine step (decode in between)
     kv_block_size: int = 64                 # tokens per KV block (one MFMA KV tile)
     # of (free HBM after weights - 6 GiB); 0.92 leaves ~20 GiB of the 288 GiB unused at the end of
     # the 20/5 bench (engine stats hbm_used_gib: 8B 264.5, Mixtral fp8 267.9; 0.95 measured no

@@ -128,7 +128,7 @@ class LLMEngine:
             seq.finish_reason = "abort"
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work() or self._inflight is not None or bool(self.cp and self.cp.queue)
+        return self.scheduler.has_work() or self._inflight is not None or bool(self.cp and self.cp.busy())
 
     def warmup(self) -> None:
         """Capture decode graphs (all TP ranks must call this together)."""
@@ -140,9 +140,9 @@ class LLMEngine:
         while step N is still on the GPU, then collect N -- the host's scheduling, input packing
         and token bookkeeping hide behind the device instead of idling it between steps."""
         self.profiler.on_step()
-        if self.cp is not None and self.cp.queue:
+        if self.cp is not None and self.cp.busy():
             with marker("engine.cp_prefill"):
-                self.cp.run_pending()
+                self.cp.run_pending()      # one layer slice of a long prompt; the step follows
         with marker("engine.step"):
             return self._step_overlap() if self.async_scheduling else self._step_sync()
 

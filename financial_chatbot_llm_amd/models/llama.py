@@ -293,8 +293,21 @@ class DecoderModel:
         x = torch.cat(xs)
         return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=torch.cat(res))
 
-    def forward_cp(self, ids: torch.Tensor, total_len: int, group=None, kv_sink=None) -> torch.Tensor:
-        """Context-parallel prefill of ONE long prompt (SURVEY §5.7 stretch path, >128k tokens).
+    def forward_cp(self, ids: torch.Tensor, total_len: int, group=None, kv_sink=None, prefix_len: int = 0,
+                   prefix_kv=None) -> torch.Tensor:
+        """:meth:`forward_cp_iter` run to the end (returns the local rows' final hidden states)."""
+        it = self.forward_cp_iter(ids, total_len, group, kv_sink, prefix_len, prefix_kv)
+        while True:
+            try:
+                next(it)
+            except StopIteration as e:
+                return e.value
+
+    def forward_cp_iter(self, ids: torch.Tensor, total_len: int, group=None, kv_sink=None, prefix_len: int = 0,
+                        prefix_kv=None):
+        """Context-parallel prefill of ONE long prompt (SURVEY §5.7 stretch path, >128k tokens),
+        as a generator that yields after every layer (the serving leader interleaves decode steps
+        between layer slices) and returns the local rows' final hidden states.
 
         ``ids`` is this rank's zig-zag shard (``parallel.context.zigzag_shard``) of a
         ``total_len``-token prompt; every CP rank holds the full weights (TP=1 inside the CP
@@ -302,7 +315,10 @@ class DecoderModel:
         attention over the CP group (K/V shards travel one xGMI hop per step; blocks on the HIP
         prefill kernel on the GPU), then O / MLP on the local rows.  Returns the final hidden
         states of the local rows.  ``kv_sink(layer, k, v)`` receives each layer's local K/V shard
-        (``zigzag_unshard`` of every rank's shards is the full cache for the decode rank)."""
+        (``zigzag_unshard`` of every rank's shards is the full cache for the decode rank).
+        ``prefix_len`` tokens before the sharded ones are already cached (a prefix-cache hit):
+        the shard's positions start there, and ``prefix_kv(layer) -> (k, v)`` [P, Hkv, D]
+        supplies that layer's prefix keys on every rank for the ring attention."""
         from ..ops.attention import rope_qk
         from ..ops.gemm import Slabs
         from ..parallel import context as cpx
@@ -310,7 +326,7 @@ class DecoderModel:
         c = self.cfg
         cp = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
-        pos = cpx.zigzag_positions(total_len, cp, rank, device=ids.device)
+        pos = cpx.zigzag_positions(total_len, cp, rank, device=ids.device) + prefix_len
         block = cpx.hip_block_attention if ops._native.use_native(self.w["embed"]) else cpx.torch_block_attention
         x = ops.embedding(ids, self.w["embed"])
         residual = x
@@ -330,10 +346,13 @@ class DecoderModel:
             v = qkv.view(T, self.hq + 2 * self.hkv, self.D)[:, self.hq + self.hkv:].contiguous()
             if kv_sink is not None:
                 kv_sink(i, k, v)
-            a = cpx.ring_attention(q, k, v, total_len, scale=self.scale, causal=True, group=group, block_fn=block)
+            pre = prefix_kv(i) if (prefix_kv is not None and prefix_len > 0) else None
+            a = cpx.ring_attention(q, k, v, total_len, scale=self.scale, causal=True, group=group, block_fn=block,
+                                   prefix=pre)
             a = linear(a.reshape(T, self.hq * self.D), self.w[p + "o"])
             h = ops.rms_norm(a, self.w[p + "post_norm"], c.norm_eps, residual=residual)
             x = self.mlp(i, h)
+            yield i
         return ops.rms_norm(x, self.w["final_norm"], c.norm_eps, residual=residual)
 
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, meta: AttentionMetadata, kv: KVCache) -> torch.Tensor:

@@ -177,24 +177,33 @@ def _ring_peers(group) -> Tuple[int, int, int, int]:
 
 def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, total_len: int,
                    scale: Optional[float] = None, causal: bool = True, group=None,
-                   block_fn: BlockFn = torch_block_attention) -> torch.Tensor:
+                   block_fn: BlockFn = torch_block_attention,
+                   prefix: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Context-parallel attention over the zig-zag shards of one sequence.
 
     ``q`` [Tl,Hq,D], ``k``/``v`` [Tl,Hkv,D] are this rank's shards (``zigzag_shard``) of a
     ``total_len``-token sequence; returns this rank's output rows [Tl,Hq,D] in ``q.dtype``.
+    ``prefix`` (k, v) [P,Hkv,D], the same on every rank: keys BEFORE the sharded tokens (a
+    prefix-cache hit), visible to every query -- one extra block merged by log-sum-exp.
     """
+    scale = scale if scale is not None else q.shape[-1] ** -0.5
+    o = lse = None
+    if prefix is not None and prefix[0].shape[0] > 0:
+        P = prefix[0].shape[0]
+        pos_p = torch.arange(P, device=q.device)
+        pos_qp = torch.full((q.shape[0],), P, dtype=pos_p.dtype, device=q.device)
+        o, lse = block_fn(q, prefix[0], prefix[1], pos_qp, pos_p, scale, False)
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         pos = torch.arange(total_len, device=q.device)
-        o, _ = block_fn(q, k, v, pos, pos, scale or q.shape[-1] ** -0.5, causal)
+        ob, lb = block_fn(q, k, v, pos, pos, scale, causal)
+        o, lse = (ob, lb) if o is None else merge_blocks(o, lse, ob, lb)
         return o.to(q.dtype)
     cp, r, nxt, prv = _ring_peers(group)
-    scale = scale if scale is not None else q.shape[-1] ** -0.5
     pos_q = zigzag_positions(total_len, cp, r, device=q.device)
     kv = torch.stack([k, v]).contiguous()                                   # one message per hop
     # gloo (CPU rehearsals of the GPU path) moves host tensors only: stage the hop through host
     # memory; RCCL sends the device buffer directly over xGMI
     host_hop = kv.is_cuda and dist.get_backend(group) == "gloo"
-    o = lse = None
     for step in range(cp):
         reqs = []
         if step + 1 < cp:                                                   # post next hop first
