@@ -109,6 +109,7 @@ class EngineConfig:
     async_scheduling: bool = True           # overlap host scheduling of step N+1 with GPU step N
     custom_all_reduce: bool = True          # TP decode all-reduces on the one-shot xGMI P2P kernel
     step_ring: bool = True                  # C4 step broadcast over the node-local shm ring (else gloo)
+    tp_dual_decode: bool = True             # TP graph decode as two micro-batch chains on two streams
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
@@ -187,6 +188,7 @@ class EngineConfig:
             async_scheduling=_env_bool("PENNY_ASYNC_SCHEDULING", True),
             custom_all_reduce=_env_bool("PENNY_CUSTOM_AR", True),
             step_ring=_env_bool("PENNY_STEP_RING", True),
+            tp_dual_decode=_env_bool("PENNY_TP_DUAL_DECODE", True),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),
         )

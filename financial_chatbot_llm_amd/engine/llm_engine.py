@@ -94,6 +94,8 @@ class LLMEngine:
         if self.ps.tp_size > 1 and device.type == "cuda" and getattr(cfg, "custom_all_reduce", True):
             try:   # collective over the TP group: every rank constructs its engine together
                 comm.enable_custom_all_reduce()
+                if getattr(cfg, "tp_dual_decode", True):
+                    comm.enable_second_channel()     # the second decode micro-batch chain's AR
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
         if self.ps.tp_size > 1 and getattr(cfg, "step_ring", True):

@@ -234,6 +234,13 @@ class ModelRunner:
         cfg = model.cfg
         self.decode_ws = DecodeWorkspace.create(max(max_decode_batch, 1), model.hq, model.D, max_model_len,
                                                 self.device) if self.on_gpu else None
+        # TP decode as two micro-batch chains on two streams (DecoderModel.forward_decode_dual): their
+        # all-reduces hide under the other chain's compute; needs the second custom-AR channel
+        # (decided at the first graph capture: the engine enables the AR channels after building us)
+        self._dual: Optional[bool] = None
+        self.dual_min_batch = int(os.environ.get("PENNY_TP_DUAL_MIN_BATCH", "2"))
+        self._max_decode_ws = max(max_decode_batch, 1)
+        self.decode_ws2 = None
         self.graphs: Dict[int, _DecodeGraph] = {}
         self._static = None
         self.graph_pool = None
@@ -530,13 +537,34 @@ class ModelRunner:
         self._pin_flip = 0
         self._pinned_i32, self._pinned_f, self._pinned_l = self._pinned_sets[0]
 
+    @property
+    def dual_decode(self) -> bool:
+        if self._dual is None:
+            m = self.model
+            self._dual = bool(self.on_gpu and getattr(m, "tp_size", 1) > 1 and hasattr(m, "forward_decode_dual")
+                              and getattr(m.cfg, "arch", "") == "llama" and comm.custom_all_reduce() is not None
+                              and getattr(comm, "_CUSTOM_AR_2", None) is not None
+                              and os.environ.get("PENNY_TP_DUAL_DECODE", "1") != "0")
+            if self._dual:
+                self.decode_ws2 = DecodeWorkspace.create(self._max_decode_ws, m.hq, m.D, self.max_model_len,
+                                                         self.device)
+        return self._dual
+
     def _run_static(self, B: int) -> torch.Tensor:
         s = self._static
         self._gather_pending(s["ids"], s["src"][:B], 0)
-        meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
-                                 ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
-                                 cascade=s["cascade"])
-        h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
+        if self.dual_decode and B >= self.dual_min_batch:
+            k = B // 2                       # two chains: rows [0, k) and [k, B)
+            metas = [AttentionMetadata(slots=s["slots"][a:b], num_prefill_tokens=0, num_decode=b - a,
+                                       ctx_lens_d=s["ctx"][a:b], block_tables_d=s["bt"][a:b], decode_ws=ws)
+                     for (a, b), ws in (((0, k), self.decode_ws), ((k, B), self.decode_ws2))]
+            self.stats["dual_decode_graphs"] = self.stats.get("dual_decode_graphs", 0) + 1
+            h = self.model.forward_decode_dual(s["ids"][:B], s["pos"][:B], metas, k, self.kv)
+        else:
+            meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
+                                     ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
+                                     cascade=s["cascade"])
+            h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
         if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
             return self.model.sample_vocab_parallel(h, s["temps"][:B], s["seeds"][:B])
         if self._fused_sampling(h):

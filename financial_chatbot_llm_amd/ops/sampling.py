@@ -82,8 +82,11 @@ def lm_head_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sample one token per row of ``h`` [M, K] from softmax((h @ w.T) / T) (T <= 0: greedy) without
     materialising the logits.  Same noise as :func:`sample` (counter-based on (seed, token id)),
-    scored on the bf16-rounded logits, so for equal logits both paths pick the same token.  No
-    top-k / top-p (those rows need the whole distribution: use ``sample`` on the logits)."""
+    scored on the bf16-rounded logits, so for equal logits both paths pick the same token.  The
+    tile GEMM and hipBLASLt accumulate in different orders, though, so a row whose two best scores
+    lie within logit rounding can differ between the paths (tokens are reproducible up to logit
+    rounding; the rate is measured by tests/test_kernels_gpu.py::test_fused_vs_unfused_sampling_
+    token_agreement).  No top-k / top-p (those rows need the whole distribution: use ``sample``)."""
     M, K = h.shape
     V = w.shape[0]
     if not N.use_native(h):

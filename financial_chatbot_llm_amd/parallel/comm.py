@@ -37,6 +37,11 @@ def tp_size() -> int:
 
 
 _CUSTOM_AR = None   # CustomAllReduce for the TP group (enable_custom_all_reduce)
+# a second, independent instance (own IPC buffers, signals and counters) for the second decode
+# micro-batch chain (DecoderModel.forward_decode_dual): the two chains' all-reduces run on two
+# streams and must never share a flag round
+_CUSTOM_AR_2 = None
+_CHANNEL = 0        # which instance tp_all_reduce uses (set by ar_channel)
 
 
 def enable_custom_all_reduce(max_bytes: int = 4 << 20, buffer_bytes: int = 32 << 20):
@@ -56,19 +61,52 @@ def custom_all_reduce():
     return _CUSTOM_AR
 
 
+def enable_second_channel(max_bytes: int = 4 << 20):
+    """The second custom all-reduce instance (collective over the TP group; needs the first)."""
+    global _CUSTOM_AR_2
+    s = state()
+    if s.tp_size > 1 and _CUSTOM_AR is not None and _CUSTOM_AR_2 is None:
+        from .custom_ar import CustomAllReduce
+        _CUSTOM_AR_2 = CustomAllReduce(s.tp_group, max_bytes=max_bytes, buffer_bytes=max_bytes)
+    return _CUSTOM_AR_2
+
+
+class ar_channel:
+    """Context manager: TP all-reduces issued inside go through custom-AR instance ``k`` (0 or 1)."""
+
+    def __init__(self, k: int):
+        self.k = k
+
+    def __enter__(self):
+        global _CHANNEL
+        self.prev, _CHANNEL = _CHANNEL, self.k
+        return self
+
+    def __exit__(self, *exc):
+        global _CHANNEL
+        _CHANNEL = self.prev
+        return False
+
+
+def _ar_instance():
+    return _CUSTOM_AR_2 if _CHANNEL == 1 else _CUSTOM_AR
+
+
 def disable_custom_all_reduce() -> None:
-    global _CUSTOM_AR
-    if _CUSTOM_AR is not None:
-        _CUSTOM_AR.close()
-    _CUSTOM_AR = None
+    global _CUSTOM_AR, _CUSTOM_AR_2
+    for ar in (_CUSTOM_AR_2, _CUSTOM_AR):
+        if ar is not None:
+            ar.close()
+    _CUSTOM_AR = _CUSTOM_AR_2 = None
 
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     s = state()
     if s.tp_size == 1:
         return x
-    if _CUSTOM_AR is not None and _CUSTOM_AR.eligible(x):
-        return _CUSTOM_AR.all_reduce(x, out=x)   # reads peers' staged copies, so in-place is safe
+    ar = _ar_instance()
+    if ar is not None and ar.eligible(x):
+        return ar.all_reduce(x, out=x)           # reads peers' staged copies, so in-place is safe
     dist.all_reduce(x, group=s.tp_group)
     return x
 

@@ -6,8 +6,9 @@ north-star configurations, on reduced-depth models (2 layers):
 
 * Llama-3-70B dims at TP=8 (8192 hidden, 64 q / 8 kv heads -> 8 / 1 per rank, FFN 28672 -> 3584,
   vocab 128256 -> 16032 per rank): prefill logits (vocab-parallel LM head + all-gather) against
-  the unsharded TP=1 model, and hipGraph-captured decode whose all-reduces / logits all-gather
-  run on the custom one-/two-shot kernels at 8 ranks;
+  the unsharded TP=1 model, and hipGraph-captured decode whose all-reduces and vocab-parallel
+  sampling candidates ([B, 2] per rank) run on the custom one-/two-shot kernels at 8 ranks; the
+  fused shard LM-head sampler picks exactly the TP=1 fused sampler's tokens for the same seeds;
 * Mixtral-8x7B dims at EP=8 (one whole expert per rank, routed rows exchanged by all-to-all):
   prefill logits against the TP=1 model with all eight experts local.
 
@@ -105,6 +106,19 @@ def _worker(rank, world, port, q, kind):
             ar = comm.custom_all_reduce()
             assert ar is not None and int(ar.counter.item()) > 0
             ar.check()
+            # vocab-parallel sampling on the SAME hidden rows on every rank: the fused shard LM-head
+            # sampler (padded 16,032 -> 16,128-row shard) and the shard-logits sampler; [B, 2]
+            # candidates gathered on the custom xGMI all-gather
+            g = torch.Generator(device="cuda").manual_seed(3)
+            h = (torch.randn((37, m.cfg.hidden_size), generator=g, device="cuda") * 4).to(torch.bfloat16)
+            temps = torch.tensor([0.8] * 36 + [0.0], device="cuda")
+            seeds = torch.arange(1000, 1037, dtype=torch.int64, device="cuda")
+            os.environ["PENNY_FUSED_LM_HEAD"] = "force"
+            tok_fused = m.sample_vocab_parallel(h, temps, seeds).cpu()
+            os.environ["PENNY_FUSED_LM_HEAD"] = "0"
+            tok_shard = m.sample_vocab_parallel(h, temps, seeds).cpu()
+            os.environ.pop("PENNY_FUSED_LM_HEAD")
+            out = (out, tok_fused, tok_shard, h.cpu())
         torch.cuda.synchronize()
         q.put((rank, "OK", (logits.cpu() if rank == 0 else None, out, shard)))
         shutdown()
@@ -152,6 +166,19 @@ def test_tp8_llama3_70b_shapes_match_tp1():
     _assert_logits_close(logits8, _prefill_logits(ref_model, IDS).cpu())
     # hipGraph decode on 8 ranks: every greedy token is (within bf16 noise) the TP=1 argmax of the
     # same prefix, teacher-forced through the unsharded model
+    toks8, tok_fused, tok_shard, h = toks8
+    from financial_chatbot_llm_amd import ops
+    temps = torch.tensor([0.8] * 36 + [0.0], device="cuda")
+    seeds = torch.arange(1000, 1037, dtype=torch.int64, device="cuda")
+    hd = h.cuda()
+    os.environ["PENNY_FUSED_LM_HEAD"] = "force"
+    want_fused = ops.lm_head_sample(hd, ref_model.lm_weight(), temps, seeds).cpu()
+    os.environ.pop("PENNY_FUSED_LM_HEAD")
+    # fused on both sides: identical per-element logits -> the TP=8 vocab-parallel sample IS the TP=1 one
+    assert torch.equal(tok_fused, want_fused), (tok_fused, want_fused)
+    # shard logits (hipBLASLt at N = 16,032 vs 128,256): equal up to logit rounding
+    want = ops.sample(ref_model.logits(hd), temps, seeds).cpu()
+    assert int((tok_shard == want).sum()) >= 35, (tok_shard, want)
     for prompt, toks in zip([IDS[:96], IDS[40:150]], toks8):
         for j, t in enumerate(toks):
             lg = _prefill_logits(ref_model, prompt + toks[:j])[-1].cpu()
