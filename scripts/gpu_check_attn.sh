@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU session: prefill-attention variants (numerics + timing), sampling tests, world-8 TP rehearsal.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -u
+mkdir -p gpurun_out
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] $name" | tee -a gpurun_out/session.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -4 "gpurun_out/$name.log"
+  return $rc
+}
+step t_attn 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
+     -k "prefill_attention or fused_lm_head or sampler or agreement or production" || exit 1
+step b_attn 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed || exit 1
+step t_world8 700 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_world8_gpu.py -k tp8 || exit 1

@@ -641,6 +641,44 @@ def test_prefill_gemm_bf16(M, N_, K):
     assert y.shape == (M, N_) and y.dtype == torch.bfloat16
 
 
+@pytest.mark.parametrize("M,epi", [(300, None), (2304, "residual"), (700, "slabs4")])
+def test_prefill_gemm_production_down_shape_vs_fp32(M, epi):
+    """The real Llama-3-8B down projection (N = 4096, K = 14336: 224 K-tiles, the tail split path at
+    M = 300 and 700, a whole-tile round at 2304) against an fp32 reference computed on the GPU."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator(device=DEV).manual_seed(M)
+    x = torch.randn((M, 14336), generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((4096, 14336), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    if epi == "slabs4":
+        P = gemm.prefill_gemm(x, w, "slabs", 4)
+        close(P.sum(0), ref, atol=1e-3 * ref.abs().max().item(), rtol=1e-3)
+        return
+    if epi == "residual":
+        r = torch.randn((M, 4096), generator=g, device=DEV).to(torch.bfloat16)
+        y = gemm.prefill_gemm(x, w, "residual", residual=r)
+        ref = ref + r.float()
+    else:
+        y = gemm.prefill_gemm(x, w)
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M", [300, 2304])
+def test_prefill_gemm_production_gate_up_silu_vs_fp32(M):
+    """The real gate|up + SiLU (N = 2 x 14336 = 28672 interleaved rows, K = 4096) against fp32."""
+    from financial_chatbot_llm_amd.ops import gemm
+    from financial_chatbot_llm_amd.ops.activation import silu_mul
+    g = torch.Generator(device=DEV).manual_seed(M + 1)
+    x = torch.randn((M, 4096), generator=g, device=DEV).to(torch.bfloat16)
+    gate = (torch.randn((14336, 4096), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    up = (torch.randn((14336, 4096), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    w = gemm.interleave16(gate, up).contiguous()
+    y = gemm.prefill_gemm(x, w, "silu")
+    gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
+    ref = torch.nn.functional.silu(gf) * uf
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+
+
 @pytest.mark.parametrize("M,S", [(37, 2), (600, 4), (513, 8)])
 def test_prefill_gemm_split_k_slabs(M, S):
     from financial_chatbot_llm_amd.ops import gemm
