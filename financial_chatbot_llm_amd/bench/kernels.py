@@ -262,12 +262,21 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         o = torch.empty_like(q)
         wl = ops.attention.prefill_work_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv)
         wd = torch.from_numpy(wl).to(dev) if wl is not None else None
+        ln = ops.attention.prefill_lean_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv)
+        ld = torch.from_numpy(ln).to(dev) if ln is not None else None
+        lc = (int(ln[0, 1]), int(ln[0, 2]), int(ln[0, 3])) if ln is not None else None
+
         def run(v):
             def f():
+                if v == "lean":
+                    ops.attention.prefill_variant(1)
+                    ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
+                                work=ld if ld is not None else wd, lean=lc)
+                    return
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2": 0, "pp": 1, "pp_valu": 2, "pp_prio": 3}
+        variants = {"pf2": 0, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():
@@ -277,7 +286,8 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         ops.attention.prefill_variant(old)
         keys = sum(ql * (c - ql) + ql * (ql + 1) / 2 for ql, c in shape)
         flops = 4 * keys * Hq * D
-        row = {"op": "prefill_attn_mixed", "step": name, "T": T}
+        row = {"op": "prefill_attn_mixed", "step": name, "T": T,
+               "lean_items": int(ln[0, 1]) if ln is not None else 0, "lean_splits": int(ln[0, 2]) if ln is not None else 0}
         for k in variants:
             row[f"{k}_us"] = round(ts[k], 1)
             row[f"{k}_TFLOPs"] = round(flops / ts[k] / 1e6, 1)

@@ -1076,12 +1076,21 @@ __device__ __forceinline__ void pp_pv(const uint4* __restrict__ vl, Frag (&vf)[D
 
 __device__ __forceinline__ void lgkm0_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Lean (KV-split) prefill work: a tile's KV walk can be cut into chunks run by different
+// workgroups; a chunk writes flash-decoding partial state (unnormalised O, running max m, row sum
+// l) to slot `slot`, and prefill_merge_kernel combines a tile's slots in chunk order.
+struct PrefillLean {
+  const int* items;     // [n, 6]: sequence, tile, first block, end block, slot (< 0: whole tile), 0
+  float* part_o;        // [slots, Hkv, 256 rows, D] f32
+  float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
+};
+
 template <int D, bool HEAD_FAST, bool LSUM, bool PRIO, bool VPRE = false>
 __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
-    float* __restrict__ lse, const int* __restrict__ work) {
+    float* __restrict__ lse, const int* __restrict__ work, PrefillLean lean) {
   constexpr int NW = 8, NBUF = 3;
   constexpr int KC = D / 32, DT = D / 16;
   constexpr int TILE = KV_BS * D * 2;
@@ -1091,9 +1100,10 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
 
   const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
-  const int s = work ? work[2 * item] : blockIdx.z;
+  const int* li = lean.items ? lean.items + 6 * item : nullptr;
+  const int s = li ? li[0] : (work ? work[2 * item] : blockIdx.z);
   const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
-  const int tile = work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item;
+  const int tile = li ? li[1] : (work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item);
   const int G = Hq / Hkv;
   const int TQ = NW * 32 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
@@ -1107,10 +1117,15 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
 
   const int last_tok = min(tok0 + TQ, qlen) - 1;
   const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
-  const int nblk = (kv_end + KV_BS - 1) / KV_BS;
-  const int* bt = block_tables + (long)s * max_blocks;
+  const int nblk_tile = (kv_end + KV_BS - 1) / KV_BS;
+  // this workgroup's KV blocks [jb, jb + nblk) of the tile (lean: one chunk of its walk)
+  const int jb = li ? li[2] : 0;
+  const int nblk = li ? min(li[3], nblk_tile) - jb : nblk_tile;
+  const int slot = li ? li[4] : -1;
+  PENNY_DASSERT(nblk >= 1);
+  const int* bt = block_tables + (long)s * max_blocks + jb;
 
-  auto stage = [&](int j) {
+  auto stage = [&](int j) {                   // j: local block index (buffer j % NBUF)
     const long phys = bt[j];
     PENNY_DASSERT(phys >= 0);
     const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
@@ -1161,11 +1176,12 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   const bool wave_live = wave_tok0 < qlen;
   const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
   const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
-  auto act = [&](int j) { return wave_live && j * KV_BS < wave_kv_end; };
-  auto qks = [&](int j) {
+  auto act = [&](int j) { return wave_live && (jb + j) * KV_BS < wave_kv_end; };
+  auto qks = [&](int j) {                     // local block j = absolute block jb + j
+    const int ja = jb + j;
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
-    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    pp_qks<D, LSUM, VPRE>(kl, kl + TILE / 16, qf, vf, o, m, l, lacc, pf, causal, j, ctx, qpos, scale_log2, lane, g,
+    const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
+    pp_qks<D, LSUM, VPRE>(kl, kl + TILE / 16, qf, vf, o, m, l, lacc, pf, causal, ja, ctx, qpos, scale_log2, lane, g,
                           __builtin_amdgcn_readfirstlane((int)!full) != 0);
   };
 
@@ -1196,6 +1212,16 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     float lt;
     if constexpr (LSUM) lt = lacc[ct][0];     // every output row of the ones-MFMA holds the full sum
     else lt = rowgroup_sum(l[ct]);
+    if (slot >= 0) {                          // a chunk of a split walk: partial state for the merge
+      const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = o[ct][dt];
+      if (g == 0) {
+        lean.part_ml[2 * pr] = m[ct];
+        lean.part_ml[2 * pr + 1] = lt;
+      }
+      continue;
+    }
     if (tok[ct] >= qlen) continue;
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
@@ -1209,6 +1235,80 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     if (lse != nullptr && g == 0)
       lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
   }
+}
+
+// Merge the chunk partials of split tiles (lean prefill): grid (splits, Hkv), 256 threads; wave
+// rows: lanes 0-31 / 32-63 take two rows, 4 dims per lane (f32x4), so every load is coalesced.
+// merge [n, 6]: sequence, tile, first slot, number of slots, 0, 0 (chunk order = slot order).
+template <int D>
+__global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restrict__ merge, const int* __restrict__ cu_q,
+                                                            const float* __restrict__ part_o,
+                                                            const float* __restrict__ part_ml, bf16* __restrict__ out,
+                                                            float* __restrict__ lse, int Hq, int Hkv) {
+  static_assert(D == 128 || D == 64, "head dim");
+  constexpr int LPR = D / 4;                  // lanes per row
+  constexpr int RPW = 64 / LPR;               // rows per wave instruction
+  const int* mg = merge + 6 * blockIdx.x;
+  const int s = mg[0], tile = mg[1], slot0 = mg[2], np = mg[3];
+  const int h = blockIdx.y, G = Hq / Hkv, TQ = 256 / G;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sub = lane / LPR, d = (lane % LPR) * 4;
+  for (int r = w * RPW + sub; r < 256; r += 4 * RPW) {
+    const int tok = tile * TQ + r / G;
+    if (tok >= qlen) continue;
+    float M = -INFINITY;
+    for (int i = 0; i < np; ++i) M = fmaxf(M, part_ml[2 * (((long)(slot0 + i) * Hkv + h) * 256 + r)]);
+    float L = 0.f;
+    f32x4 O = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < np; ++i) {
+      const long pr = ((long)(slot0 + i) * Hkv + h) * 256 + r;
+      const float mi = part_ml[2 * pr];
+      const float f = mi == -INFINITY ? 0.f : exp2f(mi - M);
+      L += part_ml[2 * pr + 1] * f;
+      O += *reinterpret_cast<const f32x4*>(part_o + pr * D + d) * f;
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const int head = h * G + r % G;
+    bf16x4 v4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v4[k] = (bf16)(O[k] * inv);
+    *reinterpret_cast<bf16x4*>(out + ((long)(q0 + tok) * Hq + head) * D + d) = v4;
+    if (lse != nullptr && d == 0)
+      lse[(long)(q0 + tok) * Hq + head] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
+  }
+}
+
+// Lean big-tile prefill: items [nitems, 6] (see PrefillLean; LPT order), merge [nmerge, 6];
+// part_o / part_ml sized for the slots the items use.  Ping-pong kernel (variant 1) only.
+PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
+                                           const void* k_cache, const void* v_cache, void* out, int Hq, int Hkv,
+                                           int D, int max_blocks, float scale, int causal, float* lse,
+                                           const int* items, int nitems, const int* merge, int nmerge,
+                                           float* part_o, float* part_ml, hipStream_t stream) {
+  if (nitems <= 0) return 0;
+  if (Hq % Hkv || (256 % (Hq / Hkv)) || !items || (nmerge > 0 && (!merge || !part_o || !part_ml)))
+    return (int)hipErrorInvalidValue;
+  const float sl2 = scale * LOG2E;
+  const PrefillLean lean{items, part_o, part_ml};
+  if (D == 128) {
+    hipLaunchKernelGGL((prefill3_kernel<128, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
+    if (nmerge > 0)
+      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+                         part_ml, (bf16*)out, lse, Hq, Hkv);
+  } else if (D == 64) {
+    hipLaunchKernelGGL((prefill3_kernel<64, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
+    if (nmerge > 0)
+      hipLaunchKernelGGL(prefill_merge_kernel<64>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+                         part_ml, (bf16*)out, lse, Hq, Hkv);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  PENNY_RETURN_LAUNCH();
 }
 
 // Big-tile prefill variant: 1 (default) ping-pong prefill3 with ones-MFMA row sums, 2 ping-pong
@@ -1260,15 +1360,15 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   if (big && head_fast && pp_env == 1)                                                                                      \
     hipLaunchKernelGGL((prefill3_kernel<DD, true, true, false>), grid2, dim3(512), 0, stream,                    \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
   else if (big && head_fast && pp_env == 2)                                                                                 \
     hipLaunchKernelGGL((prefill3_kernel<DD, true, false, false>), grid2, dim3(512), 0, stream,                   \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
   else if (big && head_fast && pp_env == 3)                                                                                 \
     hipLaunchKernelGGL((prefill3_kernel<DD, true, true, true>), grid2, dim3(512), 0, stream,                     \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
   else if (big && head_fast)                                                                                     \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), grid2, dim3(512), 0, stream,                           \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \

@@ -21,7 +21,7 @@ import torch
 
 from .. import ops
 from ..models.common import AttentionMetadata, KVCache
-from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade, prefill_work_list
+from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade, prefill_plan
 from ..parallel import comm
 from ..utils.logging import get_logger
 from ..utils.profiling import marker
@@ -50,7 +50,7 @@ class StepInputs:
     top_k: np.ndarray               # [S]
     top_p: np.ndarray               # [S]
     src: Optional[np.ndarray] = None  # [Bd] row of the previous step's sampled vector (-1: ids[] is real)
-    pwork: Optional[np.ndarray] = None  # [n, 2] prefill attention work list (filled by the runner)
+    pwork: Optional[np.ndarray] = None  # prefill attention work list (filled by the runner): [n, 2] or lean [., 6]
 
     @property
     def num_prefill_tokens(self) -> int:
@@ -328,8 +328,10 @@ class ModelRunner:
             m.block_tables_p = self._to_dev(si.bt_p)
             m.max_q_len = si.max_q_len
             if self.on_gpu:   # LPT-ordered prefill attention tiles (staged with the step when precomputed)
-                work = si.pwork if si.pwork is not None else prefill_work_list(si.cu_q, si.ctx_p, self.G)
+                work = si.pwork if si.pwork is not None else prefill_plan(si.cu_q, si.ctx_p, self.G, self.model.hkv)
                 m.prefill_work = self._to_dev(work) if work is not None else None
+                if work is not None and work.shape[1] == 6:        # lean split-KV list: its counts
+                    m.prefill_lean = (int(work[0, 1]), int(work[0, 2]), int(work[0, 3]))
         if si.num_decode:
             m.ctx_lens_d = self._to_dev(si.ctx_d)
             m.block_tables_d = self._to_dev(si.bt_d)
@@ -475,7 +477,7 @@ class ModelRunner:
         else:
             with marker(f"forward.eager[{len(si.ids)}]"):
                 if si.num_prefill_tokens and si.pwork is None and self.on_gpu:
-                    si.pwork = prefill_work_list(si.cu_q, si.ctx_p, self.G)
+                    si.pwork = prefill_plan(si.cu_q, si.ctx_p, self.G, self.model.hkv)
                 self._stage_inputs(si)
                 try:
                     out = self.logits_and_sample(si)

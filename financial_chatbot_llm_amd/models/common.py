@@ -27,7 +27,8 @@ class AttentionMetadata:
     decode_ws: Optional[DecodeWorkspace] = None
     cascade: Optional[CascadeInputs] = None     # shared-prefix groups of the decode rows
     causal: bool = True
-    prefill_work: Optional[torch.Tensor] = None  # [n, 2] int32 (ops.attention.prefill_work_list)
+    prefill_work: Optional[torch.Tensor] = None  # [n, 2] int32 (ops.attention.prefill_work_list) or lean [., 6]
+    prefill_lean: Optional[tuple] = None          # lean list counts (items, merges, slots), host ints
 
 
 class KVCache:

@@ -221,7 +221,8 @@ class DecoderModel:
                            workspace=meta.decode_ws, out=attn[tp:])
         if tp > 0:
             ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, self.scale,
-                        causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp], work=meta.prefill_work)
+                        causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp], work=meta.prefill_work,
+                        lean=meta.prefill_lean)
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)
         elif meta.num_decode > 0:

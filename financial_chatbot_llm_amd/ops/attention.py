@@ -15,7 +15,7 @@ import math
 import os
 from dataclasses import dataclass
 from functools import lru_cache
-from typing import Optional
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -204,6 +204,83 @@ def prefill_work_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, causal: bo
     return np.stack([np.asarray(seqs, np.int32)[order], np.asarray(tiles, np.int32)[order]], 1)
 
 
+# Lean (KV-split) big-tile prefill: tiles whose KV walk is longer than the step's balanced per-CU
+# share are cut into chunks run by different workgroups, each writing flash-decoding partial state
+# that ``prefill_merge_kernel`` combines in chunk order (bitwise repeatable).  A step of short
+# decide / speculative chunks behind 4-5k cached tokens then no longer waits on its longest walks:
+# LPT over chunks instead of whole tiles.  PENNY_PREFILL_LEAN=0 keeps whole tiles.
+PREFILL_LEAN = os.environ.get("PENNY_PREFILL_LEAN", "1") != "0"
+LEAN_MIN_CHUNK = 8          # KV blocks: below that a chunk's partial write + merge outweigh the balance
+
+
+def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causal: bool = True,
+                      cus: int = 256, min_chunk: int = LEAN_MIN_CHUNK) -> Optional[np.ndarray]:
+    """Lean work list of one step, or None when no tile needs splitting: int32 [1 + n + m, 6] =
+    header (-1, n items, m merges, slots, 0, 0), n items (sequence, tile, first block, end block,
+    slot or -1, 0) longest first, m merges (sequence, tile, first slot, slots, 0, 0)."""
+    if not PREFILL_LEAN or G <= 0 or 256 % G:
+        return None
+    cu = np.asarray(cu_q, np.int64)
+    ql = cu[1:] - cu[:-1]
+    if len(ql) == 0 or int(ql.max()) * G <= 128:
+        return None
+    ctx = np.asarray(ctx_lens, np.int64)
+    TQ = 256 // G
+    tiles = []
+    for s_, (n, c) in enumerate(zip(ql.tolist(), ctx.tolist())):
+        for t in range((n + TQ - 1) // TQ):
+            last = min((t + 1) * TQ, n) - 1
+            kv_end = min(c, c - n + last + 1) if causal else c
+            tiles.append((s_, t, (kv_end + KV_BS - 1) // KV_BS))
+    total = sum(nb for _, _, nb in tiles)
+    C = max(min_chunk, -(-total * Hkv // max(cus, 1)))       # balanced per-CU share of block units
+    if max(nb for _, _, nb in tiles) <= C:
+        return None
+    items, merges, slot = [], [], 0
+    for s_, t, nb in tiles:
+        if nb <= C:
+            items.append((s_, t, 0, nb, -1, 0))
+            continue
+        k = -(-nb // C)
+        cuts = [round(i * nb / k) for i in range(k + 1)]
+        merges.append((s_, t, slot, k, 0, 0))
+        items += [(s_, t, cuts[i], cuts[i + 1], slot + i, 0) for i in range(k)]
+        slot += k
+    items.sort(key=lambda r: -(r[3] - r[2]))                  # LPT over chunks
+    out = np.zeros((1 + len(items) + len(merges), 6), np.int32)
+    out[0, :4] = (-1, len(items), len(merges), slot)
+    out[1:1 + len(items)] = np.asarray(items, np.int32)
+    if merges:
+        out[1 + len(items):] = np.asarray(merges, np.int32)
+    return out
+
+
+def prefill_plan(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causal: bool = True,
+                 cus: int = 256) -> Optional[np.ndarray]:
+    """The step's prefill-attention work list: lean ([., 6], when the ping-pong kernel is selected
+    and some walk needs splitting) or whole tiles in LPT order ([n, 2])."""
+    if PREFILL_LEAN and prefill_variant() == 1:
+        lean = prefill_lean_list(cu_q, ctx_lens, G, Hkv, causal, cus)
+        if lean is not None:
+            return lean
+    return prefill_work_list(cu_q, ctx_lens, G, causal)
+
+
+_LEAN_WS: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def _lean_workspace(dev: torch.device, slots: int, Hkv: int, D: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    key = torch.device(dev).index
+    ws = _LEAN_WS.get(key)
+    need_o, need_ml = slots * Hkv * 256 * D, slots * Hkv * 256 * 2
+    if ws is None or ws[0].numel() < need_o or ws[1].numel() < need_ml:
+        grow = max(slots, 64)
+        ws = (torch.empty(grow * Hkv * 256 * D, dtype=torch.float32, device=dev),
+              torch.empty(grow * Hkv * 256 * 2, dtype=torch.float32, device=dev))
+        _LEAN_WS[key] = ws
+    return ws
+
+
 def prefill_variant(v: int = -1) -> int:
     """Select the big-tile prefill kernel for this process (returns the previous choice; -1 only
     reads it): 1 = ping-pong prefill3 with ones-MFMA row sums (default), 2 = ping-pong with VALU
@@ -215,18 +292,29 @@ def prefill_variant(v: int = -1) -> int:
 def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor,
             k_cache: torch.Tensor, v_cache: torch.Tensor, scale: float, causal: bool = True,
             max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None,
-            lse: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None) -> torch.Tensor:
+            lse: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
+            lean: Optional[Tuple[int, int, int]] = None) -> torch.Tensor:
     """Varlen paged attention for the new tokens of S sequences (chunked prefill / prefix hits:
     query i of sequence s sits at absolute position ctx_lens[s] - q_len[s] + i).  ``lse`` [T, Hq]
     f32 (optional) receives each row's natural-log sum-exp of the scaled scores (-inf: no key
     visible) -- what a ring-attention merge needs.  ``work``: :func:`prefill_work_list` of the same
-    step on the device (optional; LPT tile order)."""
+    step on the device (optional; LPT tile order), or :func:`prefill_lean_list`'s split-KV list
+    (``lean`` = its (items, merges, slots) counts, read from the header when not given)."""
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     S = block_tables.shape[0]
     assert k_cache.shape[-1] == KV_BS * D
     if N.use_native(q):
         out = torch.empty_like(q) if out is None else out
+        if work is not None and work.dim() == 2 and work.shape[1] == 6:
+            # lean work list (prefill_lean_list): the counts ride along host-side as ``lean``
+            ni, nm, nslots = lean if lean is not None else (int(work[0, 1]), int(work[0, 2]), int(work[0, 3]))
+            po, pml = _lean_workspace(q.device, max(nslots, 1), Hkv, D)
+            N.call("penny_attention_prefill_lean", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),
+                   N.ptr(k_cache), N.ptr(v_cache), N.ptr(out), Hq, Hkv, D, block_tables.shape[1], float(scale),
+                   int(causal), N.ptr(lse) if lse is not None else None, N.ptr(work[1:]), int(ni),
+                   N.ptr(work[1 + ni:]) if nm else None, int(nm), N.ptr(po), N.ptr(pml), N.stream())
+            return out
         if max_q_len is None:
             max_q_len = int((cu_q[1:] - cu_q[:-1]).max().item())
         N.call("penny_attention_prefill", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),

@@ -165,6 +165,37 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
         ops.attention.prefill_variant(old)
 
 
+@pytest.mark.parametrize("min_chunk", [1, 3, 8])
+@pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
+    (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
+    (8, 1, 128, True, [(40, 1500), (33, 500)]),
+    (12, 12, 64, False, [(200, 700), (33, 33)]),
+])
+def test_prefill_attention_lean_split_kv(min_chunk, Hq, Hkv, D, causal, lens):
+    """Lean prefill: the KV walks of long tiles cut into chunks on different workgroups, partial
+    (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse)."""
+    g = torch.Generator().manual_seed(50 + min_chunk)
+    qlens = [a for a, _ in lens]
+    ctx = [b for _, b in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    q = rnd(int(cu[-1]), Hq, D, gen=g)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, causal)
+    lse_ref = torch.empty(q.shape[0], Hq)
+    ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, causal, lse=lse_ref)
+    wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, causal, cus=100000,
+                                         min_chunk=min_chunk)
+    assert wl is not None and int(wl[0, 2]) > 0                 # some tiles were split
+    lse = torch.empty(q.shape[0], Hq, device=DEV)
+    out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, causal,
+                      max_q_len=max(qlens), lse=lse, work=torch.from_numpy(wl).to(DEV),
+                      lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])))
+    close(out, ref, atol=2e-2)
+    close(lse, lse_ref, atol=2e-2, rtol=1e-3)
+
+
 @pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
                                          # B >= 96 / >= 192: longer partitions (pb 16 / 32)
                                          (32, 8, [(37 * i) % 3000 + 1 for i in range(100)]),
