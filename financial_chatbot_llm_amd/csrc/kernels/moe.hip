@@ -76,6 +76,113 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
+// 1b. prefill routing + activation quantisation (any T): two launches instead of the torch
+//     softmax / top-k / renormalise / argsort / bincount / cumsum / gather chain plus quant_rows.
+//   moe_route_quant: one workgroup per token. Wave 0 routes it (one expert per lane: f32 softmax
+//     numerators, K rounds of wave arg-max -- ties to the smaller expert id -- renormalised over the
+//     top K, as moe_route_kernel); all four waves quantise the token's hidden row to e4m3 with the
+//     row held in registers between the amax and the convert sweeps (read from HBM once).
+//   moe_bucket: one workgroup counts the T*K pairs per expert in LDS, scans the offsets and
+//     scatters the pairs into their buckets (order inside a bucket is irrelevant -- rows are
+//     computed independently -- so the result is deterministic per row).
+// ---------------------------------------------------------------------------------------------
+template <int CPT>
+__global__ void __launch_bounds__(256) moe_route_quant_kernel(const bf16* __restrict__ x, int ldx, int H,
+                                                              const bf16* __restrict__ logits, int E, int K,
+                                                              unsigned char* __restrict__ q, float* __restrict__ scale,
+                                                              int* __restrict__ pe, float* __restrict__ pw) {
+  __shared__ float red[4];
+  const long t = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    float l = lane < E ? (float)logits[t * E + lane] : -INFINITY;
+    float mx = l;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float p = lane < E ? __expf(l - mx) : -1.f;
+    float ws = 0.f, mine = 0.f;
+    int myj = -1;
+    for (int j = 0; j < K; ++j) {
+      float bv = p;
+      int bi = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      ws += bv;
+      if (lane == bi) { mine = p; myj = j; p = -1.f; }
+    }
+    if (myj >= 0) {
+      pe[t * K + myj] = lane;
+      pw[t * K + myj] = mine / ws;
+    }
+  }
+  const uint4* xr = reinterpret_cast<const uint4*>(x + t * ldx);
+  const int nchunk = H >> 3;
+  float a[CPT][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nchunk) {
+      unpack8(xr[c], a[i]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(a[i][k]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if (lane == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = amax > 0.f ? amax / FP8_MAX : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) scale[t] = sc;
+  uint2* qr = reinterpret_cast<uint2*>(q + t * (long)H);
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nchunk) {
+      uint32_t w0 = 0, w1 = 0;
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][0] * inv, a[i][1] * inv, w0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][2] * inv, a[i][3] * inv, w0, true);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][4] * inv, a[i][5] * inv, w1, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(a[i][6] * inv, a[i][7] * inv, w1, true);
+      qr[c] = make_uint2(w0, w1);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024) moe_bucket_kernel(const int* __restrict__ pe, const float* __restrict__ pw,
+                                                          int P, int E, int K, int* __restrict__ sorted_tok,
+                                                          float* __restrict__ sorted_w, int* __restrict__ offsets,
+                                                          int* __restrict__ inv) {
+  __shared__ int cnt[64], cur[64];
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < P; i += blockDim.x) atomicAdd(&cnt[pe[i]], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      offsets[e] = acc;
+      cur[e] = acc;
+      acc += cnt[e];
+    }
+    offsets[E] = acc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const int pos = atomicAdd(&cur[pe[i]], 1);
+    inv[i] = pos;
+    sorted_tok[pos] = i / K;
+    sorted_w[pos] = pw[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 2. dynamic per-row fp8 quantisation (one workgroup per row; row length multiple of 8)
 // ---------------------------------------------------------------------------------------------
 __global__ void quant_rows_kernel(const bf16* __restrict__ x, int ld, int n, unsigned char* __restrict__ q,
@@ -305,6 +412,29 @@ PENNY_API int penny_moe_route(const void* logits, int T, int E, int K, int* sort
   if (E > 64 || K > 8 || K > E || T * K > MOE_ROUTE_CAP) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(1024), 0, stream, (const bf16*)logits, T, E, K, sorted_tok,
                      sorted_w, offsets, inv);
+  PENNY_RETURN_LAUNCH();
+}
+
+// prefill routing + quantisation: x [T, H] (row stride ldx) bf16, logits [T, E] bf16 ->
+// xq [T, H] e4m3, xs [T]; pair expert / weight scratch pe, pw [T*K]; buckets sorted_tok /
+// sorted_w [T*K], offsets [E+1], inverse map inv [T*K] (pair t*K+j -> sorted position)
+PENNY_API int penny_moe_route_quant(const void* x, int ldx, const void* logits, int T, int H, int E, int K, void* xq,
+                                    float* xs, int* pe, float* pw, int* sorted_tok, float* sorted_w, int* offsets,
+                                    int* inv, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (E > 64 || K < 1 || K > 8 || K > E || H % 8 || ldx % 8) return (int)hipErrorInvalidValue;
+  const int cpt = (H / 8 + 255) / 256;
+#define RQ_CASE(C)                                                                                        \
+  if (cpt <= C) {                                                                                         \
+    hipLaunchKernelGGL(moe_route_quant_kernel<C>, dim3(T), dim3(256), 0, stream, (const bf16*)x, ldx, H, \
+                       (const bf16*)logits, E, K, (unsigned char*)xq, xs, pe, pw);                       \
+  } else
+  RQ_CASE(1) RQ_CASE(2) RQ_CASE(4) RQ_CASE(8) return (int)hipErrorInvalidValue;
+#undef RQ_CASE
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return (int)err;
+  hipLaunchKernelGGL(moe_bucket_kernel, dim3(1), dim3(1024), 0, stream, pe, pw, T * K, E, K, sorted_tok, sorted_w,
+                     offsets, inv);
   PENNY_RETURN_LAUNCH();
 }
 

@@ -58,6 +58,7 @@ _SIGS = {
     "penny_sample_shard": [P, c_int, c_long, P, P, P, P, c_int, c_int, c_int, P],
     "penny_topk_topp_threshold": [P, c_int, c_long, P, P, P, P, c_int, c_int, P],
     "penny_moe_route": [P, c_int, c_int, c_int, P, P, P, P, P],
+    "penny_moe_route_quant": [P, c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P],
     "penny_quant_rows_fp8": [P, c_int, c_int, c_int, P, P, P],
     "penny_silu_quant_rows_fp8": [P, c_int, c_int, P, P, P],
     "penny_moe_gemm_fp8": [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],

@@ -62,6 +62,48 @@ def route_device(topi: torch.Tensor, topw: torch.Tensor, num_experts: int):
     return offsets, tok_idx, tok_w, inv.to(torch.int32)
 
 
+# prefill routing + hidden-row quantisation in two HIP launches (penny_moe_route_quant);
+# PENNY_MOE_FUSED_ROUTE=0: torch top-k + route_device + quant_rows
+FUSED_ROUTE = os.environ.get("PENNY_MOE_FUSED_ROUTE", "1") != "0"
+
+
+def route_quant_device(h: torch.Tensor, router_logits: torch.Tensor, top_k: int, num_experts: int):
+    """Route the T tokens and quantise their hidden rows on the device: -> (xq [T, H] e4m3 bytes,
+    xs [T] f32 row scales, offsets [E+1] i32, tok_idx [T*k] i32, tok_w [T*k] f32, inv [T*k] i32),
+    the outputs of :func:`topk_softmax` + :func:`route_device` + ``quant_rows`` (bucket order
+    inside an expert may differ; every row is computed independently)."""
+    from . import _native as N
+    T, H = h.shape
+    dev = h.device
+    P = T * top_k
+    lg = router_logits if router_logits.dtype == torch.bfloat16 else router_logits.to(torch.bfloat16)
+    lg = lg.contiguous()
+    xq = torch.empty((T, H), dtype=torch.uint8, device=dev)
+    xs = torch.empty(T, dtype=torch.float32, device=dev)
+    scratch = torch.empty(2 * P, dtype=torch.int32, device=dev)
+    tok_idx = torch.empty(P, dtype=torch.int32, device=dev)
+    tok_w = torch.empty(P, dtype=torch.float32, device=dev)
+    offsets = torch.empty(num_experts + 1, dtype=torch.int32, device=dev)
+    inv = torch.empty(P, dtype=torch.int32, device=dev)
+    N.call("penny_moe_route_quant", N.ptr(h), h.stride(0), N.ptr(lg), T, H, num_experts, top_k, N.ptr(xq), N.ptr(xs),
+           N.ptr(scratch), N.ptr(scratch[P:]), N.ptr(tok_idx), N.ptr(tok_w), N.ptr(offsets), N.ptr(inv), N.stream())
+    return xq, xs, offsets, tok_idx, tok_w, inv
+
+
+def _route_and_quant(h, router_logits, top_k, E):
+    """Fused device routing + quantisation, or the unfused torch chain (PENNY_MOE_FUSED_ROUTE=0)."""
+    from . import _native as N
+    if FUSED_ROUTE and h.stride(1) == 1 and h.stride(0) % 8 == 0:
+        return route_quant_device(h, router_logits, top_k, E)
+    T, H = h.shape
+    topw, topi = topk_softmax(router_logits, top_k)
+    offsets, tok_idx, tok_w, inv = route_device(topi, topw, E)
+    xq = torch.empty((T, H), dtype=torch.uint8, device=h.device)
+    xs = torch.empty(T, dtype=torch.float32, device=h.device)
+    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(xq), N.ptr(xs), N.stream())
+    return xq, xs, offsets, tok_idx, tok_w, inv
+
+
 def moe_prefill_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Tensor, s13: torch.Tensor,
                     w2t: torch.Tensor, s2: torch.Tensor, top_k: int) -> torch.Tensor:
     """Prefill-size fp8 MoE entirely on the device, no host sync: torch top-k routing +
@@ -72,12 +114,8 @@ def moe_prefill_fp8(h: torch.Tensor, router_logits: torch.Tensor, w13t: torch.Te
     E, F2 = s13.shape
     F_ = F2 // 2
     P = T * top_k
-    topw, topi = topk_softmax(router_logits, top_k)
-    offsets, tok_idx, tok_w, inv = route_device(topi, topw, E)
+    xq, xs, offsets, tok_idx, tok_w, inv = _route_and_quant(h, router_logits, top_k, E)
     st = N.stream()
-    xq = torch.empty((T, H), dtype=torch.uint8, device=h.device)
-    xs = torch.empty(T, dtype=torch.float32, device=h.device)
-    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(xq), N.ptr(xs), st)
     a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
     ntf13, ntf2 = MOE_NTF
     N.call("penny_moe_gemm_fp8", N.ptr(xq), N.ptr(xs), N.ptr(tok_idx), N.ptr(offsets), N.ptr(w13t), N.ptr(s13), None,
@@ -106,12 +144,8 @@ def moe_prefill_fp8_tiles(h: torch.Tensor, router_logits: torch.Tensor, w13q: to
     E, F2 = s13.shape
     F_ = F2 // 2
     P = T * top_k
-    topw, topi = topk_softmax(router_logits, top_k)
-    offsets, tok_idx, tok_w, inv = route_device(topi, topw, E)
+    xq, xs, offsets, tok_idx, tok_w, inv = _route_and_quant(h, router_logits, top_k, E)
     st = N.stream()
-    xq = torch.empty((T, H), dtype=torch.uint8, device=h.device)
-    xs = torch.empty(T, dtype=torch.float32, device=h.device)
-    N.call("penny_quant_rows_fp8", N.ptr(h), h.stride(0), T, H, N.ptr(xq), N.ptr(xs), st)
     a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
            N.ptr(s13), None, N.ptr(a), F_, P, E, F2, H, 7, st)

@@ -13,6 +13,6 @@ step() {  # name, timeout, command...
   return $rc
 }
 step t_attn 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
-     -k "prefill_attention or fused_lm_head or sampler or agreement or production" || exit 1
+     -k "prefill_attention or fused_lm_head or sampler or agreement or production or route_quant or moe_prefill" || exit 1
 step b_attn 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed || exit 1
 step t_world8 700 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_world8_gpu.py -k tp8 || exit 1

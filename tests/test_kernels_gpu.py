@@ -630,6 +630,36 @@ def test_moe_prefill_fp8_device_pipeline(T):
     assert err.mean() < 0.01 * ref.float().abs().mean() + 1e-4, (err.mean(), ref.abs().mean())
 
 
+@pytest.mark.parametrize("T,E,K,H", [(1, 8, 2, 512), (3000, 8, 2, 4096), (517, 64, 6, 2048), (64, 16, 4, 6144)])
+def test_moe_route_quant_matches_torch_chain(T, E, K, H):
+    """penny_moe_route_quant (route + quantise in 2 launches) == topk_softmax + route_device +
+    quant_rows: identical fp8 rows and scales, expert offsets, and the same (token, weight) pairs in
+    each expert bucket; the inverse map points every (token, j) at a slot holding that token."""
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(31)
+    h = rnd(T, H, gen=g).to(DEV)
+    # distinct logits per row (a bf16 tie would leave the top-k choice to each implementation)
+    perm = torch.stack([torch.randperm(E, generator=g) for _ in range(T)]).float()
+    logits = ((perm - E / 2) * 0.1).to(torch.bfloat16).to(DEV)
+    xq, xs, off, tok, tw, inv = moe.route_quant_device(h, logits, K, E)
+    rq, rs = moe.quant_rows_fp8(h)
+    assert torch.equal(xq.view(torch.uint8), rq.view(torch.uint8)) and torch.equal(xs, rs)
+    topw, topi = moe.topk_softmax(logits, K)
+    roff, rtok, rtw, rinv = moe.route_device(topi, topw, E)
+    assert torch.equal(off.cpu(), roff.cpu())
+    off = off.cpu().tolist()
+    tok, tw, inv = tok.cpu(), tw.cpu(), inv.cpu()
+    rtok, rtw = rtok.cpu(), rtw.cpu()
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        mine = sorted(zip(tok[a:b].tolist(), tw[a:b].tolist()))
+        ref = sorted(zip(rtok[a:b].tolist(), rtw[a:b].tolist()))
+        assert [m[0] for m in mine] == [r[0] for r in ref], e
+        assert max((abs(m[1] - r[1]) for m, r in zip(mine, ref)), default=0.0) < 1e-5, e
+    assert torch.equal(tok[inv.long()], torch.arange(T).repeat_interleave(K).to(torch.int32))
+    assert torch.equal(torch.sort(inv.long()).values, torch.arange(T * K))
+
+
 def test_moe_grouped_fp8_with_padding_rows():
     """EP receive side: rows tagged with their local expert (-1 = capacity padding) in one grouped
     call == per-row fp32 reference; padding rows come back zero."""
