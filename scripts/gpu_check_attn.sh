@@ -16,3 +16,4 @@ step t_attn 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread 
      -k "prefill_attention or fused_lm_head or sampler or agreement or production or route_quant or moe_prefill" || exit 1
 step b_attn 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed || exit 1
 step t_world8 700 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_world8_gpu.py -k tp8 || exit 1
+step b_tpov 400 python -u -m financial_chatbot_llm_amd.bench.tp_decode_overlap --world 8 --layers 4 --batch 64 --ctx 1024 --out gpurun_out/tp_decode_overlap.jsonl || exit 1
