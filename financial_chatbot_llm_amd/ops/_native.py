@@ -32,6 +32,7 @@ _SIGS = {
     "penny_silu_mul": [P, P, c_int, c_int, c_int, P],
     "penny_skinny_gemm": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_splitk_vw_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_reduce": [P, c_int, c_int, c_int, P, c_int, P, c_int, P],
     "penny_gateup_silu_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gemm_prefill": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int,

@@ -347,6 +347,43 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [1, 17, 40, 64, 100, 128])
+@pytest.mark.parametrize("N_,K,S,nf", [(384, 2048, 1, 4), (768, 2048, 4, 8), (384, 1024, 2, 12), (6144, 4096, 4, 8),
+                                       (4096, 14336, 4, 4), (384, 832, 1, 4), (256, 192, 1, 8), (384, 576, 1, 12)])
+def test_splitk_vw_gemm(M, N_, K, S, nf):
+    """Weight-in-VGPR decode GEMM (untracked W register ring + X LDS ring): f32 slabs vs the fp32
+    reference at toy and production (QKV, down) shapes; stages per K slice 32, 8, 8, 16, 56 (whole
+    ring turns), 13 (a 5-stage past-the-end turn), 3 and 9 (fewer stages than the ring is deep)."""
+    from financial_chatbot_llm_amd.ops import gemm
+    if N_ % (16 * nf):
+        pytest.skip("shape")
+    g = torch.Generator().manual_seed(13)
+    x = rnd(M, K, gen=g)
+    w = rnd(N_, K, scale=0.05, gen=g)
+    P = gemm.splitk_vw(x.to(DEV), gemm.tile_weight(w.to(DEV)), N_, S, nf)
+    ref_p = (x.float().view(M, S, K // S).transpose(0, 1) @ w.float().view(N_, S, K // S).permute(1, 2, 0))
+    close(P, ref_p, atol=2e-3 * max(1.0, (K / S / 2048) ** 0.5))
+    # same MFMA order per slice as the LDS-ring kernel: identical slabs
+    if nf in (4, 8) and M > 1:
+        assert torch.equal(gemm.splitk_partials(x.to(DEV), gemm.tile_weight(w.to(DEV)), N_, S, nf), P)
+
+
+@pytest.mark.parametrize("M", [1, 33, 128])
+@pytest.mark.parametrize("Fr,K", [(512, 1024), (14336, 4096)])
+def test_splitk_vw_gateup_silu(M, Fr, K):
+    """vw kernel with the fused SiLU(gate) * up epilogue == the LDS-ring gate|up kernel (same
+    roundings, same MFMA order: bit-equal) and close to the fp32 reference."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(6)
+    x = rnd(M, K, gen=g)
+    gate, up = rnd(Fr, K, scale=0.03, gen=g), rnd(Fr, K, scale=0.03, gen=g)
+    wt = gemm.tile_weight(gemm.interleave16(gate, up).to(DEV).contiguous())
+    y = gemm.splitk_vw(x.to(DEV), wt, 2 * Fr, 1, 8, silu=True)
+    assert torch.equal(y, gemm.gateup_silu(x.to(DEV), wt, 2 * Fr, 8))
+    gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
+    close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
+
+
 @pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])
 def test_splitk_rowmajor_tp_and_70b_shapes(N_, K, S, nf):
     """The table shapes that stream the row-major weight (70B, TP=8 shards) vs the fp32 reference."""
