@@ -174,8 +174,15 @@ __device__ __forceinline__ void read_x(const char* __restrict__ h, FragPair (&b)
 // 128-byte K-tile row in ONE v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair, unit block
 // scales (E8M0 127 = 2^0) -- 2x the bf16 MFMA rate; lane (row l & 15) feeds its 32 bytes k-block
 // (l >> 4) of A and of B alike, so the k order inside a block is the same on both operands.
+// MFMAs stay inside their phase (sched_barriers against the machine scheduler, an empty asm "use"
+// of the fp8 results against IR sinking): without that, hipcc moved every v_mfma_scale (fp8) of a
+// K-tile past the phase barriers into its last phase (1 + 31 MFMAs between barriers instead of 8
+// per phase), so the partner wave's fragment reads never overlapped them and every fragment was
+// live at once (the balanced schedule then spilled 250 VGPRs).  The bf16 v_mfma_f32_16x16x32
+// stayed in place.  tests/test_vw_asm_hazards.py checks the phase layout of both.
 template <int F0, int T0, bool FP8>
 __device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], const FragPair (&b)[2]) {
+  __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_setprio(1);
   if constexpr (FP8) {
 #pragma unroll
@@ -184,6 +191,12 @@ __device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], 
       for (int t = 0; t < 2; ++t)
         acc[F0 + f][T0 + t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
             a[f].v, b[t].v, acc[F0 + f][T0 + t], 0, 0, 0, 127, 0, 127);
+    // the results "used" here, in place: an IR pass otherwise sank every fp8 MFMA of the K-tile
+    // into its last phase (the intrinsic is pure; sched_barrier alone does not stop IR motion)
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(acc[F0 + f][T0 + t]));
   } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -195,6 +208,7 @@ __device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], 
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f].f[kk].v, b[t].f[kk].v, acc[F0 + f][T0 + t], 0, 0, 0);
   }
   __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // ABL (diagnostic builds only, penny_gemm_prefill_ablate): 1 = no LDS-DMA inside the K loop,
@@ -740,17 +754,25 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
                                          const void* W, const float* ws, const float* route_w, void* Y, int ldy,
                                          int P, int E, int N, int K, int epi, hipStream_t stream) {
   if (P <= 0) return 0;
+  // epi + 16: the plain 12/4/8/0 fragment-read schedule (A/B reference) instead of the balanced one
+  const bool plain = epi >= 16;
+  epi &= 15;
   if (N % TN || K % 128 || ldx % 16 || ldy % 8 || E <= 0 || E > 256 || !offsets || !xs || !ws)
     return (int)hipErrorInvalidValue;
   if ((epi != EPI_MOE_SILU && epi != EPI_MOE_ROUTE) || (epi == EPI_MOE_ROUTE && !route_w)) return (int)hipErrorInvalidValue;
   const MoeArgs ma{offsets, rows, xs, ws, route_w, E};
   const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
-  if (epi == EPI_MOE_SILU)
-    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_SILU, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
-  else
-    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_ROUTE, 0, 0, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
-                       ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
+#define MOE_TILE(EPI_, BAL_)                                                                                    \
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI_, 0, BAL_, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy, \
+                     (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{})
+  if (plain) {
+    if (epi == EPI_MOE_SILU) MOE_TILE(EPI_MOE_SILU, 0);
+    else MOE_TILE(EPI_MOE_ROUTE, 0);
+  } else {
+    if (epi == EPI_MOE_SILU) MOE_TILE(EPI_MOE_SILU, 1);
+    else MOE_TILE(EPI_MOE_ROUTE, 1);
+  }
+#undef MOE_TILE
   return (int)hipGetLastError();
 }
 

@@ -24,6 +24,9 @@ def topk_softmax(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tens
 # prefill-size fp8 MoE steps run moe_prefill_fp8_tiles (PENNY_MOE_PREFILL_TILES=0: the per-expert
 # hipBLASLt fp8 loop with one host read of the bucket sizes per layer)
 PREFILL_TILES = os.environ.get("PENNY_MOE_PREFILL_TILES", "1") != "0"
+# fp8 tile GEMMs: the balanced fragment-read schedule (default); PENNY_MOE_TILE_SCHED=plain takes
+# the plain 12/4/8/0 one (A/B reference; the kernel takes it as epi + 16)
+TILE_SCHED = 16 if os.environ.get("PENNY_MOE_TILE_SCHED", "balanced") == "plain" else 0
 # expert-parallel receives of at least this many rows run moe_grouped_fp8_tiles
 EP_TILE_MIN_ROWS = int(os.environ.get("PENNY_EP_TILE_MIN_ROWS", "512"))
 
@@ -148,13 +151,13 @@ def moe_prefill_fp8_tiles(h: torch.Tensor, router_logits: torch.Tensor, w13q: to
     st = N.stream()
     a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
-           N.ptr(s13), None, N.ptr(a), F_, P, E, F2, H, 7, st)
+           N.ptr(s13), None, N.ptr(a), F_, P, E, F2, H, 7 + TILE_SCHED, st)
     aq = torch.empty((P, F_), dtype=torch.uint8, device=h.device)
     as_ = torch.empty(P, dtype=torch.float32, device=h.device)
     N.call("penny_quant_rows_fp8", N.ptr(a), F_, P, F_, N.ptr(aq), N.ptr(as_), st)
     y2 = torch.empty((P, H), dtype=torch.bfloat16, device=h.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(aq), F_, None, N.ptr(as_), N.ptr(offsets), N.ptr(w2q), N.ptr(s2),
-           N.ptr(tok_w), N.ptr(y2), H, P, E, H, F_, 8, st)
+           N.ptr(tok_w), N.ptr(y2), H, P, E, H, F_, 8 + TILE_SCHED, st)
     out = torch.empty_like(h)
     N.call("penny_moe_combine", N.ptr(y2), N.ptr(inv), T, top_k, H, N.ptr(out), st)
     return out
@@ -222,14 +225,14 @@ def moe_grouped_fp8_tiles(x: torch.Tensor, expert_ids: torch.Tensor, w13q: torch
     N.call("penny_quant_rows_fp8", N.ptr(x), x.stride(0), M, H, N.ptr(xq), N.ptr(xs), st)
     a = torch.zeros((M, F_), dtype=torch.bfloat16, device=x.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(rows), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
-           N.ptr(s13), None, N.ptr(a), F_, M, E, F2, H, 7, st)
+           N.ptr(s13), None, N.ptr(a), F_, M, E, F2, H, 7 + TILE_SCHED, st)
     aq = torch.empty((M, F_), dtype=torch.uint8, device=x.device)
     as_ = torch.empty(M, dtype=torch.float32, device=x.device)
     N.call("penny_quant_rows_fp8", N.ptr(a), F_, M, F_, N.ptr(aq), N.ptr(as_), st)
     ones = torch.ones(M, dtype=torch.float32, device=x.device)
     y2 = torch.zeros((M, H), dtype=torch.bfloat16, device=x.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(aq), F_, None, N.ptr(as_), N.ptr(offsets), N.ptr(w2q), N.ptr(s2),
-           N.ptr(ones), N.ptr(y2), H, M, E, H, F_, 8, st)
+           N.ptr(ones), N.ptr(y2), H, M, E, H, F_, 8 + TILE_SCHED, st)
     y = torch.empty_like(y2)
     y.index_copy_(0, order, y2)
     return y

@@ -72,3 +72,37 @@ def test_vw_kernel_untracked_loads_are_never_read_early(tmp_path):
         assert not bad, (name, bad[:5])
         # the compiler may only drain vmcnt after the loop (the kernel's own final wait)
         assert len(loop_waits) == 0, (name, loop_waits[:5])
+
+
+GEMM_SRC = os.path.join(os.path.dirname(SRC), "gemm_prefill.hip")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_tile_gemm_mfmas_stay_in_their_phases(tmp_path):
+    """gemm_prefill.hip's ping-pong needs each phase's MFMAs between its two barriers (16 bf16 or
+    8 fp8 block-scaled MFMAs per phase): hipcc once sank every fp8 MFMA of a K-tile into the last
+    phase (1 + 31), which serialised the partner waves and made the balanced schedule spill."""
+    asm = tmp_path / "gp.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    GEMM_SRC, "-o", str(asm)], check=True, capture_output=True)
+    s = asm.read_text()
+    names = re.findall(r"^(_ZN12_GLOBAL__N_119gemm_prefill_kernel\w+):", s, re.M)
+    assert any("Lb1E" in n for n in names) and any("Lb0E" in n for n in names)
+    for name in names:
+        i = s.index(name + ":")
+        body = [ln.strip() for ln in s[i:s.index(".Lfunc_end", i)].splitlines()]
+        fp8 = bool(re.search(r"gemm_prefill_kernelILi\d+ELi\d+ELi\d+ELb1E", name))
+        counts, m = [], 0
+        for ln in body:
+            if ln.startswith("s_barrier"):
+                counts.append(m)
+                m = 0
+            elif ln.startswith("v_mfma"):
+                m += 1
+        per_phase = 8 if fp8 else 16
+        assert set(counts) <= {0, per_phase}, (name, counts[:30])
+        assert counts.count(per_phase) >= 4, (name, counts[:30])
+        diagnostic = re.search(r"gemm_prefill_kernelILi\d+ELi[123]E", name)   # ablation builds
+        if not diagnostic and "ILi9E" not in name:
+            assert not any(ln.startswith("scratch_") for ln in body), name
