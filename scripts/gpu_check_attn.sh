@@ -16,9 +16,10 @@ step() {  # name, timeout, command...
 }
 if [ "$PART" = 1 ]; then
   step t_attn 420 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
-       -k "prefill_attention or fused_lm_head or sampler or agreement or production or route_quant or moe_prefill or vw" || exit 1
+       -k "prefill_attention or fused_lm_head or sampler or agreement or production or route_quant or moe_prefill or moe_grouped or vw" || exit 1
   step b_attn 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed --out gpurun_out/prefill_mixed.jsonl || exit 1
   step b_vw 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only vw --out gpurun_out/vw.jsonl || exit 1
+  step b_moe 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only moe_prefill --out gpurun_out/moe_prefill.jsonl || exit 1
 else
   step t_world8 700 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_world8_gpu.py -k tp8 || exit 1
   step b_tpov 400 python -u -m financial_chatbot_llm_amd.bench.tp_decode_overlap --world 8 --layers 4 --batch 64 --ctx 1024 --out gpurun_out/tp_decode_overlap.jsonl || exit 1
