@@ -1074,6 +1074,15 @@ __device__ __forceinline__ void pp_pv(const uint4* __restrict__ vl, Frag (&vf)[D
   }
 }
 
+// 16 B per lane global -> LDS (M0 = this wave's LDS destination), opaque to the waitcnt pass
+__device__ __forceinline__ void glds16_untracked(const char* gptr, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gptr), "s"(lds_addr)
+               : "memory");
+}
+
 __device__ __forceinline__ void lgkm0_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Lean (KV-split) prefill work: a tile's KV walk can be cut into chunks run by different
@@ -1125,20 +1134,22 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   PENNY_DASSERT(nblk >= 1);
   const int* bt = block_tables + (long)s * max_blocks + jb;
 
+  // The LDS-DMA is issued from inline asm, invisible to hipcc's waitcnt pass: with the builtin it
+  // could not prove the P.V fragment reads do not alias the block just staged and drained vmcnt(0)
+  // before them every block (the staged prefetch then never overlapped the math).  The counted
+  // vmcnt + barrier protocol below is the only wait on these loads.
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   auto stage = [&](int j) {                   // j: local block index (buffer j % NBUF)
     const long phys = bt[j];
     PENNY_DASSERT(phys >= 0);
     const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    char* kl = smem + (j % NBUF) * 2 * TILE;
-    char* vl = kl + TILE;
+    const unsigned kl = lds0 + (j % NBUF) * 2 * TILE;
 #pragma unroll
     for (int i = 0; i < PIECES; ++i) {
       const int piece = w * PIECES + i;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kl + piece * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vl + piece * 1024),
-                                       16, 0, 0);
+      glds16_untracked(kb + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(kl + piece * 1024));
+      glds16_untracked(vb + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(kl + TILE + piece * 1024));
     }
   };
   stage(0);
