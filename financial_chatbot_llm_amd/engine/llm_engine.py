@@ -436,7 +436,9 @@ class LLMEngine:
         if not batch.empty():
             si = build_step_inputs(batch)
             if self.ps.tp_size > 1:
+                tb = time.perf_counter()
                 comm.broadcast_step(si)
+                self.timing["c4_s"] = self.timing.get("c4_s", 0.0) + time.perf_counter() - tb
             t1 = time.perf_counter()
             launched = (batch, self._samplers(batch), self.runner.launch(si))
             # teacher-forced drafts were verified at _advance: drop the rejected tail now that the
@@ -523,6 +525,7 @@ class LLMEngine:
         adds a device sync between the leader's launches."""
         prev = None
         t = self.timing
+        steps = 0
         while True:
             t0 = time.perf_counter()
             si = comm.broadcast_step(None)
@@ -537,8 +540,13 @@ class LLMEngine:
                 prev.result()
             t["post_s"] += time.perf_counter() - t2
             prev = cur
+            steps += 1
         if prev is not None:
             prev.result()
+        # the C4 anatomy of this follower: time blocked receiving the leader's steps, launching them,
+        # and waiting for its own previous step's results (its GPU time not hidden by the receive)
+        logger.info(f"tp follower rank {self.ps.rank}: {steps} steps, recv {t.get('recv_s', 0.0):.2f}s, "
+                    f"launch {t['execute_s']:.2f}s, wait {t['post_s']:.2f}s")
 
     def stop_followers(self) -> None:
         if self.ps.tp_size > 1 and self.ps.is_tp_leader:
