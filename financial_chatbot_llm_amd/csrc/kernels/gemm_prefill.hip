@@ -66,7 +66,7 @@ constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
 constexpr int GM = 4;                // token tiles per L2 group
 enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
 enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6,
-       EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8, EPI_SAMPLE = 9 };
+       EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8, EPI_SAMPLE = 9, EPI_MOE_SILU_MX = 10, EPI_MOE_ROUTE_MX = 11 };
 
 // Grouped fp8 MoE GEMM (penny_moe_gemm_prefill_fp8): rows sorted by expert, bucket bounds on the
 // DEVICE (offsets [E+1]), so tiles are found without a host round trip.
@@ -77,6 +77,14 @@ struct MoeArgs {
   const float* ws;        // [E, N] per-output-row weight scales
   const float* route_w;   // [P] routing weight of each sorted row (EPI_MOE_ROUTE)
   int E;
+  // MX hand-off between the two grouped GEMMs (EPI_MOE_SILU_MX writes, EPI_MOE_ROUTE_MX reads):
+  // E8M0 scales of the fp8 intermediate, one per 32-element k-block, [tile][K-tile][1 KiB] where
+  // "tile" is the 256-row token tile of the bucket walk (both GEMMs walk the same buckets) and a
+  // K-tile's KiB is [row group wb 4][row col 16][k-block 4] dwords whose 4 bytes are the rows
+  // wb*64 + 16j + col, j = 0..3: exactly the scale operand one lane of GEMM2 needs per K-tile
+  // (byte j selected by the MFMA's op_sel).
+  unsigned* mxs;
+  int nkt;                // K-tiles of GEMM2 (F / 128)
 };
 
 // EPI_SAMPLE: per-row temperature (<= 0: greedy) and seed; pv / pi [M, 2 * N / 256] partial bests.
@@ -180,11 +188,27 @@ __device__ __forceinline__ void read_x(const char* __restrict__ h, FragPair (&b)
 // per phase), so the partner wave's fragment reads never overlapped them and every fragment was
 // live at once (the balanced schedule then spilled 250 VGPRs).  The bf16 v_mfma_f32_16x16x32
 // stayed in place.  tests/test_vw_asm_hazards.py checks the phase layout of both.
-template <int F0, int T0, bool FP8>
-__device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], const FragPair (&b)[2]) {
+template <int F0, int T0, bool FP8, bool MXI = false>
+__device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], const FragPair (&b)[2],
+                                    unsigned sc = 0) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_setprio(1);
-  if constexpr (FP8) {
+  if constexpr (FP8 && MXI) {
+    // block-scaled X: byte T0 + t of this lane's scale word is the E8M0 scale of its token row
+    // (fragment T0 + t) and k-block (lane >> 4); W keeps the unit scale (its row scales stay in
+    // the epilogue)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      acc[F0 + f][T0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[f].v, b[0].v, acc[F0 + f][T0], 0, 0, 0,
+                                                                         127, T0, (int)sc);
+      acc[F0 + f][T0 + 1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[f].v, b[1].v, acc[F0 + f][T0 + 1], 0, 0,
+                                                                             0, 127, T0 + 1, (int)sc);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(acc[F0 + f][T0 + t]));
+  } else if constexpr (FP8) {
 #pragma unroll
     for (int f = 0; f < 4; ++f)
 #pragma unroll
@@ -227,9 +251,14 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
                                                            SampleArgs sa, TailArgs ta) {
   constexpr int ESZ = FP8 ? 1 : 2;        // bytes per element
   constexpr int BKE = 128 / ESZ;          // elements per K-tile row (128 bytes)
+  constexpr bool MXI = EPI == EPI_MOE_ROUTE_MX;   // X carries E8M0 block scales (GEMM2 of the MX hand-off)
+  constexpr bool MXO = EPI == EPI_MOE_SILU_MX;    // the epilogue writes fp8 + block scales (GEMM1)
+  static_assert(!(MXI || MXO) || (FP8 && BAL), "MX hand-off: fp8 tiles on the balanced schedule");
+  // X0 half-tiles carry one more LDS-DMA per wave under MXI (the K-tile's 1 KiB of scales)
+  constexpr int XL0 = MXI ? 3 : 2;
   const char* __restrict__ X = static_cast<const char*>(Xv);
   const char* __restrict__ W = static_cast<const char*>(Wv);
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + (MXI ? 2048 : 0)];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wa = w >> 2, wb = w & 3;  // wave grid 2 (W rows) x 4 (tokens)
@@ -285,7 +314,11 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   PENNY_DASSERT(N % TN == 0 && nt >= 1 && tm < Mt && tn < Nt);
 
   // ---- per-lane LDS-DMA sources: half h, piece i -> LDS rows 16w + 8i .. +7 of that half ----
+  // fp8 (grouped MoE): 32-bit byte offsets from the wave-uniform W / X bases (SGPRs), the saddr
+  // form of the DMA -- half the VGPRs of 64-bit per-lane pointers (an expert's W is < 2 GiB and
+  // so are the [P, K] activations), which the balanced schedule + MX scales need.
   const char* src[4][2];
+  unsigned soff[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -294,11 +327,13 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       const int c = (lane & 7) ^ swz<FP8>(lr);            // logical 16-B chunk held by this slot
       if (h == H_W0 || h == H_W1) {
         const int n = n0 + (lr >> 6) * 128 + (h == H_W1 ? 64 : 0) + (lr & 63);
-        src[h][i] = W + ((long)n * K + k0) * ESZ + 16 * c;
+        if constexpr (FP8) soff[h][i] = (unsigned)(((long)n * K + k0) + 16 * c);
+        else src[h][i] = W + ((long)n * K + k0) * ESZ + 16 * c;
       } else {
         int m = min(m0 + (lr >> 5) * 64 + (h == H_X1 ? 32 : 0) + (lr & 31), mend - 1);
         if (FP8 && ma.rows) m = ma.rows[m];              // GEMM1 gathers the routed token rows
-        src[h][i] = X + ((long)m * ldx + k0) * ESZ + 16 * c;
+        if constexpr (FP8) soff[h][i] = (unsigned)(((long)m * ldx + k0) + 16 * c);
+        else src[h][i] = X + ((long)m * ldx + k0) * ESZ + 16 * c;
       }
     }
   // The LDS-DMA is issued from inline asm, invisible to hipcc's waitcnt pass: with the builtin,
@@ -306,18 +341,52 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   // before every phase.  The counted vmcnt(6) below is then the only wait on these loads (the
   // loop issues no other vector-memory instruction), and M0 is set and restored in the statement.
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  // MXI: the K-tile's scale KiB lands next to the two K-tile buffers, each wave 128 B of it (lanes
+  // 0-31, 4 B each); issued with the X_q0 half, so it is retired by that half's wait
+  // (wave-uniform base: kept in SGPRs; the lane offset is added at issue -- a per-lane pointer held
+  // across the loop cost the two VGPRs that made the GEMM2 loop spill)
+  const char* mxbase = nullptr;
+  if constexpr (MXI) mxbase = reinterpret_cast<const char*>(ma.mxs) + ((long)tm * ma.nkt + k0 / BKE) * 1024 + w * 128;
   auto stage = [&](int h, int t, unsigned buf) {
     if (ABL == 1 && t > 1) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const char* gp = src[h][i] + (long)t * 128;
       const unsigned dst = buf + h * HALF + (16 * w + 8 * i) * 128;
       unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(gp), "s"(dst)
-                   : "memory");
+      if constexpr (FP8) {
+        const unsigned vo = soff[h][i] + (unsigned)t * 128;
+        const char* base = (h == H_W0 || h == H_W1) ? W : X;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(vo), "s"(dst), "s"(base)
+                     : "memory");
+      } else {
+        const char* gp = src[h][i] + (long)t * 128;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(gp), "s"(dst)
+                     : "memory");
+      }
     }
+    if constexpr (MXI) {
+      if (h == H_X0) {
+        const char* gp = mxbase + (long)t * 1024 + lane * 4;
+        const unsigned dst = lds0 + 2 * BUF + (t & 1) * 1024 + w * 128;
+        unsigned keep;
+        if (lane < 32)
+          asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                       : "=&s"(keep)
+                       : "v"(gp), "s"(dst)
+                       : "memory");
+      }
+    }
+  };
+  // this lane's scale word of K-tile t (byte j: token row wb*64 + 16j + col, k-block g)
+  auto read_sc = [&](int t) -> unsigned {
+    if constexpr (MXI)
+      return *reinterpret_cast<const unsigned*>(smem + 2 * BUF + (t & 1) * 1024 + wb * 256 + col * 16 + g * 4);
+    else
+      return 0u;
   };
 
   const int rowoff = col * 128;
@@ -338,7 +407,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   if (nt > 1) {
 #pragma unroll
     for (int h = 0; h < 3; ++h) stage(h, 1, lds0 + BUF);
-    wait_vm<6>();
+    wait_vm<4 + XL0>();
   } else {
     wait_vm<0>();
   }
@@ -354,11 +423,11 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   if (wa == 1) bar();
 
   // one phase: [fragment reads + DMA issued by the caller] barrier lgkmcnt(0) 16 MFMAs barrier
-  auto phase = [&](auto F0c, auto T0c, const FragPair (&aa)[4], const FragPair (&bb)[2]) {
+  auto phase = [&](auto F0c, auto T0c, const FragPair (&aa)[4], const FragPair (&bb)[2], unsigned sc = 0) {
     constexpr int F0 = decltype(F0c)::value, T0 = decltype(T0c)::value;
     bar();
     wait_lgkm0();
-    mma<F0, T0, FP8>(acc, aa, bb);
+    mma<F0, T0, FP8, MXI>(acc, aa, bb, sc);
     bar();
   };
   using I0 = std::integral_constant<int, 0>;
@@ -371,34 +440,39 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     // 12 / 4 / 8 / 0 (phase 1's 48 KB of reads + 16 KB of landing DMA filled its whole MFMA
     // window on the LDS).  The extra wait: vmcnt(8) in phase 3 retires X_q0 (and W_q0) of t+1
     // (4 younger half-tiles may stay in flight), a phase before it is read.
+    // MXI: a K-tile's scale word is read with its W_q0 fragments (phase 1; it landed with X_q0,
+    // retired by the phase-3 wait of the tile before) and held through the tile -- its buffer is
+    // restaged with X_q0 of t+2 in phase 3, two phases later
     FragPair c0[2];
+    unsigned sc = 0;
     auto tile = [&](int t, FragPair (&bc)[2], FragPair (&bn)[2]) {
       const char* cur = smem + (t & 1) * BUF;
       const char* nx = smem + ((t + 1) & 1) * BUF;
       const unsigned lcur = lds0 + (t & 1) * BUF, lnxt = lds0 + ((t + 1) & 1) * BUF;
       const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
       if (ABL != 2 || t == 0) read_w(cur + H_W0 * HALF, a, wa, rowoff, choff);
+      sc = read_sc(t);
       if (more1) stage(H_W1, t + 1, lnxt);
-      phase(I0{}, I0{}, a, bc);
+      phase(I0{}, I0{}, a, bc, sc);
       if (ABL != 2 || t == 0) read_x(cur + H_X1 * HALF, b1, wb, rowoff, choff);
       if (more2) stage(H_W0, t + 2, lcur);
-      phase(I0{}, I2{}, a, b1);
+      phase(I0{}, I2{}, a, b1, sc);
       if (ABL != 2 || t == 0) read_w(cur + H_W1 * HALF, a, wa, rowoff, choff);
       if (more2) {
         stage(H_X0, t + 2, lcur);
-        if (ABL != 3) wait_vm<8>();
+        if (ABL != 3) wait_vm<6 + XL0>();
       } else {
         wait_vm<0>();
       }
-      phase(I4{}, I2{}, a, b1);
+      phase(I4{}, I2{}, a, b1, sc);
       if (more1 && (ABL != 2 || t == 0)) read_x(nx + H_X0 * HALF, bn, wb, rowoff, choff);
       if (more2) {
         stage(H_X1, t + 2, lcur);
-        if (ABL != 3) wait_vm<6>();
+        if (ABL != 3) wait_vm<4 + XL0>();
       } else {
         wait_vm<0>();
       }
-      phase(I4{}, I0{}, a, bc);
+      phase(I4{}, I0{}, a, bc, sc);
     };
     read_x(smem + H_X0 * HALF, b0, wb, rowoff, choff);
     int t = 0;
@@ -486,14 +560,75 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   // token row m, so a lane masked off by m >= M always has a masked swap partner), after which a
   // lane holds 8 consecutive columns at lane_off + 16*(group pair index)
   const int lane_off = 8 * (g >> 1) + 16 * (g & 1);
+  if constexpr (MXO) {
+    // GEMM1 of the MX hand-off: SiLU(gate) * up with EPI_MOE_SILU's roundings, then per (row,
+    // 32-column block) an E8M0 scale 2^X, X = ceil(log2(amax / 448)) (no saturation), and the
+    // block's e4m3 bytes of value / 2^X -- the intermediate leaves as fp8 (half the bytes of bf16)
+    // and GEMM2 reads it without a per-row quantisation pass.  A block's 32 columns are lanes
+    // g = 0..3 (4 each) x two column groups q: amax is two xor-shuffles over g.
+    const float* wsc = ma.ws + (long)e * N + n0 + wa * 128;
+    unsigned char* yq = static_cast<unsigned char*>(Y);
+    const int ocol = ((n0 + wa * 128) >> 1) + 4 * g;        // this lane's first output column
+    unsigned word[2] = {0u, 0u};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int m = m0 + wb * 64 + t * 16 + col;
+      const bool valid = m < mend;                        // uniform over the 4 lanes of row m
+      const int mr = min(m, mend - 1);
+      const float sx = ma.xs[ma.rows ? ma.rows[mr] : mr];
+      float o[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 sg = *reinterpret_cast<const f32x4*>(wsc + 32 * q + 4 * g);
+        const f32x4 su = *reinterpret_cast<const f32x4*>(wsc + 32 * q + 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gv = (float)(bf16)(acc[2 * q][t][r] * sx * sg[r]);
+          const float uv = (float)(bf16)(acc[2 * q + 1][t][r] * sx * su[r]);
+          o[q][r] = (float)(bf16)((float)(bf16)(gv / (1.f + __expf(-gv))) * uv);
+        }
+      }
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        float amax = 0.f;
+#pragma unroll
+        for (int q = 2 * bb; q < 2 * bb + 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(o[q][r]));
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const unsigned bits = __float_as_uint(amax * (1.f / 448.f));
+        const int ex = (int)((bits >> 23) & 0xff);
+        int X = ex == 0 ? -127 : ex - 127 + ((bits & 0x7fffff) != 0);
+        X = max(-127, min(X, 126));
+        word[bb] |= (unsigned)(X + 127) << (8 * t);
+        const float inv = __uint_as_float((unsigned)(127 - X) << 23);   // 2^-X, exact
+        if (valid) {
+#pragma unroll
+          for (int q = 2 * bb; q < 2 * bb + 2; ++q) {
+            uint32_t pk = 0;
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(o[q][0] * inv, o[q][1] * inv, pk, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(o[q][2] * inv, o[q][3] * inv, pk, true);
+            *reinterpret_cast<uint32_t*>(yq + (long)m * ldy + ocol + 16 * q) = pk;
+          }
+        }
+      }
+    }
+    // lane g < 2 stores block g's scale word: rows wb*64 + 16j + col (byte j), k-block wa*2 + g of
+    // GEMM2's K-tile n0 / 256
+    if (g < 2)
+      ma.mxs[((long)tm * ma.nkt + n0 / 256) * 256 + wb * 64 + col * 4 + wa * 2 + g] = g == 0 ? word[0] : word[1];
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int m = m0 + wb * 64 + t * 16 + col;
     if (m >= mend) continue;
-    if constexpr (EPI == EPI_MOE_SILU || EPI == EPI_MOE_ROUTE) {
+    if constexpr (EPI == EPI_MOE_SILU || EPI == EPI_MOE_ROUTE || EPI == EPI_MOE_ROUTE_MX) {
       // dequantise (activation row scale x weight row scale), then the decode pipeline's epilogue
-      // roundings (moe.hip moe_gemm_kernel): SiLU(gate) * up, or x routing weight
-      const float sx = ma.xs[ma.rows ? ma.rows[m] : m];
+      // roundings (moe.hip moe_gemm_kernel): SiLU(gate) * up, or x routing weight.  MX input: the
+      // activation's block scales were applied inside the MFMA
+      const float sx = MXI ? 1.f : ma.xs[ma.rows ? ma.rows[m] : m];
       const float* wsc = ma.ws + (long)e * N + n0 + wa * 128;
       if constexpr (EPI == EPI_MOE_SILU) {
         bf16x4 o[4];
@@ -760,7 +895,7 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
   if (N % TN || K % 128 || ldx % 16 || ldy % 8 || E <= 0 || E > 256 || !offsets || !xs || !ws)
     return (int)hipErrorInvalidValue;
   if ((epi != EPI_MOE_SILU && epi != EPI_MOE_ROUTE) || (epi == EPI_MOE_ROUTE && !route_w)) return (int)hipErrorInvalidValue;
-  const MoeArgs ma{offsets, rows, xs, ws, route_w, E};
+  const MoeArgs ma{offsets, rows, xs, ws, route_w, E, nullptr, 0};
   const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
 #define MOE_TILE(EPI_, BAL_)                                                                                    \
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI_, 0, BAL_, true>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy, \
@@ -773,6 +908,41 @@ PENNY_API int penny_moe_gemm_prefill_fp8(const void* X, int ldx, const int* rows
     else MOE_TILE(EPI_MOE_ROUTE, 1);
   }
 #undef MOE_TILE
+  return (int)hipGetLastError();
+}
+
+// The MX hand-off between the two grouped GEMMs of an fp8 MoE layer (no per-row quantisation pass
+// between them):
+//   epi 10 (GEMM1): X = routed token rows (fp8, row scales xs, gathered by rows), W = W13 [E, 2F, H];
+//                   Y = the SiLU(gate) * up intermediate as e4m3 bytes [P, F] (ldy = F) and its
+//                   E8M0 block scales into mxs (one per 32 columns; layout: MoeArgs::mxs);
+//   epi 11 (GEMM2): X = that intermediate [P, F] (ldx = F) with mxs, W = W2 [E, H, F];
+//                   Y[p, H] bf16 = (X x W2_e) * ws2 * route_w[p].
+// mxs holds ((P + 255) / 256 + E) * (F / 128) KiB; nkt = F / 128.  Contract as above.
+PENNY_API int penny_moe_gemm_prefill_fp8_mx(const void* X, int ldx, const int* rows, const float* xs,
+                                            const int* offsets, const void* W, const float* ws, const float* route_w,
+                                            void* Y, int ldy, int P, int E, int N, int K, int epi, unsigned* mxs,
+                                            int nkt, hipStream_t stream) {
+  if (P <= 0) return 0;
+  if (N % TN || K % 128 || ldx % 16 || ldy % 8 || E <= 0 || E > 256 || !offsets || !ws || !mxs || nkt <= 0)
+    return (int)hipErrorInvalidValue;
+  if (epi == EPI_MOE_SILU_MX) {
+    if (!xs || nkt != N / 256) return (int)hipErrorInvalidValue;
+  } else if (epi == EPI_MOE_ROUTE_MX) {
+    if (!route_w || nkt != K / 128) return (int)hipErrorInvalidValue;
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  MoeArgs ma{offsets, rows, xs, ws, route_w, E, nullptr, 0};
+  ma.mxs = mxs;
+  ma.nkt = nkt;
+  const dim3 grid((unsigned)(((P + TM - 1) / TM + E) * (N / TN)));
+  if (epi == EPI_MOE_SILU_MX)
+    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_SILU_MX, 0, 1, true>), grid, dim3(512), 0, stream, X, ldx, W, K,
+                       Y, ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
+  else
+    hipLaunchKernelGGL((gemm_prefill_kernel<EPI_MOE_ROUTE_MX, 0, 1, true>), grid, dim3(512), 0, stream, X, ldx, W, K,
+                       Y, ldy, (const bf16*)nullptr, 0, P, N, 1, RopeArgs{}, ma, SampleArgs{}, TailArgs{});
   return (int)hipGetLastError();
 }
 

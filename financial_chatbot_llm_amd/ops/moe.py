@@ -27,6 +27,9 @@ PREFILL_TILES = os.environ.get("PENNY_MOE_PREFILL_TILES", "1") != "0"
 # fp8 tile GEMMs: the balanced fragment-read schedule (default); PENNY_MOE_TILE_SCHED=plain takes
 # the plain 12/4/8/0 one (A/B reference; the kernel takes it as epi + 16)
 TILE_SCHED = 16 if os.environ.get("PENNY_MOE_TILE_SCHED", "balanced") == "plain" else 0
+# prefill tiles: the SiLU intermediate handed from GEMM1 to GEMM2 as MX fp8 (e4m3 + one E8M0 scale per
+# 32 columns, written by GEMM1's epilogue) instead of bf16 + a per-row quantisation pass
+MX_HANDOFF = os.environ.get("PENNY_MOE_MX", "0") == "1"
 # expert-parallel receives of at least this many rows run moe_grouped_fp8_tiles
 EP_TILE_MIN_ROWS = int(os.environ.get("PENNY_EP_TILE_MIN_ROWS", "512"))
 
@@ -149,6 +152,20 @@ def moe_prefill_fp8_tiles(h: torch.Tensor, router_logits: torch.Tensor, w13q: to
     P = T * top_k
     xq, xs, offsets, tok_idx, tok_w, inv = _route_and_quant(h, router_logits, top_k, E)
     st = N.stream()
+    if MX_HANDOFF and F_ % 128 == 0:
+        # GEMM1 writes the intermediate as e4m3 + E8M0 block scales, GEMM2 consumes them in its
+        # block-scaled MFMAs: no bf16 intermediate, no per-row quantisation pass
+        nkt = F_ // 128
+        mxs = torch.empty((((P + 255) // 256 + E) * nkt * 256,), dtype=torch.int32, device=h.device)
+        aq = torch.empty((P, F_), dtype=torch.uint8, device=h.device)
+        N.call("penny_moe_gemm_prefill_fp8_mx", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets),
+               N.ptr(w13q), N.ptr(s13), None, N.ptr(aq), F_, P, E, F2, H, 10, N.ptr(mxs), nkt, st)
+        y2 = torch.empty((P, H), dtype=torch.bfloat16, device=h.device)
+        N.call("penny_moe_gemm_prefill_fp8_mx", N.ptr(aq), F_, None, None, N.ptr(offsets), N.ptr(w2q), N.ptr(s2),
+               N.ptr(tok_w), N.ptr(y2), H, P, E, H, F_, 11, N.ptr(mxs), nkt, st)
+        out = torch.empty_like(h)
+        N.call("penny_moe_combine", N.ptr(y2), N.ptr(inv), T, top_k, H, N.ptr(out), st)
+        return out
     a = torch.empty((P, F_), dtype=torch.bfloat16, device=h.device)
     N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(w13q),
            N.ptr(s13), None, N.ptr(a), F_, P, E, F2, H, 7 + TILE_SCHED, st)
@@ -322,9 +339,21 @@ def _fake_quant_rows(x: torch.Tensor) -> torch.Tensor:
     return q.float() * s[..., None]
 
 
-def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act: bool = False):
+def _fake_quant_mx(x: torch.Tensor) -> torch.Tensor:
+    """Round-trip rows through MX fp8: per 32-column block an E8M0 scale 2^X with
+    X = ceil(log2(amax / 448)), e4m3 of value / 2^X (the GEMM1 epilogue of the MX hand-off)."""
+    R, C = x.shape
+    b = x.float().view(R, C // 32, 32)
+    amax = b.abs().amax(-1, keepdim=True)
+    X = torch.where(amax > 0, torch.ceil(torch.log2(amax / FP8_MAX)), torch.full_like(amax, -127.0)).clamp(-127, 126)
+    sc = torch.exp2(X)
+    return ((b / sc).to(FP8).float() * sc).view(R, C)
+
+
+def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act=False):
     """fp32 reference of the fp8 MoE MLP (weights dequantised).  ``quant_act`` additionally rounds
-    both GEMM inputs through dynamic per-row fp8, matching the HIP pipeline's arithmetic."""
+    both GEMM inputs through dynamic per-row fp8, matching the HIP pipeline's arithmetic;
+    ``quant_act="mx"`` rounds the intermediate through MX fp8 (the tiles' MX hand-off) instead."""
     topw, topi = topk_softmax(h.float() @ router_w.float().t(), top_k)
     out = torch.zeros(h.shape, dtype=torch.float32, device=h.device)
     from .activation import silu_mul
@@ -339,7 +368,9 @@ def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act: bool = 
         if quant_act:
             x = _fake_quant_rows(x)
         a = silu_mul((x @ w13.t()).to(torch.bfloat16), interleave16=True).float()
-        if quant_act:
+        if quant_act == "mx":
+            a = _fake_quant_mx(a)
+        elif quant_act:
             a = _fake_quant_rows(a)
         y = a @ w2.t()
         wt = (topw * sel).sum(-1)[rows]

@@ -900,6 +900,49 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
     assert err < 0.03, err
 
 
+@pytest.mark.parametrize("T,E", [(1000, 8), (3001, 4)])
+def test_moe_prefill_mx_handoff(T, E, monkeypatch):
+    """MX hand-off of the fp8 tile pipeline (GEMM1 epilogue writes the SiLU intermediate as e4m3 +
+    E8M0 scales per 32 columns, GEMM2 consumes them in its block-scaled MFMAs) vs the fp32
+    per-expert reference with the same activation roundings (rows: per-row fp8; intermediate:
+    MX fp8), and vs the per-row-quantised tile pipeline it replaces."""
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    g = torch.Generator(device=DEV).manual_seed(T)
+    H, F_, K = 1024, 1536, 2
+    w13 = (torch.randn((E, 2 * F_, H), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    w13 = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    w2 = (torch.randn((E, H, F_), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    h = torch.randn((T, H), device=DEV, generator=g).to(torch.bfloat16)
+    logits = (torch.randn((T, E), device=DEV, generator=g) * 2).to(torch.bfloat16)
+    monkeypatch.setattr(moe, "MX_HANDOFF", False)
+    rowq = moe.moe_prefill_fp8_tiles(h, logits, q13.contiguous(), s13, q2.contiguous(), s2, K).float()
+    monkeypatch.setattr(moe, "MX_HANDOFF", True)
+    got = moe.moe_prefill_fp8_tiles(h, logits, q13.contiguous(), s13, q2.contiguous(), s2, K).float()
+    topw, topi = moe.topk_softmax(logits, K)
+    xq, xs = moe.quant_rows_fp8(h)
+    xd = xq.float() * xs[:, None]
+    ref = torch.zeros((T, H), device=DEV)
+    for e in range(E):
+        sel = (topi == e)
+        rows = sel.any(1).nonzero().flatten()
+        if rows.numel() == 0:
+            continue
+        w13d = q13[e].float() * s13[e][:, None]
+        w2d = q2[e].float() * s2[e][:, None]
+        a = gemm.silu_mul((xd[rows] @ w13d.t()).to(torch.bfloat16), interleave16=True)
+        y = moe._fake_quant_mx(a.float()) @ w2d.t()
+        ref[rows] += (topw * sel).sum(1)[rows][:, None] * y
+    err = (got - ref).abs()
+    assert float(err.max() / ref.abs().max()) < 0.03, float(err.max() / ref.abs().max())
+    # an activation on the other side of an e4m3 rounding boundary moves single outputs: bound
+    # the mean (as the other fp8 pipeline tests do)
+    assert float(err.mean()) < 0.01 * float(ref.abs().mean()) + 1e-4, (float(err.mean()), float(ref.abs().mean()))
+    # per-32-column scales are at least as fine as per-row ones: no worse than the row-quantised pipe
+    assert float((got - rowq).abs().mean()) < 0.03 * float(rowq.abs().mean())
+
+
 def test_moe_grouped_fp8_tiles_matches_reference():
     """Expert-parallel receive side on the tile kernel: y[i] = expert_{ids[i]}(x[i]) in the
     received (unsorted) row order, padding rows (id -1) zero."""
