@@ -276,7 +276,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2": 0, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean"}
+        variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():

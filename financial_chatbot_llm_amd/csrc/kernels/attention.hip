@@ -95,7 +95,7 @@ struct CascadeArgs {
 // ONE copy of the MFMA code in the loop: with two inlined copies (one per mode, behind an if/else)
 // the accumulators meet at a join point and hipcc materialises the merge as v_mov_b64 copies of
 // MFMA results (each one waits for its MFMA to retire), ~64 per block.
-template <int D, int MASK, bool PREF = false>
+template <int D, int MASK, bool PREF = false, bool SB = false>
 __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
                                              const Frag (&qf)[2][D / 32], f32x4 (&o)[2][D / 16], float (&m)[2],
                                              float (&l)[2], bool causal, int j, int ctx,
@@ -109,6 +109,9 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
   if constexpr (PREF) {
 #pragma unroll
     for (int f = 0; f < 4 * KC; ++f) kfa[f].u = kl[f * 64 + lane];
+    // SB: pin the 16 reads ahead of the MFMAs -- hipcc otherwise sinks each pair next to its use
+    // and waits for it (lgkmcnt(0) every 2-4 MFMAs: the LDS latency exposed 8 times per block)
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -130,6 +133,7 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
   if constexpr (PREF) {   // V fragments in flight while the softmax runs
 #pragma unroll
     for (int f = 0; f < 2 * DT; ++f) vfa[f].u = vl[f * 64 + lane];
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- online softmax (base-2) -------------------------------------------------------
@@ -821,7 +825,7 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true>
+template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -926,7 +930,7 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
     const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    attend_block<D, 2, PREF>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
+    attend_block<D, 2, PREF, SB>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
                              __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
@@ -1322,8 +1326,9 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   PENNY_RETURN_LAUNCH();
 }
 
-// Big-tile prefill variant: 1 (default) ping-pong prefill3 with ones-MFMA row sums, 2 ping-pong
-// with VALU row sums, 3 = 1 + static priority for waves 4-7, 0 prefill2 (PENNY_PREFILL_PP, or
+// Big-tile prefill variant: 0 (default) prefill2, 1 ping-pong prefill3 with ones-MFMA row sums,
+// 2 ping-pong with VALU row sums, 3 = 1 + static priority for waves 4-7, 4 = prefill2 with its K/V
+// fragment prefetch pinned ahead of the MFMAs (PENNY_PREFILL_PP, or
 // penny_attention_prefill_variant for in-process A/B runs)
 static int g_prefill_variant = -1;
 static int prefill_variant() {
@@ -1380,6 +1385,10 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
     hipLaunchKernelGGL((prefill3_kernel<DD, true, true, true>), grid2, dim3(512), 0, stream,                     \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
+  else if (big && head_fast && pp_env == 4)                                                                      \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true>), grid2, dim3(512), 0, stream,               \
+                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big && head_fast)                                                                                     \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), grid2, dim3(512), 0, stream,                           \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \

@@ -13,11 +13,13 @@ step() {  # name, timeout, command...
   tail -3 "gpurun_out/$name.log"
   return $rc
 }
-step t_pf 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "prefill_attention" || exit 1
+step t_pf 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "prefill_attention or moe_prefill or moe_grouped or mx_handoff" || exit 1
 step b_pf 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed --out gpurun_out/prefill_mixed_v2.jsonl || exit 1
 step pmc_tiles 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \
      --kernel-trace --output-format csv -d gpurun_out/pmc_tiles -o run -- \
      python3 -m financial_chatbot_llm_amd.bench.kernels --only gemm_lds_probe || exit 1
 step moe_plain 240 env PENNY_MOE_TILE_SCHED=plain python -u -m financial_chatbot_llm_amd.bench.kernels --only moe_prefill \
      --out gpurun_out/moe_prefill_plain.jsonl || exit 1
+step moe_mx 240 env PENNY_MOE_MX=1 python -u -m financial_chatbot_llm_amd.bench.kernels --only moe_prefill \
+     --out gpurun_out/moe_prefill_mx.jsonl || exit 1
 step bench8b 420 python -u bench.py --steps 20 --warmup 5 || exit 1
