@@ -825,12 +825,21 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// Lean (KV-split) prefill work: a tile's KV walk can be cut into chunks run by different
+// workgroups; a chunk writes flash-decoding partial state (unnormalised O, running max m, row sum
+// l) to slot `slot`, and prefill_merge_kernel combines a tile's slots in chunk order.
+struct PrefillLean {
+  const int* items;     // [n, 6]: sequence, tile, first block, end block, slot (< 0: whole tile), 0
+  float* part_o;        // [slots, Hkv, 256 rows, D] f32
+  float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
+};
+
 template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
-    float* __restrict__ lse, const int* __restrict__ work) {
+    float* __restrict__ lse, const int* __restrict__ work, PrefillLean lean = PrefillLean{}) {
   constexpr int KC = D / 32, DT = D / 16;
   constexpr int TILE = KV_BS * D * 2;         // bytes of one K (or V) block tile
   constexpr int PIECES = TILE / 1024 / NW;    // 1-KiB glds pieces per wave per tile
@@ -847,9 +856,10 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   // round instead of trailing it, and no workgroup is launched for a tile past a short sequence's
   // end).  Without it: grid (.., max tiles, sequences), each sequence's tiles longest first.
   const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
-  const int s = work ? work[2 * item] : blockIdx.z;
+  const int* li = lean.items ? lean.items + 6 * item : nullptr;
+  const int s = li ? li[0] : (work ? work[2 * item] : blockIdx.z);
   const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
-  const int tile = work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item;
+  const int tile = li ? li[1] : (work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item);
   const int G = Hq / Hkv;
   const int TQ = NW * 32 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
@@ -860,8 +870,12 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 
   const int last_tok = min(tok0 + TQ, qlen) - 1;
   const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
-  const int nblk = (kv_end + KV_BS - 1) / KV_BS;
-  const int* bt = block_tables + (long)s * max_blocks;
+  const int nblk_tile = (kv_end + KV_BS - 1) / KV_BS;
+  // lean items: this workgroup's blocks [jb, jb + nblk) of the tile's walk, partial state to `slot`
+  const int jb = li ? li[2] : 0;
+  const int nblk = li ? min(li[3], nblk_tile) - jb : nblk_tile;
+  const int slot = li ? li[4] : -1;
+  const int* bt = block_tables + (long)s * max_blocks + jb;
 
   auto stage = [&](int j) {
     const long phys = bt[j];
@@ -921,16 +935,17 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   const bool wave_live = wave_tok0 < qlen;
   const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
   const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
-  for (int j = 0; j < nblk; ++j) {
+  for (int j = 0; j < nblk; ++j) {           // local block j = absolute block jb + j
     // my pieces of block j landed (younger blocks j+1.. may stay in flight), then publish
     if (j + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
     else wait_vmcnt_barrier<0>();
     if (j + NBUF - 1 < nblk) stage(j + NBUF - 1);   // refills the buffer everyone finished at j-1
-    if (!wave_live || j * KV_BS >= wave_kv_end) continue;
+    const int ja = jb + j;
+    if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
-    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    attend_block<D, 2, PREF, SB>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
+    const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
+    attend_block<D, 2, PREF, SB>(kl, vl, qf, o, m, l, causal, ja, ctx, qpos, scale_log2, lane, g,
                              __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
@@ -938,6 +953,16 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   for (int ct = 0; ct < 2; ++ct) {
     float lt = l[ct];
     lt = rowgroup_sum(lt);
+    if (slot >= 0) {                          // a chunk of a split walk: partial state for the merge
+      const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = o[ct][dt];
+      if (g == 0) {
+        lean.part_ml[2 * pr] = m[ct];
+        lean.part_ml[2 * pr + 1] = lt;
+      }
+      continue;
+    }
     if (tok[ct] >= qlen) continue;
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
@@ -1089,14 +1114,6 @@ __device__ __forceinline__ void glds16_untracked(const char* gptr, unsigned lds_
 
 __device__ __forceinline__ void lgkm0_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Lean (KV-split) prefill work: a tile's KV walk can be cut into chunks run by different
-// workgroups; a chunk writes flash-decoding partial state (unnormalised O, running max m, row sum
-// l) to slot `slot`, and prefill_merge_kernel combines a tile's slots in chunk order.
-struct PrefillLean {
-  const int* items;     // [n, 6]: sequence, tile, first block, end block, slot (< 0: whole tile), 0
-  float* part_o;        // [slots, Hkv, 256 rows, D] f32
-  float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
-};
 
 template <int D, bool HEAD_FAST, bool LSUM, bool PRIO, bool VPRE = false>
 __global__ void __launch_bounds__(512, 1) prefill3_kernel(
@@ -1294,8 +1311,11 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
   }
 }
 
+static int prefill_variant();
+
 // Lean big-tile prefill: items [nitems, 6] (see PrefillLean; LPT order), merge [nmerge, 6];
-// part_o / part_ml sized for the slots the items use.  Ping-pong kernel (variant 1) only.
+// part_o / part_ml sized for the slots the items use.  Runs the kernel of the selected big-tile
+// variant: prefill2 (0, 4) or the ping-pong prefill3 (1-3; D = 64 always prefill3).
 PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                            const void* k_cache, const void* v_cache, void* out, int Hq, int Hkv,
                                            int D, int max_blocks, float scale, int causal, float* lse,
@@ -1306,7 +1326,20 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
     return (int)hipErrorInvalidValue;
   const float sl2 = scale * LOG2E;
   const PrefillLean lean{items, part_o, part_ml};
-  if (D == 128) {
+  const int var = prefill_variant();
+  if (D == 128 && (var == 0 || var == 4)) {
+    if (var == 4)
+      hipLaunchKernelGGL((prefill2_kernel<128, 8, 3, true, true, true>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
+                         (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
+                         (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
+    else
+      hipLaunchKernelGGL((prefill2_kernel<128, 8, 3, true>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
+                         (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
+                         (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
+    if (nmerge > 0)
+      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+                         part_ml, (bf16*)out, lse, Hq, Hkv);
+  } else if (D == 128) {
     hipLaunchKernelGGL((prefill3_kernel<128, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
