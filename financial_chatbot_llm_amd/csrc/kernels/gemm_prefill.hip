@@ -946,6 +946,36 @@ PENNY_API int penny_moe_gemm_prefill_fp8_mx(const void* X, int ldx, const int* r
   return (int)hipGetLastError();
 }
 
+// Probe of the block-scaled MFMA's scale operands (one wave, one v_mfma_scale_f32_16x16x128_f8f6f4):
+// A, B: 64 lanes x 32 e4m3 bytes (lane l: row l & 15, k-block l >> 4), sa / sb: one 32-bit scale
+// word per lane, out: the 64 x 4 accumulator.  tests/test_kernels_gpu.py pins the lane / byte
+// semantics the MX hand-off relies on.
+template <int OPSEL>
+__global__ void __launch_bounds__(64) mfma_scale_probe_kernel(const int* __restrict__ A, const int* __restrict__ B,
+                                                               const int* __restrict__ sa, const int* __restrict__ sb,
+                                                               float* __restrict__ out) {
+  const int lane = threadIdx.x;
+  i32x8 a, b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = A[lane * 8 + i], b[i] = B[lane * 8 + i];
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa[lane], OPSEL, sb[lane]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) out[lane * 4 + r] = acc[r];
+}
+
+PENNY_API int penny_probe_mfma_scale(const int* A, const int* B, const int* sa, const int* sb, float* out, int opsel,
+                                     hipStream_t stream) {
+  switch (opsel) {
+    case 0: hipLaunchKernelGGL(mfma_scale_probe_kernel<0>, dim3(1), dim3(64), 0, stream, A, B, sa, sb, out); break;
+    case 1: hipLaunchKernelGGL(mfma_scale_probe_kernel<1>, dim3(1), dim3(64), 0, stream, A, B, sa, sb, out); break;
+    case 2: hipLaunchKernelGGL(mfma_scale_probe_kernel<2>, dim3(1), dim3(64), 0, stream, A, B, sa, sb, out); break;
+    case 3: hipLaunchKernelGGL(mfma_scale_probe_kernel<3>, dim3(1), dim3(64), 0, stream, A, B, sa, sb, out); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 // Reduce a row's (score, token) partials of the fused LM head (EPI_SAMPLE) to its sampled token:
 // one 256-thread workgroup per row, ties to the smallest token id (sample_final_kernel's rule).
 __global__ void __launch_bounds__(256) lm_sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,

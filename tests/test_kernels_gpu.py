@@ -900,6 +900,136 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
     assert err < 0.03, err
 
 
+@pytest.mark.parametrize("opsel", [0, 1, 2, 3])
+def test_mfma_scale_operand_semantics(opsel):
+    """What the MX hand-off assumes of v_mfma_scale_f32_16x16x128_f8f6f4's B scale: lane l of the
+    B operand (row l & 15, k-block l >> 4) scales its own 32-element block by 2^(byte - 127), the
+    byte being byte `op_sel` of that lane's scale word.  Prints the best-fitting model on failure."""
+    import itertools
+    from financial_chatbot_llm_amd.ops import _native as N
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(opsel)
+    # small integers (exact in e4m3) for A [16 rows, 128 k] and B [16 rows, 128 k]
+    Am = torch.randint(-3, 4, (16, 128), generator=g).float()
+    Bm = torch.randint(-3, 4, (16, 128), generator=g).float()
+    def lanes(M):   # lane l: row l & 15, k-block l >> 4 (32 bytes)
+        return torch.stack([M[l & 15, 32 * (l >> 4):32 * (l >> 4) + 32] for l in range(64)])
+    A8 = lanes(Am).to(moe.FP8).view(torch.uint8).contiguous().view(torch.int32)
+    B8 = lanes(Bm).to(moe.FP8).view(torch.uint8).contiguous().view(torch.int32)
+    sa = torch.full((64,), 127, dtype=torch.int32)
+    sbytes = torch.randint(125, 130, (64, 4), generator=g, dtype=torch.int32)
+    sb = (sbytes[:, 0] | sbytes[:, 1] << 8 | sbytes[:, 2] << 16 | sbytes[:, 3] << 24).to(torch.int32)
+    out = torch.zeros(256, dtype=torch.float32, device=DEV)
+    N.call("penny_probe_mfma_scale", N.ptr(A8.to(DEV)), N.ptr(B8.to(DEV)), N.ptr(sa.to(DEV)), N.ptr(sb.to(DEV)),
+           N.ptr(out), opsel, N.stream())
+    torch.cuda.synchronize()
+    o = out.cpu().view(64, 4)
+    C = torch.zeros(16, 16)
+    for l in range(64):
+        for r in range(4):
+            C[4 * (l >> 4) + r, l & 15] = o[l, r]
+    def model(byte):   # scale of B row j, k-block kb = byte `byte` of lane kb*16 + j
+        sc = torch.exp2((sbytes[:, byte].float() - 127)).view(4, 16)   # [kb, j]
+        ref = torch.zeros(16, 16)
+        for kb in range(4):
+            ref += (Am[:, 32 * kb:32 * kb + 32] @ Bm[:, 32 * kb:32 * kb + 32].t()) * sc[kb][None, :]
+        return ref
+    fits = {b: float((model(b) - C).abs().max()) for b in range(4)}
+    assert fits[opsel] == 0.0, fits
+
+
+def _mx_setup(T=600, E=4, H=512, F_=512, seed=9):
+    from financial_chatbot_llm_amd.ops import gemm, moe
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    w13 = (torch.randn((E, 2 * F_, H), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    w13 = torch.stack([gemm.interleave16(w13[e, :F_], w13[e, F_:]) for e in range(E)])
+    q13, s13 = moe.quantize_fp8_rowwise(w13)
+    w2 = (torch.randn((E, H, F_), device=DEV, generator=g) * 0.05).to(torch.bfloat16)
+    q2, s2 = moe.quantize_fp8_rowwise(w2)
+    h = torch.randn((T, H), device=DEV, generator=g).to(torch.bfloat16)
+    logits = (torch.randn((T, E), device=DEV, generator=g) * 2).to(torch.bfloat16)
+    xq, xs, offsets, tok_idx, tok_w, inv = moe.route_quant_device(h, logits, 2, E)
+    return q13.contiguous(), s13, q2.contiguous(), s2, xq, xs, offsets, tok_idx, tok_w, T * 2, E, H, F_
+
+
+def _mx_scale_of(mxs, offsets, P, E, F_):
+    """Decode the MX scale buffer into [P, F/32] exponents (the documented layout)."""
+    nkt = F_ // 128
+    off = offsets.cpu().tolist()
+    words = mxs.view(torch.uint8).cpu().view(-1, nkt, 4, 16, 4, 4)   # [tile][kt][wb][col][kblock][j]
+    X = torch.zeros((P, F_ // 32), dtype=torch.int32)
+    tm = 0
+    for e in range(E):
+        lo, hi = off[e], off[e + 1]
+        for m0 in range(lo, hi, 256):
+            for r in range(min(256, hi - m0)):
+                wb, j, col = r // 64, (r % 64) // 16, r % 16
+                X[m0 + r] = words[tm, :, wb, col, :, j].reshape(-1).to(torch.int32) - 127
+            tm += 1
+    return X
+
+
+def test_moe_mx_gemm1_writes_fp8_and_block_scales():
+    """GEMM1 of the MX hand-off alone: its e4m3 bytes x 2^X (X decoded from the scale layout) ==
+    MX fp8 rounding of the bf16 SiLU intermediate the per-row pipeline's GEMM1 writes."""
+    from financial_chatbot_llm_amd.ops import _native as N
+    from financial_chatbot_llm_amd.ops import moe
+    q13, s13, q2, s2, xq, xs, offsets, tok_idx, tok_w, P, E, H, F_ = _mx_setup()
+    st = N.stream()
+    a = torch.empty((P, F_), dtype=torch.bfloat16, device=DEV)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(q13),
+           N.ptr(s13), None, N.ptr(a), F_, P, E, 2 * F_, H, 7, st)
+    nkt = F_ // 128
+    mxs = torch.zeros((((P + 255) // 256 + E) * nkt * 256,), dtype=torch.int32, device=DEV)
+    aq = torch.zeros((P, F_), dtype=torch.uint8, device=DEV)
+    N.call("penny_moe_gemm_prefill_fp8_mx", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(q13),
+           N.ptr(s13), None, N.ptr(aq), F_, P, E, 2 * F_, H, 10, N.ptr(mxs), nkt, st)
+    X = _mx_scale_of(mxs, offsets, P, E, F_)
+    ref = moe._fake_quant_mx(a.float()).cpu()
+    got = (aq.view(moe.FP8).float().cpu().view(P, F_ // 32, 32) * torch.exp2(X.float())[..., None]).view(P, F_)
+    amax = a.float().cpu().view(P, F_ // 32, 32).abs().amax(-1)
+    want_X = torch.where(amax > 0, torch.ceil(torch.log2(amax / 448.0)), torch.full_like(amax, -127.0))
+    assert float((X.float() == want_X).float().mean()) > 0.999, (X[:2, :8], want_X[:2, :8])
+    assert torch.allclose(got, ref, rtol=0, atol=1e-6 + 0.0), float((got - ref).abs().max())
+
+
+def test_moe_mx_gemm2_applies_block_scales():
+    """GEMM2 of the MX hand-off alone on a hand-built intermediate: unit scales (E8M0 127) ==
+    the per-row GEMM2 at xs = 1; random scales == the fp32 reference of the scaled operand."""
+    from financial_chatbot_llm_amd.ops import _native as N
+    from financial_chatbot_llm_amd.ops import moe
+    q13, s13, q2, s2, xq, xs, offsets, tok_idx, tok_w, P, E, H, F_ = _mx_setup()
+    st = N.stream()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    aq = (torch.randn((P, F_), device=DEV, generator=g) * 20).to(moe.FP8).view(torch.uint8)
+    nkt = F_ // 128
+    ntile = (P + 255) // 256 + E
+    y_ref = torch.empty((P, H), dtype=torch.bfloat16, device=DEV)
+    ones = torch.ones(P, dtype=torch.float32, device=DEV)
+    N.call("penny_moe_gemm_prefill_fp8", N.ptr(aq), F_, None, N.ptr(ones), N.ptr(offsets), N.ptr(q2), N.ptr(s2),
+           N.ptr(tok_w), N.ptr(y_ref), H, P, E, H, F_, 8, st)
+    for mode in ("unit", "random"):
+        if mode == "unit":
+            mxs = torch.full((ntile * nkt * 1024,), 127, dtype=torch.uint8, device=DEV)
+        else:
+            mxs = torch.randint(124, 131, (ntile * nkt * 1024,), dtype=torch.uint8, device=DEV, generator=g)
+        y = torch.empty((P, H), dtype=torch.bfloat16, device=DEV)
+        N.call("penny_moe_gemm_prefill_fp8_mx", N.ptr(aq), F_, None, None, N.ptr(offsets), N.ptr(q2), N.ptr(s2),
+               N.ptr(tok_w), N.ptr(y), H, P, E, H, F_, 11, N.ptr(mxs.view(torch.int32)), nkt, st)
+        if mode == "unit":
+            assert torch.equal(y, y_ref), float((y.float() - y_ref.float()).abs().max())
+        else:
+            X = _mx_scale_of(mxs.view(torch.int32), offsets, P, E, F_).to(DEV)
+            xd = (aq.view(moe.FP8).float().view(P, F_ // 32, 32) * torch.exp2(X.float())[..., None]).view(P, F_)
+            off = offsets.cpu().tolist()
+            ref = torch.zeros((P, H), device=DEV)
+            for e in range(E):
+                lo, hi = off[e], off[e + 1]
+                ref[lo:hi] = (xd[lo:hi] @ (q2[e].float() * s2[e][:, None]).t()) * tok_w[lo:hi, None]
+            err = float((y.float() - ref).abs().max() / ref.abs().max())
+            assert err < 0.01, err
+
+
 @pytest.mark.parametrize("T,E", [(1000, 8), (3001, 4)])
 def test_moe_prefill_mx_handoff(T, E, monkeypatch):
     """MX hand-off of the fp8 tile pipeline (GEMM1 epilogue writes the SiLU intermediate as e4m3 +
