@@ -13,7 +13,8 @@ step() {  # name, timeout, command...
   tail -3 "gpurun_out/$name.log"
   return $rc
 }
-step t_pf 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "prefill_attention or moe_prefill or moe_grouped or mx_handoff" || exit 1
+step t_pf 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "prefill_attention or moe_prefill_fp8 or moe_grouped or route_quant" || exit 1
+step t_mx 200 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "mfma_scale_operand or mx_gemm or mx_handoff"
 step b_pf 300 python -u -m financial_chatbot_llm_amd.bench.kernels --only prefill_mixed --out gpurun_out/prefill_mixed_v2.jsonl || exit 1
 step pmc_tiles 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \
      --kernel-trace --output-format csv -d gpurun_out/pmc_tiles -o run -- \

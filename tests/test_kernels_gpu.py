@@ -130,7 +130,7 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
     # respond chunk behind a cached prefix + decide-like and spec-like chunks (dead waves: 17 x 4 rows)
     (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
@@ -139,8 +139,8 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     (12, 12, 64, False, [(200, 200), (33, 33)], 1.0),         # bidirectional, D = 64
 ])
 def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, qscale):
-    """The ping-pong kernel (prefill3, variants 1-3) and prefill2 (0) vs the fp32 reference, with the
-    LPT work list and without (also the lse output)."""
+    """The ping-pong kernel (prefill3, variants 1-3), prefill2 (0) and prefill2 with pinned fragment
+    prefetch (4) vs the fp32 reference, with the LPT work list and without (also the lse output)."""
     g = torch.Generator().manual_seed(40 + variant)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
@@ -165,15 +165,17 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
         ops.attention.prefill_variant(old)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 4])
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
     (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
     (8, 1, 128, True, [(40, 1500), (33, 500)]),
     (12, 12, 64, False, [(200, 700), (33, 33)]),
 ])
-def test_prefill_attention_lean_split_kv(min_chunk, Hq, Hkv, D, causal, lens):
+def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal, lens):
     """Lean prefill: the KV walks of long tiles cut into chunks on different workgroups, partial
-    (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse)."""
+    (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse), on the prefill2
+    (0, 4) and ping-pong (1) kernels."""
     g = torch.Generator().manual_seed(50 + min_chunk)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
@@ -189,9 +191,13 @@ def test_prefill_attention_lean_split_kv(min_chunk, Hq, Hkv, D, causal, lens):
                                          min_chunk=min_chunk)
     assert wl is not None and int(wl[0, 2]) > 0                 # some tiles were split
     lse = torch.empty(q.shape[0], Hq, device=DEV)
-    out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, causal,
-                      max_q_len=max(qlens), lse=lse, work=torch.from_numpy(wl).to(DEV),
-                      lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])))
+    old = ops.attention.prefill_variant(variant)
+    try:
+        out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, causal,
+                          max_q_len=max(qlens), lse=lse, work=torch.from_numpy(wl).to(DEV),
+                          lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])))
+    finally:
+        ops.attention.prefill_variant(old)
     close(out, ref, atol=2e-2)
     close(lse, lse_ref, atol=2e-2, rtol=1e-3)
 
