@@ -1359,15 +1359,16 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   PENNY_RETURN_LAUNCH();
 }
 
-// Big-tile prefill variant: 0 (default) prefill2, 1 ping-pong prefill3 with ones-MFMA row sums,
-// 2 ping-pong with VALU row sums, 3 = 1 + static priority for waves 4-7, 4 = prefill2 with its K/V
-// fragment prefetch pinned ahead of the MFMAs (PENNY_PREFILL_PP, or
-// penny_attention_prefill_variant for in-process A/B runs)
+// Big-tile prefill variant: 4 (default) prefill2 with its K/V fragment prefetch pinned ahead of the
+// MFMAs (+4-6 % over 0 on the workload's steps, profiles/r4_prefill_attn_pinned_prefetch_variant4.jsonl),
+// 0 prefill2, 1 ping-pong prefill3 with ones-MFMA row sums, 2 ping-pong with VALU row sums,
+// 3 = 1 + static priority for waves 4-7 (PENNY_PREFILL_PP, or penny_attention_prefill_variant for
+// in-process A/B runs)
 static int g_prefill_variant = -1;
 static int prefill_variant() {
   if (g_prefill_variant < 0) {
     const char* v = getenv("PENNY_PREFILL_PP");
-    g_prefill_variant = v ? atoi(v) : 0;
+    g_prefill_variant = v ? atoi(v) : 4;
   }
   return g_prefill_variant;
 }

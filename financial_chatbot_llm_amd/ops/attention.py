@@ -138,8 +138,10 @@ def rope_qk(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor, H
     T = qkv.shape[0]
     if N.use_native(qkv):
         qk = torch.empty((T, Hq + Hkv, D), dtype=qkv.dtype, device=qkv.device)
-        N.call("penny_rope_qk", N.ptr(qkv.contiguous()), N.ptr(positions.to(torch.int32).contiguous()),
-               N.ptr(cos_sin), N.ptr(qk), T, Hq, Hkv, D, N.stream())
+        # converted inputs bound to names: a temporary passed as N.ptr(x.contiguous()) is freed before
+        # the launch, and the next temporary's copy can reuse (overwrite) its block on the stream
+        src, pos = qkv.contiguous(), positions.to(torch.int32).contiguous()
+        N.call("penny_rope_qk", N.ptr(src), N.ptr(pos), N.ptr(cos_sin), N.ptr(qk), T, Hq, Hkv, D, N.stream())
         return qk
     return _rope_ref(qkv.view(T, -1, D)[:, :Hq + Hkv], positions, cos_sin).to(qkv.dtype)
 
@@ -257,9 +259,9 @@ def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, 
 
 def prefill_plan(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causal: bool = True,
                  cus: int = 256) -> Optional[np.ndarray]:
-    """The step's prefill-attention work list: lean ([., 6], when the ping-pong kernel is selected
-    and some walk needs splitting) or whole tiles in LPT order ([n, 2])."""
-    if PREFILL_LEAN and prefill_variant() == 1:
+    """The step's prefill-attention work list: lean ([., 6], when some walk needs splitting; the
+    prefill2 and ping-pong kernels take it) or whole tiles in LPT order ([n, 2])."""
+    if PREFILL_LEAN and prefill_variant() in (0, 1, 4):
         lean = prefill_lean_list(cu_q, ctx_lens, G, Hkv, causal, cus)
         if lean is not None:
             return lean
@@ -283,9 +285,9 @@ def _lean_workspace(dev: torch.device, slots: int, Hkv: int, D: int) -> Tuple[to
 
 def prefill_variant(v: int = -1) -> int:
     """Select the big-tile prefill kernel for this process (returns the previous choice; -1 only
-    reads it): 1 = ping-pong prefill3 with ones-MFMA row sums (default), 2 = ping-pong with VALU
-    row sums, 3 = 1 + static priority for waves 4-7, 0 = prefill2 (``PENNY_PREFILL_PP`` sets the
-    initial value).  In-process A/B runs and tests only."""
+    reads it): 4 = prefill2 with pinned K/V fragment prefetch (default), 0 = prefill2, 1 = ping-pong
+    prefill3 with ones-MFMA row sums, 2 = ping-pong with VALU row sums, 3 = 1 + static priority for
+    waves 4-7 (``PENNY_PREFILL_PP`` sets the initial value).  In-process A/B runs and tests only."""
     return int(N.load().penny_attention_prefill_variant(int(v)))
 
 

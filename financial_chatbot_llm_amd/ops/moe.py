@@ -279,7 +279,8 @@ def silu_quant_rows_fp8(gu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         return quant_rows_fp8(silu_mul(gu, interleave16=True))
     q = torch.empty((M, F2 // 2), dtype=torch.uint8, device=gu.device)
     s = torch.empty(M, dtype=torch.float32, device=gu.device)
-    N.call("penny_silu_quant_rows_fp8", N.ptr(gu.contiguous()), M, F2 // 2, N.ptr(q), N.ptr(s), N.stream())
+    src = gu.contiguous()                      # alive across the launch
+    N.call("penny_silu_quant_rows_fp8", N.ptr(src), M, F2 // 2, N.ptr(q), N.ptr(s), N.stream())
     return q.view(FP8), s
 
 

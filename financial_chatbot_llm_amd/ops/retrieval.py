@@ -65,10 +65,12 @@ def filtered_topk(corpus: torch.Tensor, user_codes: torch.Tensor, dates: torch.T
     out_scores = torch.zeros((nq, kmax), dtype=torch.float32, device=corpus.device)
     out_count = torch.empty((nq,), dtype=torch.int32, device=corpus.device)
     queries = queries.to(torch.bfloat16).contiguous()
+    # converted inputs bound to names: as N.ptr(x.to(...)) temporaries they would be freed before
+    # the launch and the next conversion could reuse (overwrite) their memory on the stream
+    qu, qf, kk = q_user.to(torch.int32).contiguous(), q_floor.to(torch.int64).contiguous(), ks.to(torch.int32).contiguous()
     N.call("penny_filtered_topk", N.ptr(corpus), N.ptr(user_codes), N.ptr(dates), corpus.shape[0], D,
-           N.ptr(queries), N.ptr(q_user.to(torch.int32)), N.ptr(q_floor.to(torch.int64)),
-           N.ptr(ks.to(torch.int32)), nq, kmax, N.ptr(counts), N.ptr(cand), N.ptr(scores), cap, N.ptr(out_ids),
-           N.ptr(out_scores), N.ptr(out_count), N.stream())
+           N.ptr(queries), N.ptr(qu), N.ptr(qf), N.ptr(kk), nq, kmax, N.ptr(counts), N.ptr(cand), N.ptr(scores), cap,
+           N.ptr(out_ids), N.ptr(out_scores), N.ptr(out_count), N.stream())
     oc = out_count.cpu()
     big = (oc < 0).nonzero().flatten().tolist()
     for i in big:  # > SORT_CAP candidates: finish on device with torch.topk

@@ -94,9 +94,9 @@ def lm_head_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor,
         return sample(F.linear(h.float(), w.float()).to(h.dtype), temperatures, seeds, out=out)
     out = torch.empty((M,), dtype=torch.int32, device=h.device) if out is None else out
     ws = torch.empty((2 * M * 2 * (V // 256),), dtype=torch.float32, device=h.device)
-    N.call("penny_lm_head_sample", N.ptr(h), h.stride(0), N.ptr(w), K, M, V,
-           N.ptr(temperatures.to(torch.float32).contiguous()), N.ptr(seeds.contiguous()), N.ptr(ws), N.ptr(out),
-           N.stream())
+    temps, sd = temperatures.to(torch.float32).contiguous(), seeds.contiguous()   # alive across the launch
+    N.call("penny_lm_head_sample", N.ptr(h), h.stride(0), N.ptr(w), K, M, V, N.ptr(temps), N.ptr(sd), N.ptr(ws),
+           N.ptr(out), N.stream())
     return out
 
 
@@ -145,9 +145,9 @@ def lm_head_sample_shard(h: torch.Tensor, w_pad: torch.Tensor, vvalid: int, voff
     Vpad = w_pad.shape[0]
     pairs = torch.empty((M, 2), dtype=torch.int32, device=h.device)
     ws = torch.empty((2 * M * 2 * (Vpad // 256),), dtype=torch.float32, device=h.device)
+    temps, sd = temperatures.to(torch.float32).contiguous(), seeds.contiguous()   # alive across the launch
     N.call("penny_lm_head_sample_shard", N.ptr(h), h.stride(0), N.ptr(w_pad), K, M, Vpad, int(vvalid), int(voff),
-           N.ptr(temperatures.to(torch.float32).contiguous()), N.ptr(seeds.contiguous()), N.ptr(ws), N.ptr(pairs),
-           N.stream())
+           N.ptr(temps), N.ptr(sd), N.ptr(ws), N.ptr(pairs), N.stream())
     return pairs
 
 
@@ -166,9 +166,9 @@ def topk_topp_threshold(logits: torch.Tensor, temperatures: torch.Tensor, top_k:
     """The HIP filter's per-row logit threshold (-inf: keep all) -- diagnostics/tests."""
     B, V = logits.shape
     th = torch.empty((B,), dtype=torch.float32, device=logits.device)
+    tk, tp = top_k.to(torch.int32).contiguous(), top_p.to(torch.float32).contiguous()   # alive across the launch
     N.call("penny_topk_topp_threshold", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
-           N.ptr(temperatures), N.ptr(top_k.to(torch.int32).contiguous()),
-           N.ptr(top_p.to(torch.float32).contiguous()), N.ptr(th), B, V, N.stream())
+           N.ptr(temperatures), N.ptr(tk), N.ptr(tp), N.ptr(th), B, V, N.stream())
     return th
 
 

@@ -926,8 +926,8 @@ def test_mfma_scale_operand_semantics(opsel):
     sbytes = torch.randint(125, 130, (64, 4), generator=g, dtype=torch.int32)
     sb = (sbytes[:, 0] | sbytes[:, 1] << 8 | sbytes[:, 2] << 16 | sbytes[:, 3] << 24).to(torch.int32)
     out = torch.zeros(256, dtype=torch.float32, device=DEV)
-    N.call("penny_probe_mfma_scale", N.ptr(A8.to(DEV)), N.ptr(B8.to(DEV)), N.ptr(sa.to(DEV)), N.ptr(sb.to(DEV)),
-           N.ptr(out), opsel, N.stream())
+    Ad, Bd, sad, sbd = A8.to(DEV), B8.to(DEV), sa.to(DEV), sb.to(DEV)      # alive across the launch
+    N.call("penny_probe_mfma_scale", N.ptr(Ad), N.ptr(Bd), N.ptr(sad), N.ptr(sbd), N.ptr(out), opsel, N.stream())
     torch.cuda.synchronize()
     o = out.cpu().view(64, 4)
     C = torch.zeros(16, 16)
