@@ -564,8 +564,14 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     // GEMM1 of the MX hand-off: SiLU(gate) * up with EPI_MOE_SILU's roundings, then per (row,
     // 32-column block) an E8M0 scale 2^X, X = ceil(log2(amax / 448)) (no saturation), and the
     // block's e4m3 bytes of value / 2^X -- the intermediate leaves as fp8 (half the bytes of bf16)
-    // and GEMM2 reads it without a per-row quantisation pass.  A block's 32 columns are lanes
-    // g = 0..3 (4 each) x two column groups q: amax is two xor-shuffles over g.
+    // and GEMM2 reads it without a per-row quantisation pass.
+    // The blocks are the ones the block-scaled MFMA scales together with the fragment layout of
+    // GEMM2 (lane group g holds 16-B chunks 2g, 2g+1 of the 128-B K-tile row): measured
+    // (tests/test_kernels_gpu.py test_mfma_scale_operand_map_dump), the scale of lane group g'
+    // covers chunks {0,2}, {4,6}, {1,3}, {5,7} for g' = 0..3 -- i.e. in this
+    // wave's 4 column groups q (16 columns each; wave wa holds chunks 4wa..4wa+3) block bb takes
+    // q = bb and bb + 2, and its scale is k-block g' = wa + 2bb.  A block's 32 columns are lanes
+    // g = 0..3 (4 each) x the two q: amax is two xor-shuffles over g.
     const float* wsc = ma.ws + (long)e * N + n0 + wa * 128;
     unsigned char* yq = static_cast<unsigned char*>(Y);
     const int ocol = ((n0 + wa * 128) >> 1) + 4 * g;        // this lane's first output column
@@ -592,7 +598,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       for (int bb = 0; bb < 2; ++bb) {
         float amax = 0.f;
 #pragma unroll
-        for (int q = 2 * bb; q < 2 * bb + 2; ++q)
+        for (int q = bb; q < 4; q += 2)
 #pragma unroll
           for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(o[q][r]));
         amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
@@ -605,7 +611,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
         const float inv = __uint_as_float((unsigned)(127 - X) << 23);   // 2^-X, exact
         if (valid) {
 #pragma unroll
-          for (int q = 2 * bb; q < 2 * bb + 2; ++q) {
+          for (int q = bb; q < 4; q += 2) {
             uint32_t pk = 0;
             pk = __builtin_amdgcn_cvt_pk_fp8_f32(o[q][0] * inv, o[q][1] * inv, pk, false);
             pk = __builtin_amdgcn_cvt_pk_fp8_f32(o[q][2] * inv, o[q][3] * inv, pk, true);
@@ -614,10 +620,10 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
         }
       }
     }
-    // lane g < 2 stores block g's scale word: rows wb*64 + 16j + col (byte j), k-block wa*2 + g of
+    // lane g < 2 stores block g's scale word: rows wb*64 + 16j + col (byte j), k-block wa + 2g of
     // GEMM2's K-tile n0 / 256
     if (g < 2)
-      ma.mxs[((long)tm * ma.nkt + n0 / 256) * 256 + wb * 64 + col * 4 + wa * 2 + g] = g == 0 ? word[0] : word[1];
+      ma.mxs[((long)tm * ma.nkt + n0 / 256) * 256 + wb * 64 + col * 4 + wa + 2 * g] = g == 0 ? word[0] : word[1];
     return;
   }
 #pragma unroll

@@ -340,15 +340,37 @@ def _fake_quant_rows(x: torch.Tensor) -> torch.Tensor:
     return q.float() * s[..., None]
 
 
-def _fake_quant_mx(x: torch.Tensor) -> torch.Tensor:
-    """Round-trip rows through MX fp8: per 32-column block an E8M0 scale 2^X with
-    X = ceil(log2(amax / 448)), e4m3 of value / 2^X (the GEMM1 epilogue of the MX hand-off)."""
+# the 16-column chunks of a 128-column K-tile that one E8M0 scale of the block-scaled MFMA covers,
+# with the tile kernel's fp8 fragment layout (lane group g: chunks 2g, 2g + 1): measured on the
+# GPU (tests/test_kernels_gpu.py test_mfma_scale_operand_map_dump) -- scale k-block b of a chunk
+MX_CHUNK_BLOCK = (0, 2, 0, 2, 1, 3, 1, 3)
+
+
+def mx_blocks(x: torch.Tensor) -> torch.Tensor:
+    """[R, C] -> [R, C / 128, 4 k-blocks, 32] in the MFMA's scale-block grouping (MX_CHUNK_BLOCK)."""
     R, C = x.shape
-    b = x.float().view(R, C // 32, 32)
+    ch = x.reshape(R, C // 128, 8, 16)
+    order = [c for b in range(4) for c in range(8) if MX_CHUNK_BLOCK[c] == b]
+    return ch[:, :, order].reshape(R, C // 128, 4, 32)
+
+
+def mx_unblocks(b: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`mx_blocks`."""
+    R, T = b.shape[0], b.shape[1]
+    order = [c for k in range(4) for c in range(8) if MX_CHUNK_BLOCK[c] == k]
+    inv = [order.index(c) for c in range(8)]
+    return b.reshape(R, T, 8, 16)[:, :, inv].reshape(R, T * 128)
+
+
+def _fake_quant_mx(x: torch.Tensor) -> torch.Tensor:
+    """Round-trip rows through MX fp8 as the hand-off does: per scale block (32 columns grouped as
+    the block-scaled MFMA groups them, :func:`mx_blocks`) an E8M0 scale 2^X with
+    X = ceil(log2(amax / 448)), e4m3 of value / 2^X (the GEMM1 epilogue of the MX hand-off)."""
+    b = mx_blocks(x.float())
     amax = b.abs().amax(-1, keepdim=True)
     X = torch.where(amax > 0, torch.ceil(torch.log2(amax / FP8_MAX)), torch.full_like(amax, -127.0)).clamp(-127, 126)
     sc = torch.exp2(X)
-    return ((b / sc).to(FP8).float() * sc).view(R, C)
+    return mx_unblocks((b / sc).to(FP8).float() * sc)
 
 
 def moe_fp8_reference(h, router_w, w13q, s13, w2q, s2, top_k, quant_act=False):

@@ -906,11 +906,46 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
     assert err < 0.03, err
 
 
+def test_mfma_scale_operand_map_dump():
+    """Maps, for every (op_sel, lane, byte) of the B scale word, which accumulator entries it
+    scales (one byte raised to 2^1 at a time) and writes the raw results to gpurun_out/ for the
+    offline fit (diagnostic; asserts only that every experiment ran)."""
+    from financial_chatbot_llm_amd.ops import _native as N
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(11)
+    Am = torch.randint(1, 4, (16, 128), generator=g).float()
+    Bm = torch.randint(1, 4, (16, 128), generator=g).float()
+    def lanes(M):
+        return torch.stack([M[l & 15, 32 * (l >> 4):32 * (l >> 4) + 32] for l in range(64)])
+    Ad = lanes(Am).to(moe.FP8).view(torch.uint8).contiguous().view(torch.int32).to(DEV)
+    Bd = lanes(Bm).to(moe.FP8).view(torch.uint8).contiguous().view(torch.int32).to(DEV)
+    sad = torch.full((64,), 127, dtype=torch.int32, device=DEV)
+    base_word = 127 | 127 << 8 | 127 << 16 | 127 << 24
+    res = torch.zeros((4, 65, 4, 64, 4), dtype=torch.float32)
+    for opsel in range(4):
+        for lane in range(65):                 # lane 64: no change (baseline)
+            for byte in range(4):
+                sb = torch.full((64,), base_word, dtype=torch.int64)
+                if lane < 64:
+                    sb[lane] = base_word + (1 << (8 * byte))
+                sbd = sb.to(torch.int32).to(DEV)
+                out = torch.zeros(256, dtype=torch.float32, device=DEV)
+                N.call("penny_probe_mfma_scale", N.ptr(Ad), N.ptr(Bd), N.ptr(sad), N.ptr(sbd), N.ptr(out), opsel,
+                       N.stream())
+                torch.cuda.synchronize()
+                res[opsel, lane, byte] = out.cpu().view(64, 4)
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    torch.save({"A": Am, "B": Bm, "res": res}, "gpurun_out/mfma_scale_probe.pt")
+    assert torch.isfinite(res).all()
+
+
 @pytest.mark.parametrize("opsel", [0, 1, 2, 3])
 def test_mfma_scale_operand_semantics(opsel):
-    """What the MX hand-off assumes of v_mfma_scale_f32_16x16x128_f8f6f4's B scale: lane l of the
-    B operand (row l & 15, k-block l >> 4) scales its own 32-element block by 2^(byte - 127), the
-    byte being byte `op_sel` of that lane's scale word.  Prints the best-fitting model on failure."""
+    """What the MX hand-off relies on in v_mfma_scale_f32_16x16x128_f8f6f4's B scale (measured with
+    test_mfma_scale_operand_map_dump): byte `op_sel` of lane l's scale word scales column l & 15
+    over the 16-element k chunks c of the fragment layout (lane l: row l & 15, chunks 2(l>>4),
+    2(l>>4)+1) with moe.MX_CHUNK_BLOCK[c] == l >> 4 -- NOT the lane's own 32 elements."""
     import itertools
     from financial_chatbot_llm_amd.ops import _native as N
     from financial_chatbot_llm_amd.ops import moe
@@ -934,11 +969,11 @@ def test_mfma_scale_operand_semantics(opsel):
     for l in range(64):
         for r in range(4):
             C[4 * (l >> 4) + r, l & 15] = o[l, r]
-    def model(byte):   # scale of B row j, k-block kb = byte `byte` of lane kb*16 + j
-        sc = torch.exp2((sbytes[:, byte].float() - 127)).view(4, 16)   # [kb, j]
+    def model(byte):   # chunk c of column j scaled by byte `byte` of lane MX_CHUNK_BLOCK[c]*16 + j
+        sc = torch.exp2((sbytes[:, byte].float() - 127)).view(4, 16)   # [block, j]
         ref = torch.zeros(16, 16)
-        for kb in range(4):
-            ref += (Am[:, 32 * kb:32 * kb + 32] @ Bm[:, 32 * kb:32 * kb + 32].t()) * sc[kb][None, :]
+        for c in range(8):
+            ref += (Am[:, 16 * c:16 * c + 16] @ Bm[:, 16 * c:16 * c + 16].t()) * sc[moe.MX_CHUNK_BLOCK[c]][None, :]
         return ref
     fits = {b: float((model(b) - C).abs().max()) for b in range(4)}
     assert fits[opsel] == 0.0, fits
@@ -959,11 +994,11 @@ def _mx_setup(T=600, E=4, H=512, F_=512, seed=9):
 
 
 def _mx_scale_of(mxs, offsets, P, E, F_):
-    """Decode the MX scale buffer into [P, F/32] exponents (the documented layout)."""
+    """Decode the MX scale buffer into [P, F/128, 4] exponents (per K-tile and MFMA scale block)."""
     nkt = F_ // 128
     off = offsets.cpu().tolist()
     words = mxs.view(torch.uint8).cpu().view(-1, nkt, 4, 16, 4, 4)   # [tile][kt][wb][col][kblock][j]
-    X = torch.zeros((P, F_ // 32), dtype=torch.int32)
+    X = torch.zeros((P, nkt * 4), dtype=torch.int32)
     tm = 0
     for e in range(E):
         lo, hi = off[e], off[e + 1]
@@ -990,12 +1025,12 @@ def test_moe_mx_gemm1_writes_fp8_and_block_scales():
     aq = torch.zeros((P, F_), dtype=torch.uint8, device=DEV)
     N.call("penny_moe_gemm_prefill_fp8_mx", N.ptr(xq), H, N.ptr(tok_idx), N.ptr(xs), N.ptr(offsets), N.ptr(q13),
            N.ptr(s13), None, N.ptr(aq), F_, P, E, 2 * F_, H, 10, N.ptr(mxs), nkt, st)
-    X = _mx_scale_of(mxs, offsets, P, E, F_)
+    X = _mx_scale_of(mxs, offsets, P, E, F_).view(P, F_ // 128, 4)
     ref = moe._fake_quant_mx(a.float()).cpu()
-    got = (aq.view(moe.FP8).float().cpu().view(P, F_ // 32, 32) * torch.exp2(X.float())[..., None]).view(P, F_)
-    amax = a.float().cpu().view(P, F_ // 32, 32).abs().amax(-1)
+    got = moe.mx_unblocks(moe.mx_blocks(aq.view(moe.FP8).float().cpu()) * torch.exp2(X.float())[..., None])
+    amax = moe.mx_blocks(a.float().cpu()).abs().amax(-1)
     want_X = torch.where(amax > 0, torch.ceil(torch.log2(amax / 448.0)), torch.full_like(amax, -127.0))
-    assert float((X.float() == want_X).float().mean()) > 0.999, (X[:2, :8], want_X[:2, :8])
+    assert float((X.float() == want_X).float().mean()) > 0.999, (X[:2, :2], want_X[:2, :2])
     assert torch.allclose(got, ref, rtol=0, atol=1e-6 + 0.0), float((got - ref).abs().max())
 
 
@@ -1025,8 +1060,8 @@ def test_moe_mx_gemm2_applies_block_scales():
         if mode == "unit":
             assert torch.equal(y, y_ref), float((y.float() - y_ref.float()).abs().max())
         else:
-            X = _mx_scale_of(mxs.view(torch.int32), offsets, P, E, F_).to(DEV)
-            xd = (aq.view(moe.FP8).float().view(P, F_ // 32, 32) * torch.exp2(X.float())[..., None]).view(P, F_)
+            X = _mx_scale_of(mxs.view(torch.int32), offsets, P, E, F_).to(DEV).view(P, F_ // 128, 4)
+            xd = moe.mx_unblocks(moe.mx_blocks(aq.view(moe.FP8).float()) * torch.exp2(X.float())[..., None])
             off = offsets.cpu().tolist()
             ref = torch.zeros((P, H), device=DEV)
             for e in range(E):
