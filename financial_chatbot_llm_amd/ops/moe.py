@@ -29,7 +29,7 @@ PREFILL_TILES = os.environ.get("PENNY_MOE_PREFILL_TILES", "1") != "0"
 TILE_SCHED = 16 if os.environ.get("PENNY_MOE_TILE_SCHED", "balanced") == "plain" else 0
 # prefill tiles: the SiLU intermediate handed from GEMM1 to GEMM2 as MX fp8 (e4m3 + one E8M0 scale per
 # 32 columns, written by GEMM1's epilogue) instead of bf16 + a per-row quantisation pass
-MX_HANDOFF = os.environ.get("PENNY_MOE_MX", "0") == "1"
+MX_HANDOFF = os.environ.get("PENNY_MOE_MX", "1") == "1"
 # expert-parallel receives of at least this many rows run moe_grouped_fp8_tiles
 EP_TILE_MIN_ROWS = int(os.environ.get("PENNY_EP_TILE_MIN_ROWS", "512"))
 

@@ -1110,8 +1110,21 @@ def test_moe_prefill_mx_handoff(T, E, monkeypatch):
     # an activation on the other side of an e4m3 rounding boundary moves single outputs: bound
     # the mean (as the other fp8 pipeline tests do)
     assert float(err.mean()) < 0.01 * float(ref.abs().mean()) + 1e-4, (float(err.mean()), float(ref.abs().mean()))
-    # per-32-column scales are at least as fine as per-row ones: no worse than the row-quantised pipe
-    assert float((got - rowq).abs().mean()) < 0.03 * float(rowq.abs().mean())
+    # accuracy: against the same pipeline with an UNquantised intermediate, the MX hand-off (scale
+    # per 32 values) is no worse than the per-row quantisation it replaces
+    exact = torch.zeros((T, H), device=DEV)
+    for e in range(E):
+        sel = (topi == e)
+        rows = sel.any(1).nonzero().flatten()
+        if rows.numel() == 0:
+            continue
+        w13d = q13[e].float() * s13[e][:, None]
+        w2d = q2[e].float() * s2[e][:, None]
+        a = gemm.silu_mul((xd[rows] @ w13d.t()).to(torch.bfloat16), interleave16=True).float()
+        exact[rows] += (topw * sel).sum(1)[rows][:, None] * (a @ w2d.t())
+    e_mx = float((got - exact).abs().mean())
+    e_row = float((rowq - exact).abs().mean())
+    assert e_mx <= 1.1 * e_row, (e_mx, e_row)
 
 
 def test_moe_grouped_fp8_tiles_matches_reference():
