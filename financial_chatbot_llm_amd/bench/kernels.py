@@ -230,6 +230,9 @@ MIXED_STEPS = {
     "16decides": [(200, 4800)] * 16,
     "respond-long": [(2400, 6400), (1600, 5200)],
     "first-turn": [(4096, 4096)],
+    "1decide": [(220, 4600)],
+    "2decides": [(230, 4700), (210, 4500)],
+    "1respond-short": [(600, 4200)],
 }
 
 
@@ -268,15 +271,16 @@ def bench_prefill_mixed(dev) -> List[Dict]:
 
         def run(v):
             def f():
-                if v == "lean":
-                    ops.attention.prefill_variant(1)
+                if isinstance(v, str):
+                    ops.attention.prefill_variant(int(v.split("_")[1]))
                     ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
                                 work=ld if ld is not None else wd, lean=lc)
                     return
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean"}
+        variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean_1",
+                    "pf2_sb_lean": "lean_4"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():

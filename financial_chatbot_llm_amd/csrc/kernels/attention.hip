@@ -1269,8 +1269,12 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   }
 }
 
-// Merge the chunk partials of split tiles (lean prefill): grid (splits, Hkv), 256 threads; wave
-// rows: lanes 0-31 / 32-63 take two rows, 4 dims per lane (f32x4), so every load is coalesced.
+// Merge the chunk partials of split tiles (lean prefill): grid (splits, Hkv, 256 / RPB), 256
+// threads, one row per thread group: lanes 0-31 / 32-63 take two rows (D = 128), 4 dims per lane
+// (f32x4), so every load is coalesced.  A single-tile step splits its walk into up to ~32 chunks;
+// a row per thread group (instead of 32 rows looped per workgroup) keeps the slot loads
+// independent and in flight together -- the looped form was latency-bound at 126 us per merge
+// (profiles/r4_bench_kernel_stats_head.md).
 // merge [n, 6]: sequence, tile, first slot, number of slots, 0, 0 (chunk order = slot order).
 template <int D>
 __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restrict__ merge, const int* __restrict__ cu_q,
@@ -1280,35 +1284,39 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
   static_assert(D == 128 || D == 64, "head dim");
   constexpr int LPR = D / 4;                  // lanes per row
   constexpr int RPW = 64 / LPR;               // rows per wave instruction
+  constexpr int RPB = 4 * RPW;                // rows per workgroup
   const int* mg = merge + 6 * blockIdx.x;
   const int s = mg[0], tile = mg[1], slot0 = mg[2], np = mg[3];
   const int h = blockIdx.y, G = Hq / Hkv, TQ = 256 / G;
   const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int sub = lane / LPR, d = (lane % LPR) * 4;
-  for (int r = w * RPW + sub; r < 256; r += 4 * RPW) {
-    const int tok = tile * TQ + r / G;
-    if (tok >= qlen) continue;
-    float M = -INFINITY;
-    for (int i = 0; i < np; ++i) M = fmaxf(M, part_ml[2 * (((long)(slot0 + i) * Hkv + h) * 256 + r)]);
-    float L = 0.f;
-    f32x4 O = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < np; ++i) {
-      const long pr = ((long)(slot0 + i) * Hkv + h) * 256 + r;
-      const float mi = part_ml[2 * pr];
-      const float f = mi == -INFINITY ? 0.f : exp2f(mi - M);
-      L += part_ml[2 * pr + 1] * f;
-      O += *reinterpret_cast<const f32x4*>(part_o + pr * D + d) * f;
-    }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    const int head = h * G + r % G;
-    bf16x4 v4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v4[k] = (bf16)(O[k] * inv);
-    *reinterpret_cast<bf16x4*>(out + ((long)(q0 + tok) * Hq + head) * D + d) = v4;
-    if (lse != nullptr && d == 0)
-      lse[(long)(q0 + tok) * Hq + head] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
+  const int r = blockIdx.z * RPB + w * RPW + sub;
+  const int tok = tile * TQ + r / G;
+  if (tok >= qlen) return;
+  const long stride = (long)Hkv * 256;        // rows between consecutive slots
+  const long pr0 = ((long)slot0 * Hkv + h) * 256 + r;
+  float M = -INFINITY;
+#pragma unroll 8
+  for (int i = 0; i < np; ++i) M = fmaxf(M, part_ml[2 * (pr0 + i * stride)]);
+  float L = 0.f;
+  f32x4 O = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int i = 0; i < np; ++i) {
+    const long pr = pr0 + i * stride;
+    const float mi = part_ml[2 * pr];
+    const float f = mi == -INFINITY ? 0.f : exp2f(mi - M);
+    L += part_ml[2 * pr + 1] * f;
+    O += *reinterpret_cast<const f32x4*>(part_o + pr * D + d) * f;
   }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int head = h * G + r % G;
+  bf16x4 v4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v4[k] = (bf16)(O[k] * inv);
+  *reinterpret_cast<bf16x4*>(out + ((long)(q0 + tok) * Hq + head) * D + d) = v4;
+  if (lse != nullptr && d == 0)
+    lse[(long)(q0 + tok) * Hq + head] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
 }
 
 static int prefill_variant();
@@ -1337,21 +1345,21 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                          (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
                          (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
     if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv, 32), dim3(256), 0, stream, merge, cu_q, part_o,
                          part_ml, (bf16*)out, lse, Hq, Hkv);
   } else if (D == 128) {
     hipLaunchKernelGGL((prefill3_kernel<128, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
     if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv, 32), dim3(256), 0, stream, merge, cu_q, part_o,
                          part_ml, (bf16*)out, lse, Hq, Hkv);
   } else if (D == 64) {
     hipLaunchKernelGGL((prefill3_kernel<64, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
     if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<64>, dim3(nmerge, Hkv), dim3(256), 0, stream, merge, cu_q, part_o,
+      hipLaunchKernelGGL(prefill_merge_kernel<64>, dim3(nmerge, Hkv, 16), dim3(256), 0, stream, merge, cu_q, part_o,
                          part_ml, (bf16*)out, lse, Hq, Hkv);
   } else {
     return (int)hipErrorInvalidValue;

@@ -870,8 +870,9 @@ def test_bge_encoder_bulk_tile_kernels_match_library_path(monkeypatch):
 
 @pytest.mark.parametrize("T,E", [(300, 8), (2100, 8), (777, 4)])
 def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
-    """Grouped fp8 tile GEMMs over device expert buckets (block-scaled 16x16x128 MFMA at unit
-    scales) == the per-expert fp8 x fp8 reference loop on the same quantized experts."""
+    """Grouped fp8 tile GEMMs over device expert buckets (block-scaled 16x16x128 MFMA) == the
+    per-expert fp8 x fp8 reference loop on the same quantized experts, with the intermediate
+    rounded the way the tiles hand it over (MX blocks by default, per-row with PENNY_MOE_MX=0)."""
     from financial_chatbot_llm_amd.ops import gemm, moe
     g = torch.Generator(device=DEV).manual_seed(T)
     H, F_, K = 1024, 1536, 2
@@ -898,8 +899,11 @@ def test_moe_prefill_fp8_tiles_matches_expert_loop(T, E):
         w13d = q13[e].float() * s13[e][:, None]
         w2d = q2[e].float() * s2[e][:, None]
         a = gemm.silu_mul((xd[rows] @ w13d.t()).to(torch.bfloat16), interleave16=True)
-        aq, as_ = moe.quant_rows_fp8(a)
-        y = (aq.float() * as_[:, None]) @ w2d.t()
+        if moe.MX_HANDOFF:                       # the tiles hand the intermediate over in MX fp8
+            y = moe._fake_quant_mx(a.float()) @ w2d.t()
+        else:
+            aq, as_ = moe.quant_rows_fp8(a)
+            y = (aq.float() * as_[:, None]) @ w2d.t()
         wgt = (topw * sel).sum(1)[rows]
         ref[rows] += wgt[:, None] * y
     err = float((got - ref).abs().max() / ref.abs().max())
