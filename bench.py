@@ -119,7 +119,9 @@ async def run(args, ps):
                         sched_sjf_tokens=int(os.environ.get("PENNY_SJF_TOKENS", EngineConfig.sched_sjf_tokens)),
                         sched_sjf_step_cap=int(os.environ.get("PENNY_SJF_STEP_CAP", EngineConfig.sched_sjf_step_cap)),
                         sched_short_reserve_tokens=int(os.environ.get("PENNY_SHORT_RESERVE",
-                                                                      EngineConfig.sched_short_reserve_tokens)))
+                                                                      EngineConfig.sched_short_reserve_tokens)),
+                        sched_short_first=os.environ.get("PENNY_SHORT_FIRST",
+                                                         str(int(EngineConfig.sched_short_first))) == "1")
     if args.tp > 1 and not ps.is_tp_leader:
         # TP follower: the same engine shard, warmed up (graph capture) in lockstep with its leader,
         # then replays every step the leader broadcasts until the leader's engine shuts down

@@ -147,6 +147,8 @@ class EngineConfig:
     # per-step reservation for waiting short-output (decide) prompts against continuing long
     # prefills (engine/scheduler.py; 0 = off)
     sched_short_reserve_tokens: int = 0
+    # admission order: short-output (decide) prompts ahead of aged long-output ones (scheduler.py)
+    sched_short_first: bool = False
     enable_prefix_caching: bool = True
     # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
     # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
@@ -181,6 +183,7 @@ class EngineConfig:
             sched_sjf_tokens=_env_int("PENNY_SJF_TOKENS", cls.sched_sjf_tokens),
             sched_sjf_step_cap=_env_int("PENNY_SJF_STEP_CAP", cls.sched_sjf_step_cap),
             sched_short_reserve_tokens=_env_int("PENNY_SHORT_RESERVE", cls.sched_short_reserve_tokens),
+            sched_short_first=bool(_env_int("PENNY_SHORT_FIRST", int(cls.sched_short_first))),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
             enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),

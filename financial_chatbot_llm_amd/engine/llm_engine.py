@@ -81,7 +81,8 @@ class LLMEngine:
                                    burst_age_s=getattr(cfg, "sched_burst_age_s", 0.5),
                                    sjf_tokens=getattr(cfg, "sched_sjf_tokens", 0),
                                    sjf_step_cap=getattr(cfg, "sched_sjf_step_cap", 0),
-                                   short_reserve_tokens=getattr(cfg, "sched_short_reserve_tokens", 0))
+                                   short_reserve_tokens=getattr(cfg, "sched_short_reserve_tokens", 0),
+                                   short_first=getattr(cfg, "sched_short_first", False))
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
                                   use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
                                   cascade=cfg.enable_cascade_attention)
@@ -576,6 +577,7 @@ class LLMEngine:
                 "burst_steps": self.scheduler.num_burst_steps,
                 "sjf_admits": self.scheduler.num_sjf_admits,
                 "short_reserved_steps": self.scheduler.num_reserved_steps,
+                "short_wait": dict(self.scheduler.short_wait),
                 "spec_draft_tokens": self.spec_stats["proposed"], "spec_accepted_tokens": self.spec_stats["accepted"],
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},

@@ -30,7 +30,7 @@ from __future__ import annotations
 import time
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Deque, List, Tuple
+from typing import Deque, Dict, List, Tuple
 
 from .sequence import Sequence, SeqStatus
 
@@ -74,7 +74,8 @@ class Scheduler:
                  max_model_len: int = 8192, decode_first: bool = True, short_output_tokens: int = 160,
                  aging_s: float = 1.0, clock=time.perf_counter, token_quantum: int = 0,
                  cost_model: "StepCostModel" = None, burst_tokens: int = 0, burst_age_s: float = 0.5,
-                 sjf_tokens: int = 0, sjf_step_cap: int = 0, short_reserve_tokens: int = 0):
+                 sjf_tokens: int = 0, sjf_step_cap: int = 0, short_reserve_tokens: int = 0,
+                 short_first: bool = False):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -105,14 +106,26 @@ class Scheduler:
         # (starvation-free) and the reserve is only held while short prompts actually wait
         self.short_reserve_tokens = short_reserve_tokens
         self.num_reserved_steps = 0
+        # short_first: aged long-output prompts keep priority over fresh long ones but no longer
+        # over short-output (decide-class) prompts, which are bounded in size (admission classes
+        # 0 preempted, 1 short, 2 aged long, 3 rest; off: short and aged share class 1)
+        self.short_first = short_first
+        # TTFT-tail anatomy: steps that ended with a short-output prompt still waiting, by what
+        # stopped admission ("budget" / "grow" / "seqs" / "pending") and where those steps'
+        # tokens went (decode rows, speculative chunks, continuing prefills, admitted prompts)
+        self.short_wait: Dict[str, int] = {k: 0 for k in (
+            "steps", "budget", "grow", "seqs", "pending", "tok_decode", "tok_spec", "tok_cont",
+            "tok_admit_short", "tok_admit_long", "waiting_short", "waiting_short_tokens")}
 
     def _priority(self, seq: Sequence, now: float):
         if seq.num_preemptions:
             cls = 0
-        elif seq.params.max_tokens <= self.short_output_tokens or now - seq.arrival >= self.aging_s:
+        elif seq.params.max_tokens <= self.short_output_tokens:
             cls = 1
+        elif now - seq.arrival >= self.aging_s:
+            cls = 2 if self.short_first else 1
         else:
-            cls = 2
+            cls = 3
         return (cls, seq.priority_time)
 
     def add(self, seq: Sequence) -> None:
@@ -176,6 +189,7 @@ class Scheduler:
             self.bm.grow(seq, seq.num_tokens)
             batch.decode.append(seq)
             budget -= 1
+        tok_spec = 0
         # 1b) speculative chunks (last token + prompt-lookup draft, engine.speculative): decode-class
         # rows, scheduled whole -- every draft position must be sampled in the same step
         for seq in sorted((s for s in self.running if s.spec_rows and not s.awaiting
@@ -189,6 +203,7 @@ class Scheduler:
                 continue
             batch.prefill.append((seq, seq.num_computed, n))
             budget -= n
+            tok_spec += n
         # step-time bound: a decide call is decoding -> keep this step short (its next token waits
         # for it); the cap never drops below min_prefill_tokens, so prefill always progresses
         if self.cost.target_ms > 0 and any(s.params.max_tokens <= self.short_output_tokens for s in batch.decode):
@@ -214,6 +229,7 @@ class Scheduler:
         # 2) continuing prefills (not the sequences 2a just admitted: their computed count moves only
         # when this step resolves)
         taken = {id(q) for q, _, _ in batch.prefill}
+        tok_cont = 0
         for seq in sorted((s for s in self.running if s.remaining_prefill > 1 and not s.awaiting
                            and not s.spec_rows and id(s) not in taken), key=lambda s: s.priority_time):
             if budget <= 0:
@@ -224,14 +240,25 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
+            tok_cont += n
         budget += reserve
         # 3) admit waiting sequences, by priority class (preempted, short-output/aged, rest)
         if len(self.waiting) > 1:
             now = self.clock()
             self.waiting = deque(sorted(self.waiting, key=lambda q: self._priority(q, now)))
-        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+        stop, tok_admit = "", [0, 0]
+        while True:
+            if not self.waiting:
+                break
+            if budget <= 0:
+                stop = "budget"
+                break
+            if len(self.running) >= self.max_num_seqs:
+                stop = "seqs"
+                break
             seq = self.waiting[0]
             if seq.pending_src >= 0 or seq.awaiting:
+                stop = "pending"
                 break   # preempted with an in-flight token: re-admit once it is known
             if not seq.block_table:
                 self.bm.match_prefix(seq)
@@ -239,8 +266,10 @@ class Scheduler:
             if not self.bm.grow(seq, seq.num_computed + n):
                 if seq.block_table and not self.running:
                     raise MemoryError("KV pool too small for a single prompt")
+                stop = "grow"
                 break
             self.waiting.popleft()
+            tok_admit[seq.params.max_tokens > self.short_output_tokens] += n
             if seq.admit_time is None:
                 seq.admit_time = self.clock()
             seq.status = SeqStatus.RUNNING
@@ -248,6 +277,18 @@ class Scheduler:
             batch.prefill.append((seq, seq.num_computed, n))
             seq.num_prefilled += n
             budget -= n
+        short = [q for q in self.waiting if q.params.max_tokens <= self.short_output_tokens]
+        if short:
+            sw = self.short_wait
+            sw["steps"] += 1
+            sw[stop] += 1
+            sw["tok_decode"] += len(batch.decode)
+            sw["tok_spec"] += tok_spec
+            sw["tok_cont"] += tok_cont
+            sw["tok_admit_short"] += tok_admit[0]
+            sw["tok_admit_long"] += tok_admit[1]
+            sw["waiting_short"] += len(short)
+            sw["waiting_short_tokens"] += sum(q.remaining_prefill for q in short)
         self._quantise(batch)
         return batch
 

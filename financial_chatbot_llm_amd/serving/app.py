@@ -111,7 +111,8 @@ def create_app(services: Services, start_consumer: bool = True) -> FastAPI:
     async def metrics():
         if services.engine is not None and hasattr(services.engine, "stats"):
             for k, v in services.engine.stats().items():
-                METRICS.set_gauge(f"engine_{k}", float(v))
+                for kk, vv in (v.items() if isinstance(v, dict) else ((None, v),)):
+                    METRICS.set_gauge(f"engine_{k}" if kk is None else f"engine_{k}_{kk}", float(vv))
         return METRICS.render_prometheus()
 
     @app.post("/process_message")

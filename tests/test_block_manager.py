@@ -339,3 +339,30 @@ def test_short_job_first_admits_short_prompt_once_ahead_of_long_prefill():
     ids = [q.request_id for q, _, _ in b2.prefill]
     assert ids == ["short", "long"] and len(set(ids)) == len(ids)
     assert sum(n for _, _, n in b2.prefill) == 512 and sch.num_sjf_admits == 1
+
+
+@pytest.mark.parametrize("short_first", [False, True])
+def test_short_first_orders_decides_ahead_of_aged_long_prompts(short_first):
+    """An aged long-output prompt (waited past aging_s) and a fresh decide-class prompt compete
+    for one step's budget: by default they share the priority class and the older long prompt
+    goes first; with short_first the decide does, the aged prompt still beats fresh long ones,
+    and the admission anatomy (short_wait) records why the loser waited."""
+    clock = [100.0]
+    bm = PyBlockManager(512, BS, True)
+    sch = Scheduler(bm, max_num_seqs=64, max_num_batched_tokens=128, max_model_len=8192, clock=lambda: clock[0],
+                    aging_s=1.0, short_first=short_first)
+    aged = _mk_params(list(range(20000, 20000 + 400)), "aged", 512, arrival=98.0)
+    fresh = _mk_params(list(range(30000, 30000 + 400)), "fresh", 512, arrival=99.9)
+    decide = _mk_params(list(range(5000, 5000 + 100)), "decide", 96, arrival=99.95)
+    for q in (fresh, aged, decide):
+        sch.add(q)
+    batch = sch.schedule()
+    first = batch.prefill[0][0]
+    assert first is (decide if short_first else aged)
+    assert all(q is not fresh for q, _, _ in batch.prefill)     # fresh long prompt is last either way
+    sw = sch.short_wait
+    if short_first:
+        assert sw["steps"] == 0                                 # no short prompt left waiting
+    else:
+        assert sw["steps"] == 1 and sw["tok_admit_long"] == 128 and sw["waiting_short"] == 1
+        assert sw["budget"] == 1                                # the aged long prompt took the budget
