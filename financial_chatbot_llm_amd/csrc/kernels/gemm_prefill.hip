@@ -43,21 +43,17 @@
 //     is a COUNTED vmcnt(6) once per K-tile (never 0 in the steady state).
 //   * blockIdx is remapped bijectively so each XCD owns a contiguous range of tiles, grouped
 //     4 token-tiles x N so the XCD's 32 concurrent tiles share X and W panels in its L2.
-//   * wave quantisation (TailArgs, stream-K): when the tile count T is not a multiple of the CU
-//     count C, the first dpn tiles run whole, one per workgroup, and the last sk tiles (sk = T mod C,
-//     or T mod C + C when that round is too thin, or all T when T < C) are cut into one contiguous
-//     run of K-tiles per workgroup over P workgroups (sk * K/64 / P K-tiles each, >= 16): a
-//     workgroup's run may end one tile and start the next, so each runs a short loop of segments.
-//     At M = 2304 the O / down projections' 144 tiles occupy all 256 CUs for 144/256 of a tile's
-//     time instead of 144 CUs for a whole one.  A segment that is not a whole tile stores its f32
-//     accumulators, releases them (agent fence) and draws a ticket from the tile's counter; the
-//     workgroup drawing the tile's last ticket acquires, sums every segment's partial (in K order:
-//     bitwise repeatable), resets the counter and runs the tile's ordinary epilogue.  No workgroup
-//     ever waits on another.
+//   * wave quantisation (TailArgs): when the tile count T is not a multiple of the CU count C, the
+//     first T - L tiles (L = T mod C) run whole, one per workgroup, and each of the L tail tiles is
+//     split over s = C / L workgroups along K -- the last partial round costs 1/s of a tile
+//     instead of a whole one (at M = 512 the QKV GEMM's 48 tiles become 240 workgroups).  Each
+//     split stores its f32 accumulators, releases them (agent fence) and draws a ticket from the
+//     tile's counter; the workgroup drawing s - 1 acquires, adds the other splits' partials into
+//     its registers (in split order: bitwise repeatable), resets the counter and runs the tile's
+//     ordinary epilogue.  No workgroup ever waits on another.
 #include "common.h"
 #include "kv_layout.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -102,23 +98,13 @@ struct SampleArgs {
   int voff, vvalid;
 };
 
-// wave-quantisation tail (above): dpn whole tiles, then L stream-K tiles over P workgroups; part =
-// [L + P, 256*256] f32 (segment (tile i, workgroup u) -> slot i + u: injective, segments advance i
-// or u or both), cnt = [L] zero-initialised tickets (self-resetting); P == 0: no tail
+// wave-quantisation tail (above): dpn whole tiles, then L tail tiles x s K-splits; part =
+// [L, s, 256*256] f32, cnt = [L] zero-initialised tickets (self-resetting); s <= 1: no tail
 struct TailArgs {
-  int dpn, L, P;
+  int dpn, L, s;
   float* part;
   int* cnt;
 };
-
-// Stream-K: workgroup u of P runs K-tile iterations [u*I/P, (u+1)*I/P) of the I = L * ntot; the
-// workgroup whose run holds iteration `it`
-__host__ __device__ inline int sk_owner(long it, int P, long I) {
-  int u = (int)(it * P / I);
-  while (u + 1 < P && (long)(u + 1) * I / P <= it) ++u;
-  while (u > 0 && (long)u * I / P > it) --u;
-  return u;
-}
 
 struct RopeArgs {
   const int* positions;   // [M]
@@ -273,34 +259,22 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   const char* __restrict__ X = static_cast<const char*>(Xv);
   const char* __restrict__ W = static_cast<const char*>(Wv);
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF + (MXI ? 2048 : 0)];
-  // ---- tile of this workgroup: bijective XCD remap, then L2 groups of GM token tiles ----
-  const int Mt = (M + TM - 1) / TM + (FP8 ? ma.E : 0), Nt = N / TN, tiles = Mt * Nt;
-  const bool tail = !FP8 && ta.P > 0 && (int)blockIdx.x >= ta.dpn;   // workgroup-uniform
-  // stream-K run of this workgroup (tail only): iterations [skit, skend) of the tail's I
-  const int ntot = K / BKE, sku = tail ? (int)blockIdx.x - ta.dpn : 0;
-  const long skI = (long)ta.L * ntot;
-  long skit = tail ? (long)sku * skI / ta.P : 0;
-  const long skend = tail ? (long)(sku + 1) * skI / ta.P : 0;
-  do {                                        // one segment per pass; only the tail loops
-  // lane-derived values are rebuilt per segment from an opaque thread id: hoisted out of the
-  // segment loop they (and every epilogue address derived from them) would stay live across the
-  // K loop and spill
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wa = w >> 2, wb = w & 3;  // wave grid 2 (W rows) x 4 (tokens)
   const int g = lane >> 4, col = lane & 15;
-  int s = 0, tile, tu = 0, kb = 0, ke = 0;
+
+  // ---- tile of this workgroup: bijective XCD remap, then L2 groups of GM token tiles ----
+  const int Mt = (M + TM - 1) / TM + (FP8 ? ma.E : 0), Nt = N / TN, tiles = Mt * Nt;
+  const bool tail = !FP8 && ta.s > 1 && (int)blockIdx.x >= ta.dpn;   // workgroup-uniform
+  int s = 0, tile, tu = 0, tj = 0;
   if (tail) {
-    tu = (int)(skit / ntot);                  // stream-K tile of this segment, its K-tiles [kb, ke)
-    kb = (int)(skit - (long)tu * ntot);
-    ke = skend - (long)tu * ntot < ntot ? (int)(skend - (long)tu * ntot) : ntot;
-    skit = (long)tu * ntot + ke;
+    const int u = blockIdx.x - ta.dpn;        // tail workgroups are dispatched last, round robin
+    tu = u % ta.L;
+    tj = u / ta.L;
     tile = ta.dpn + tu;
-    __syncthreads();                          // the previous segment's LDS reads / flag are done
   } else {
-    const int nwg = ta.P > 0 ? ta.dpn : tiles * S;
+    const int nwg = ta.s > 1 ? ta.dpn : tiles * S;
     int id = blockIdx.x;
     const int xcd = id & 7, q = nwg >> 3, r = nwg & 7;
     id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
@@ -328,7 +302,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     W += (long)e * N * K;
   }
   int k0, nt;
-  if (tail) {
+  if (tail) {                                 // K-tiles [tj * ntot / s, (tj + 1) * ntot / s)
+    const int ntot = K / BKE, kb = tj * ntot / ta.s, ke = (tj + 1) * ntot / ta.s;
     k0 = kb * BKE;
     nt = ke - kb;
   } else {
@@ -539,12 +514,10 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
   }
   if (wa == 0) bar();
 
-  if (!FP8 && tail && (kb > 0 || ke < ntot)) {
-    // ---- stream-K tail: publish this segment's accumulators; the tile's last ticket combines ----
+  if (!FP8 && tail) {
+    // ---- wave-quantisation tail: publish this K-split's accumulators; the last split combines ----
     // partial layout [wave][f][t][lane] f32x4: every store / load instruction moves 1 KiB contiguous
-    const long it0 = (long)tu * ntot;
-    const int uf = sk_owner(it0, ta.P, skI), nseg = sk_owner(it0 + ntot - 1, ta.P, skI) - uf + 1;
-    float* mine = ta.part + ((long)tu + sku) * (TM * TN);
+    float* mine = ta.part + ((long)tu * ta.s + tj) * (TM * TN);
 #pragma unroll
     for (int f = 0; f < 8; ++f)
 #pragma unroll
@@ -557,7 +530,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       wait_vm<0>();
       const int old = __hip_atomic_fetch_add(&ta.cnt[tu], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == nseg - 1;
+      const int last = old == ta.s - 1;
       if (last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         wait_vm<0>();
@@ -566,31 +539,19 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       *reinterpret_cast<volatile int*>(flag) = last;
     }
     __syncthreads();
-    if (!*reinterpret_cast<volatile int*>(flag)) continue;     // next segment of the run, if any
-    // compiler-visible vmcnt(0) (the asm waits above are invisible to hipcc's waitcnt pass): with
-    // the segment loop's back edge the pass otherwise merges the previous segment's epilogue stores
-    // into this point and drains vmcnt(0) after EVERY partial load below (32 serial round trips)
-    __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-    // sum every segment (its own included, re-read) in K order whichever drew the last ticket, so
+    if (!*reinterpret_cast<volatile int*>(flag)) return;
+    // sum every split (its own included, re-read) in split order whichever drew the last ticket, so
     // the result is bitwise repeatable; each pass issues its 32 independent 16-B loads at once
-    // (segment j of tile tu is workgroup uf + j's: slot tu + uf + j)
-    const float* base = ta.part + ((long)tu + uf) * (TM * TN) + ((w * 32 * 64 + lane) << 2);
-    // (groups of 8 loads pinned in flight together by an empty asm "use": inside the segment loop
-    // hipcc otherwise reused one 4-VGPR temporary for all 32 loads, each waited for in turn)
-    for (int j = 0; j < nseg; ++j) {
+    const float* base = ta.part + (long)tu * ta.s * (TM * TN) + ((w * 32 * 64 + lane) << 2);
+    for (int j = 0; j < ta.s; ++j) {
       const float* pj = base + (long)j * (TM * TN);
 #pragma unroll
-      for (int f = 0; f < 8; f += 2) {
-        f32x4 v[8];
+      for (int f = 0; f < 8; ++f)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4*>(pj + (((f + (q >> 2)) * 4 + (q & 3)) * 64 << 2));
-        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          f32x4& a = acc[f + (q >> 2)][q & 3];
-          a = j == 0 ? v[q] : a + v[q];
+        for (int t = 0; t < 4; ++t) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(pj + ((f * 4 + t) * 64 << 2));
+          acc[f][t] = j == 0 ? v : acc[f][t] + v;
         }
-      }
     }
   }
 
@@ -826,7 +787,6 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       }
     }
   }
-  } while (tail && skit < skend);
 }
 
 }  // namespace
@@ -840,37 +800,23 @@ static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const 
 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
 
-// Tail plan for T tiles on `cus` CUs (S == 1 launches, bf16): stream-K over the last sk tiles
-// (module comment).  sk = T mod cus when that round gives every CU >= 16 K-tiles, else that round
-// plus one whole round (T >= cus), else the thin round over fewer workgroups (>= 16 K-tiles each:
-// a 256x256 f32 partial store + combine costs ~ a few K-tiles' time, bench/kernels.py gemm_tail).
-// Taken when it saves >= 8 K-tile times per CU, workspace permitting (ws_floats >= (sk + P) *
-// 256 * 256, ncnt >= sk).  Returns the grid; ta.P == 0 means no tail.
-// PENNY_GEMM_SK=1 enables the tile-crossing plan above (off until measured); 0: the r3 plan on the
-// same machinery -- only the T mod cus tiles, each split into
-// s = min(cus / L, ntot / 16) equal K ranges (P = L * s; no tile-crossing runs).
-static bool stream_k_enabled() {
-  static const int on = [] {
-    const char* v = getenv("PENNY_GEMM_SK");
-    return v ? atoi(v) : 0;
-  }();
-  return on != 0;
-}
-
+// Tail plan for T tiles on `cus` CUs (S == 1 launches): L = T mod cus tiles split s = cus / L ways
+// (>= 2, each split >= 16 K-tiles), workspace permitting (ws_floats >= L * s * 256 * 256, ncnt >= L).
+// Returns the grid; ta.s <= 1 means no tail.
 static dim3 tail_plan(int M, int N, int K, int cus, float* ws, long ws_floats, int* cnt, int ncnt, TailArgs& ta) {
   ta = TailArgs{};
   const int T = ((M + TM - 1) / TM) * (N / TN);
-  if (cus <= 0 || !ws || !cnt || T % cus == 0) return dim3((unsigned)T);
-  const int ntot = K / BK, L = T % cus;
-  int sk = L;
-  if (stream_k_enabled() && (long)L * ntot < 16L * cus && T >= L + cus) sk = L + cus;
-  const long I = (long)sk * ntot;
-  const int P = stream_k_enabled() ? (int)std::min<long>(cus, I / 16) : L * std::min(cus / L, ntot / 16);
-  // rounds of whole tiles: DP ceil(T / cus); stream-K (T - sk) / cus + I / (P * ntot)
-  const double saved = ((double)((T + cus - 1) / cus) - (double)(T - sk) / cus - (double)I / ((double)P * ntot)) * ntot;
-  if (P < 2 || saved < 8.0 || sk > ncnt || (long)(sk + P) * TM * TN > ws_floats) return dim3((unsigned)T);
-  ta = TailArgs{T - sk, sk, P, ws, cnt};
-  return dim3((unsigned)(T - sk + P));
+  if (cus > 0 && ws && cnt) {
+    const int L = T % cus, ntot = K / BK;
+    int s = L ? cus / L : 0;
+    s = min(s, ntot / 16);          // >= 16 K-tiles per split: the f32 partial store + combine of a
+                                    // 256x256 tile costs ~ a few K-tiles' time (bench/kernels.py gemm_tail)
+    if (L && s >= 2 && L <= ncnt && (long)L * s * TM * TN <= ws_floats) {
+      ta = TailArgs{T - L, L, s, ws, cnt};
+      return dim3((unsigned)(T - L + L * s));
+    }
+  }
+  return dim3((unsigned)T);
 }
 
 // Contract (checked): N % 256 == 0, K % (64*S) == 0, ldx % 8 == 0, rows 16-B aligned; EPI_SILU

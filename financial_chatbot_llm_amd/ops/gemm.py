@@ -496,10 +496,9 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
     return y
 
 
-# Wave-quantisation tail of the tile kernel (gemm_prefill.hip TailArgs, stream-K): one workspace
-# per (device, stream) -- f32 partial tiles for the segments of at most sk + P <= 3 rounds of
-# workgroups (192 MB on 256 CUs) and self-resetting ticket counters.  PENNY_GEMM_TAIL=0 launches
-# whole tiles only (A/B).
+# Wave-quantisation tail of the tile kernel (gemm_prefill.hip TailArgs): one workspace per
+# (device, stream) -- f32 partial tiles of at most one round of tail workgroups (64 MB) and
+# self-resetting ticket counters.  PENNY_GEMM_TAIL=0 launches whole tiles only (A/B).
 _TAIL_WS: Dict[Tuple[int, int], Tuple[torch.Tensor, torch.Tensor, int]] = {}
 
 
@@ -510,8 +509,8 @@ def tail_workspace(dev: torch.device) -> Tuple:
     ent = _TAIL_WS.get(key)
     if ent is None:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        part = torch.empty((3 * cus * 256 * 256,), dtype=torch.float32, device=dev)
-        cnt = torch.zeros((2 * cus,), dtype=torch.int32, device=dev)
+        part = torch.empty((cus * 256 * 256,), dtype=torch.float32, device=dev)
+        cnt = torch.zeros((cus,), dtype=torch.int32, device=dev)
         ent = _TAIL_WS[key] = (part, cnt, cus)
     part, cnt, cus = ent
     return (N.ptr(part), part.numel(), N.ptr(cnt), cnt.numel(), cus)

@@ -1251,16 +1251,13 @@ def test_fused_lm_head_graph_decode_falls_back_for_top_p(monkeypatch):
 
 @pytest.mark.parametrize("M,N_,K,epi", [(512, 6144, 4096, None), (2560, 1024, 2048, "silu"), (300, 512, 1024, "residual"),
                                         (1000, 768, 768, "bias_gelu"),
-                                        # stream-K: 144 tiles < 256 CUs (runs of 36 K-tiles cross tiles)
-                                        (2304, 4096, 4096, None),
-                                        (2304, 4096, 14336, "residual"),          # the down projection
-                                        (768, 6144, 4096, None),                  # 18-K-tile runs, 5 segments a tile
-                                        (1024, 28672, 4096, "silu"),              # 448 tiles: last 192 stream-K
-                                        (4608, 4096, 4096, "residual")])          # thin round + a whole one
+                                        # production shapes around the tail's decision points
+                                        (2304, 4096, 4096, None), (2304, 4096, 14336, "residual"),
+                                        (768, 6144, 4096, None), (1024, 28672, 4096, "silu"),
+                                        (4608, 4096, 4096, "residual")])
 def test_prefill_gemm_wave_quantisation_tail(M, N_, K, epi, monkeypatch):
-    """Stream-K tail (runs of K-tiles across tile boundaries, the tile's last ticket combines every
-    segment's partial in K order) equals the whole-tile launch up to f32 summation order, bitwise
-    the same every call (the ticket counters reset themselves)."""
+    """Tail tiles split along K over idle CUs (last split combines in registers) equal the whole-tile
+    launch up to f32 summation order, every call (the ticket counters reset themselves)."""
     from financial_chatbot_llm_amd.ops import gemm
     g = torch.Generator().manual_seed(M + N_)
     x, w = rnd(M, K, gen=g).to(DEV), rnd(N_, K, scale=0.05, gen=g).to(DEV)
