@@ -280,7 +280,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
         variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean_1",
-                    "pf2_sb_lean": "lean_4", "pf4": 5, "pf4_lean": "lean_5"}
+                    "pf2_sb_lean": "lean_4"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():

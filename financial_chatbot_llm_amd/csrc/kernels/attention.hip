@@ -979,376 +979,6 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// Software-pipelined prefill (prefill4_kernel, variant 5): prefill2's tile and LDS ring, but each
-// wave overlaps its own softmax with its MFMAs.
-// ------------------------------------------------------------------------------------------
-// In prefill2 a wave runs {QK^T MFMAs ; softmax VALU ; P.V MFMAs} per block, and the two waves of
-// a SIMD reach the same phase together (one barrier per block), so the matrix pipe idles through
-// every softmax and the VALU through every MFMA run -- per SIMD and block ~2 x 1k MFMA cycles plus
-// ~2 x 1.2k VALU cycles, serialised.  Here iteration j of a wave issues the QK^T MFMAs of block
-// j+1 and the P.V MFMAs of block j-1 (64 MFMAs, no dependence on the softmax) interleaved, slice by
-// slice, with the softmax of block j (the FA3 schedule): a v_mfma occupies the matrix pipe for 16
-// cycles while the same wave keeps issuing VALU.  Slices are fenced with sched_barrier so hipcc
-// keeps the interleave.  LDS ring of 5 blocks (all 160 KiB): iteration j reads K(j+1) and V(j-1)
-// and stages block j+3 into the buffer V(j-2) left.  Masked blocks (diagonal, or past a wave's
-// last row) go through the select path, so a wave past its causal end computes zeros instead of branching the
-// MFMA code (one copy of it in the loop: no accumulator copies at join points).  The running max
-// is deferred as in attend_block; the O rescale runs at the end of the iteration, after the P.V of
-// block j-1 (relative to the previous max) and before that of block j.
-// Empty asm "use" of softmax values inside their slice: the exps are pure, so without it LLVM
-// sank the whole softmax chain to the end of the iteration (its results only feed the next P.V),
-// away from the MFMAs it is meant to overlap.
-__device__ __forceinline__ void pin_row(f32x4& a, f32x4& b) { asm volatile("" : "+v"(a), "+v"(b)); }
-
-template <int D, bool HEAD_FAST>
-__global__ void __launch_bounds__(512, 1) prefill4_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
-    float* __restrict__ lse, const int* __restrict__ work, PrefillLean lean = PrefillLean{}) {
-  static_assert(D == 128, "head dim 128 (launch_prefill4 runs nothing else)");
-  constexpr int NW = 8, NBUF = 5;
-  constexpr int KC = D / 32, DT = D / 16;
-  constexpr int TILE = KV_BS * D * 2;
-  constexpr int PIECES = TILE / 1024 / NW;
-  static_assert(PIECES >= 1 && TILE % (1024 * NW) == 0, "tile must split evenly over the waves");
-  constexpr int LOADS = 2 * PIECES;           // glds per wave per staged block (K + V)
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][K|V], 160 KiB
-
-  const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
-  const int* li = lean.items ? lean.items + 6 * item : nullptr;
-  const int s = li ? li[0] : (work ? work[2 * item] : blockIdx.z);
-  const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
-  const int tile = li ? li[1] : (work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item);
-  const int G = Hq / Hkv;
-  const int TQ = NW * 32 / G;
-  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
-  const int tok0 = tile * TQ;
-  if (tok0 >= qlen) return;
-  const int ctx = ctx_lens[s];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
-  const int last_tok = min(tok0 + TQ, qlen) - 1;
-  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
-  const int nblk_tile = (kv_end + KV_BS - 1) / KV_BS;
-  const int jb = li ? li[2] : 0;
-  const int nblk = li ? min(li[3], nblk_tile) - jb : nblk_tile;
-  const int slot = li ? li[4] : -1;
-  const int* bt = block_tables + (long)s * max_blocks + jb;
-
-  auto stage = [&](int j) {
-    const long phys = bt[j];
-    PENNY_DASSERT(phys >= 0);
-    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    char* kl = smem + (j % NBUF) * 2 * TILE;
-    char* vl = kl + TILE;
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const int piece = w * PIECES + i;
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kl + piece * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vl + piece * 1024),
-                                       16, 0, 0);
-    }
-  };
-  if (nblk > 0) stage(0);
-  if (nblk > 1) stage(1);
-  if (nblk > 2) stage(2);
-
-  int tok[2], head[2], qpos[2];
-  Frag qf[2][KC];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const int r = w * 32 + ct * 16 + col;
-    tok[ct] = tok0 + r / G;
-    head[ct] = h * G + r % G;
-    const bool valid = tok[ct] < qlen;
-    qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
-    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
-#pragma unroll
-    for (int c = 0; c < KC; ++c)
-      qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);          // Q and blocks 0-2 resident (compiler-visible)
-  __builtin_amdgcn_s_barrier();
-
-  f32x4 o[2][DT];
-  float m[2], l[2];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    m[ct] = -INFINITY;
-    l[ct] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int wave_tok0 = tok0 + (w * 32) / G;
-  const bool wave_live = wave_tok0 < qlen;
-
-  if (!wave_live) {
-    // all 32 rows are padding: stage this wave's pieces and meet every barrier, nothing else
-    for (int j = 0; j < nblk; ++j) {
-      if (j + 2 < nblk) wait_vmcnt_barrier<LOADS>();
-      else wait_vmcnt_barrier<0>();
-      if (j + 3 < nblk) stage(j + 3);
-    }
-  } else {
-    f32x4 sc[2][4];                            // raw S^T of the block being softmaxed
-    Frag pp[2][2];                             // P of the previous block (bf16), for its P.V
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) pp[ct][st].u = make_uint4(0, 0, 0, 0);
-    {
-      const uint4* kl = reinterpret_cast<const uint4*>(smem);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          Frag kf;
-          kf.u = kl[(t * KC + c) * 64 + lane];
-          sc[0][t] = mfma16(kf.v, qf[0][c].v, sc[0][t]);
-          sc[1][t] = mfma16(kf.v, qf[1][c].v, sc[1][t]);
-        }
-      }
-    }
-    // masking of block ja's scores (diagonal / past the context / past this wave's rows): applied
-    // right after its S^T is complete -- S(0) here, S(j+1) at the end of iteration j -- so the
-    // pipelined body below is one basic block (a branch in front of it made hipcc tail-duplicate
-    // the softmax into both paths, away from the MFMAs it is meant to overlap)
-    auto mask_block = [&](f32x4 (&sx)[2][4], int ja) {
-      const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-      if (__builtin_amdgcn_readfirstlane((int)!full)) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int key = ja * KV_BS + 16 * t + 4 * g + r;
-              const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));
-              sx[ct][t][r] = ok ? sx[ct][t][r] : -INFINITY;
-            }
-      }
-    };
-    mask_block(sc, jb);
-    for (int j = 0; j < nblk; ++j) {
-      // block j+1 landed everywhere (j+2 may stay in flight); iteration j-1 done
-      if (j + 2 < nblk) wait_vmcnt_barrier<LOADS>();
-      else wait_vmcnt_barrier<0>();
-      if (j + 3 < nblk) stage(j + 3);          // into the buffer V(j-2) left
-      const int ja = jb + j;
-      // K of block j+1 (stale but finite past the end: its scores are never used) and V of block
-      // j-1 (block 0 at j = 0, against P = 0)
-      const uint4* kl = reinterpret_cast<const uint4*>(smem + ((j + 1) % NBUF) * 2 * TILE);
-      const uint4* vl = reinterpret_cast<const uint4*>(smem + ((j + NBUF - 1) % NBUF) * 2 * TILE * (j > 0) + TILE);
-      f32x4 sn[2][4];                          // S^T of block j+1
-      Frag kf[KC], vf[2][2];
-      float mt[2], alpha[2];
-      bool grow[2];
-      Frag pn[2][2];
-      // slice 1: QK(j+1) t=0 | row max of ct 0
-#pragma unroll
-      for (int c = 0; c < KC; ++c) kf[c].u = kl[(0 * KC + c) * 64 + lane];
-      __builtin_amdgcn_sched_barrier(0);
-      sn[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sn[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        sn[0][0] = mfma16(kf[c].v, qf[0][c].v, sn[0][0]);
-        sn[1][0] = mfma16(kf[c].v, qf[1][c].v, sn[1][0]);
-      }
-      {
-        float x = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x = fmaxf(x, sc[0][t][r]);
-        mt[0] = x;
-      }
-#pragma unroll
-      for (int c = 0; c < KC; ++c) kf[c].u = kl[(1 * KC + c) * 64 + lane];
-      __builtin_amdgcn_sched_barrier(0);
-      // slice 2: QK(j+1) t=1 | row max of ct 1, cross-lane maxima
-      sn[0][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sn[1][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        sn[0][1] = mfma16(kf[c].v, qf[0][c].v, sn[0][1]);
-        sn[1][1] = mfma16(kf[c].v, qf[1][c].v, sn[1][1]);
-      }
-      {
-        float x = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x = fmaxf(x, sc[1][t][r]);
-        mt[1] = x;
-      }
-      mt[0] = rowgroup_max(mt[0]) * scale_log2;
-      mt[1] = rowgroup_max(mt[1]) * scale_log2;
-      asm volatile("" : "+v"(mt[0]), "+v"(mt[1]));   // keep the softmax in its slice (see pin_row)
-#pragma unroll
-      for (int c = 0; c < KC; ++c) kf[c].u = kl[(2 * KC + c) * 64 + lane];
-      __builtin_amdgcn_sched_barrier(0);
-      // slice 3: QK(j+1) t=2 | new running max, exp of ct 0 t=0,1
-      sn[0][2] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sn[1][2] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        sn[0][2] = mfma16(kf[c].v, qf[0][c].v, sn[0][2]);
-        sn[1][2] = mfma16(kf[c].v, qf[1][c].v, sn[1][2]);
-      }
-      float mref[2], ls[2];
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        grow[ct] = mt[ct] > m[ct] + 8.f;
-        const float mn = grow[ct] ? mt[ct] : m[ct];
-        alpha[ct] = grow[ct] ? fast_exp2(m[ct] - mn) : 1.f;
-        m[ct] = mn;
-        mref[ct] = (mn == -INFINITY) ? 0.f : mn;
-        ls[ct] = 0.f;
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(fmaf(sc[0][t][r], scale_log2, -mref[0]));
-          sc[0][t][r] = p;
-          ls[0] += p;
-        }
-      pin_row(sc[0][0], sc[0][1]);
-#pragma unroll
-      for (int c = 0; c < KC; ++c) kf[c].u = kl[(3 * KC + c) * 64 + lane];
-      __builtin_amdgcn_sched_barrier(0);
-      // slice 4: QK(j+1) t=3 | exp of ct 0 t=2,3
-      sn[0][3] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sn[1][3] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        sn[0][3] = mfma16(kf[c].v, qf[0][c].v, sn[0][3]);
-        sn[1][3] = mfma16(kf[c].v, qf[1][c].v, sn[1][3]);
-      }
-#pragma unroll
-      for (int t = 2; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(fmaf(sc[0][t][r], scale_log2, -mref[0]));
-          sc[0][t][r] = p;
-          ls[0] += p;
-        }
-      pin_row(sc[0][2], sc[0][3]);
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        vf[0][st].u = vl[(0 * 2 + st) * 64 + lane];
-        vf[1][st].u = vl[(1 * 2 + st) * 64 + lane];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // slices 5-8: P.V of block j-1, dt pairs | exp of ct 1, row sums, P of block j to bf16
-#pragma unroll
-      for (int dp = 0; dp < DT / 2; ++dp) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            o[0][2 * dp + e] = mfma16(vf[e][st].v, pp[0][st].v, o[0][2 * dp + e]);
-            o[1][2 * dp + e] = mfma16(vf[e][st].v, pp[1][st].v, o[1][2 * dp + e]);
-          }
-        if (dp == 0 || dp == 1) {
-#pragma unroll
-          for (int t = 2 * dp; t < 2 * dp + 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float p = fast_exp2(fmaf(sc[1][t][r], scale_log2, -mref[1]));
-              sc[1][t][r] = p;
-              ls[1] += p;
-            }
-          pin_row(sc[1][2 * dp], sc[1][2 * dp + 1]);
-        } else {
-          const int ct = dp - 2;
-          l[ct] = l[ct] * alpha[ct] + ls[ct];
-#pragma unroll
-          for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              pn[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
-              pn[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
-            }
-          asm volatile("" : "+v"(pn[ct][0].u.x), "+v"(pn[ct][0].u.y), "+v"(pn[ct][0].u.z), "+v"(pn[ct][0].u.w),
-                       "+v"(pn[ct][1].u.x), "+v"(pn[ct][1].u.y), "+v"(pn[ct][1].u.z), "+v"(pn[ct][1].u.w), "+v"(l[ct]));
-        }
-        if (dp + 1 < DT / 2) {
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            vf[0][st].u = vl[((2 * dp + 2) * 2 + st) * 64 + lane];
-            vf[1][st].u = vl[((2 * dp + 3) * 2 + st) * 64 + lane];
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // O now holds every block < j relative to the old max: move it to the new one before the
-      // P.V of block j (next iteration) adds to it
-      if (__any(grow[0] || grow[1])) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha[ct];
-      }
-      if (j + 1 < nblk) mask_block(sn, ja + 1);
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-        for (int st = 0; st < 2; ++st) pp[ct][st] = pn[ct][st];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) sc[ct][t] = sn[ct][t];
-      }
-    }
-    // drain: P.V of the last block (its V tile is still in buffer (nblk - 1) % NBUF)
-    if (nblk > 0) {
-      const uint4* vl = reinterpret_cast<const uint4*>(smem + ((nblk - 1) % NBUF) * 2 * TILE + TILE);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          Frag vv;
-          vv.u = vl[(dt * 2 + st) * 64 + lane];
-          o[0][dt] = mfma16(vv.v, pp[0][st].v, o[0][dt]);
-          o[1][dt] = mfma16(vv.v, pp[1][st].v, o[1][dt]);
-        }
-    }
-  }
-
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    float lt = l[ct];
-    lt = rowgroup_sum(lt);
-    if (slot >= 0) {
-      const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = o[ct][dt];
-      if (g == 0) {
-        lean.part_ml[2 * pr] = m[ct];
-        lean.part_ml[2 * pr + 1] = lt;
-      }
-      continue;
-    }
-    if (tok[ct] >= qlen) continue;
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      bf16x4 v4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
-    }
-    if (lse != nullptr && g == 0)
-      lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // Ping-pong prefill (prefill3_kernel): the 8-wave tile of prefill2 with its two SIMD partners
 // half a block apart.
 // ------------------------------------------------------------------------------------------
@@ -1689,17 +1319,6 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
     lse[(long)(q0 + tok) * Hq + head] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
 }
 
-// variant 5 (prefill4, D = 128 only): compiled for the launcher's DD = 64 instance as a no-op
-template <int DD>
-static void launch_prefill4(dim3 grid, hipStream_t stream, const bf16* q, const int* cu_q, const int* ctx_lens,
-                            const int* block_tables, const bf16* k_cache, const bf16* v_cache, bf16* out, float sl2,
-                            int Hq, int Hkv, int max_blocks, int causal, float* lse, const int* work,
-                            PrefillLean lean) {
-  if constexpr (DD == 128)
-    hipLaunchKernelGGL((prefill4_kernel<128, true>), grid, dim3(512), 0, stream, q, cu_q, ctx_lens, block_tables,
-                       k_cache, v_cache, out, sl2, Hq, Hkv, max_blocks, causal, lse, work, lean);
-}
-
 static int prefill_variant();
 
 // Lean big-tile prefill: items [nitems, 6] (see PrefillLean; LPT order), merge [nmerge, 6];
@@ -1716,14 +1335,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   const float sl2 = scale * LOG2E;
   const PrefillLean lean{items, part_o, part_ml};
   const int var = prefill_variant();
-  if (D == 128 && var == 5) {
-    launch_prefill4<128>(dim3(Hkv, nitems, 1), stream, (const bf16*)q, cu_q, ctx_lens, block_tables,
-                         (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse,
-                         (const int*)nullptr, lean);
-    if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv, 32), dim3(256), 0, stream, merge, cu_q, part_o,
-                         part_ml, (bf16*)out, lse, Hq, Hkv);
-  } else if (D == 128 && (var == 0 || var == 4)) {
+  if (D == 128 && (var == 0 || var == 4)) {
     if (var == 4)
       hipLaunchKernelGGL((prefill2_kernel<128, 8, 3, true, true, true>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
                          (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
@@ -1815,9 +1427,6 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
     hipLaunchKernelGGL((prefill3_kernel<DD, true, true, true>), grid2, dim3(512), 0, stream,                     \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
-  else if (big && head_fast && pp_env == 5 && DD == 128)                                                          \
-    launch_prefill4<DD>(grid2, stream, (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache,       \
-                        (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{}); \
   else if (big && head_fast && pp_env == 4)                                                                      \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true>), grid2, dim3(512), 0, stream,               \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \

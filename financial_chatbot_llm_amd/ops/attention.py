@@ -261,7 +261,7 @@ def prefill_plan(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causa
                  cus: int = 256) -> Optional[np.ndarray]:
     """The step's prefill-attention work list: lean ([., 6], when some walk needs splitting; the
     prefill2 and ping-pong kernels take it) or whole tiles in LPT order ([n, 2])."""
-    if PREFILL_LEAN and prefill_variant() in (0, 1, 4, 5):
+    if PREFILL_LEAN and prefill_variant() in (0, 1, 4):
         lean = prefill_lean_list(cu_q, ctx_lens, G, Hkv, causal, cus)
         if lean is not None:
             return lean
