@@ -7,10 +7,12 @@ from financial_chatbot_llm_amd.ops import gemm
 
 def test_policy_table_choices(monkeypatch):
     monkeypatch.delenv("PENNY_PREFILL_GEMM", raising=False)
-    # O: the residual epilogue only where the caller can take it, else the library
+    # O: split-K slabs, then the residual epilogue, where the caller can take them, else the library
     assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=True) == "R"
     assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=False) == "lib"
-    assert gemm.prefill_choice(2048, 4096, 4096, None, True, fused_residual=True) == "lib"
+    assert gemm.prefill_choice(2048, 4096, 4096, None, True, fused_residual=True) == "S2"
+    assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "S4"
+    assert gemm.prefill_choice(512, 4096, 4096, None, False) == "lib"
     # down: split-K slabs only when the consumer reads slabs
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=True) == "S4"
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=False) == "lib"
