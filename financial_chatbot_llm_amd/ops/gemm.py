@@ -402,7 +402,7 @@ PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (6144, 4096): [(1280, "lib"), (1 << 30, "fused")],                                    # QKV
     (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
-    (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "lib")],         # down
+    (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down
 }
 
 
