@@ -392,6 +392,9 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 #   "R"    tile kernel adding the residual stream in place (ResidualSum; the consumer's RMSNorm
 #          then skips the add): O from M = 2816 is 3-5 % faster than hipBLASLt + add&norm; only
 #          where the caller passes fuse_residual
+# QKV (r4): the fused RoPE + paged-KV-write tile kernel at every M > 256 as well (hipBLASLt was
+# 7-15 us per layer faster at 257-1280 rows; at the driver config the bench is unchanged, 32.2
+# turns/s, profiles/r4_bench128_20x5_all_prefill_gemms_tile_kernel.json).
 # O (r4): every M > 256 on the tile kernel -- split-K slabs to 2048 rows, the residual epilogue
 # above.  Between 257 and 3072 rows hipBLASLt is 2-7 us per layer faster (5-8 %, 256x256 tiles
 # underfill the CUs: profiles/r4_gemm_stream_k_tail_rejected.jsonl "r3 kernel" rows), ~0.2 ms
@@ -399,7 +402,7 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 # add pass, and the projection on the framework's own MFMA kernel at every prefill size.
 # Shapes without an entry use ``_default_choice``.
 PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
-    (6144, 4096): [(1280, "lib"), (1 << 30, "fused")],                                    # QKV
+    (6144, 4096): [(1 << 30, "fused")],                                                   # QKV
     (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
     (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down

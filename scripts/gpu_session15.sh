@@ -14,4 +14,4 @@ step() {  # name, timeout, command...
   return $rc
 }
 step t_pol 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_prefill_policy_gpu.py tests/test_prefill_policy.py || exit 1
-step b_dpol 400 python -u bench.py --steps 20 --warmup 5 || exit 1
+step b_qpol 400 python -u bench.py --steps 20 --warmup 5 || exit 1
