@@ -268,9 +268,20 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         ln = ops.attention.prefill_lean_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv)
         ld = torch.from_numpy(ln).to(dev) if ln is not None else None
         lc = (int(ln[0, 1]), int(ln[0, 2]), int(ln[0, 3])) if ln is not None else None
+        # finer lean balance targets: the per-CU share computed as if the chip had 2x / 4x the CUs
+        fine = {}
+        for mult in (2, 4):
+            lf = ops.attention.prefill_lean_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv, cus=256 * mult)
+            fine[mult] = ((torch.from_numpy(lf).to(dev), (int(lf[0, 1]), int(lf[0, 2]), int(lf[0, 3])))
+                          if lf is not None else (wd, None))
 
         def run(v):
             def f():
+                if isinstance(v, str) and v.startswith("fine"):
+                    ops.attention.prefill_variant(4)
+                    wk, lk = fine[int(v[4:])]
+                    ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wk, lean=lk)
+                    return
                 if isinstance(v, str):
                     ops.attention.prefill_variant(int(v.split("_")[1]))
                     ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
@@ -280,7 +291,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
         variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean_1",
-                    "pf2_sb_lean": "lean_4"}
+                    "pf2_sb_lean": "lean_4", "pf2_sb_lean_x2": "fine2", "pf2_sb_lean_x4": "fine4"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():
