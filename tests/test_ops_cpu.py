@@ -202,3 +202,25 @@ def test_prefill_work_list_lpt_order():
               for n, c in [((cu[s + 1] - cu[s]), ctx[s])]]
     assert blocks == sorted(blocks, reverse=True)
     assert prefill_work_list(np.array([0, 30, 60], np.int32), np.array([100, 200], np.int32), 4) is None
+
+
+def test_mx_block_grouping_round_trip_and_fake_quant_bounds():
+    """The MX hand-off's CPU model (ops.moe): mx_blocks / mx_unblocks are inverse permutations that
+    group 16-element chunks {0,2}, {4,6}, {1,3}, {5,7} of each 128-wide K-tile (the measured
+    block-scaled MFMA grouping), and the fake quantiser's blocks use power-of-two scales with every
+    scaled element inside e4m3's range, error <= half an e4m3 step of the block's scale."""
+    from financial_chatbot_llm_amd.ops import moe
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((5, 256), generator=g) * torch.logspace(-3, 3, 256)
+    b = moe.mx_blocks(x)
+    assert b.shape == (5, 2, 4, 32)
+    assert torch.equal(moe.mx_unblocks(b), x)
+    assert torch.equal(b[0, 0, 0, :16], x[0, 0:16]) and torch.equal(b[0, 0, 0, 16:], x[0, 32:48])
+    assert torch.equal(b[0, 0, 2, :16], x[0, 16:32]) and torch.equal(b[0, 1, 1, 16:], x[0, 128 + 96:128 + 112])
+    q = moe._fake_quant_mx(x)
+    amax = b.abs().amax(-1)
+    X = torch.ceil(torch.log2(amax / moe.FP8_MAX))
+    assert (amax / torch.exp2(X) <= moe.FP8_MAX).all()
+    err = (moe.mx_blocks(q) - b).abs()
+    # e4m3 has 3 mantissa bits: relative rounding <= 2^-4 of the element, or a subnormal step
+    assert (err <= b.abs() * 2 ** -4 + torch.exp2(X - 9)[..., None] + 1e-30).all()
