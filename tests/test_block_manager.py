@@ -366,3 +366,21 @@ def test_short_first_orders_decides_ahead_of_aged_long_prompts(short_first):
     else:
         assert sw["steps"] == 1 and sw["tok_admit_long"] == 128 and sw["waiting_short"] == 1
         assert sw["budget"] == 1                                # the aged long prompt took the budget
+
+
+def test_short_wait_records_kv_pool_exhaustion():
+    """A decide-class prompt that cannot be admitted because the KV pool is full is counted under
+    the "grow" reason of the admission anatomy, not "budget"."""
+    clock = [100.0]
+    bm = PyBlockManager(8, BS, True)                 # 8 blocks
+    sch = Scheduler(bm, max_num_seqs=64, max_num_batched_tokens=4096, max_model_len=8192, clock=lambda: clock[0])
+    big = _mk_params(list(range(40000, 40000 + 7 * BS)), "respond", 512, arrival=99.0)
+    sch.add(big)
+    batch = sch.schedule()                           # takes 7 of the 8 blocks
+    for q, st, n in batch.prefill:
+        q.num_computed = st + n
+    decide = _mk_params(list(range(50000, 50000 + 3 * BS)), "decide", 96, arrival=99.5)
+    sch.add(decide)
+    sch.schedule()
+    assert decide in sch.waiting
+    assert sch.short_wait["grow"] >= 1 and sch.short_wait["budget"] == 0
