@@ -1103,6 +1103,162 @@ def gemm_lds_probe(dev) -> List[Dict]:
     return [{"op": "gemm_lds_probe", "done": True}]
 
 
+# Every projection shape of the north-star config 4 (Llama-3-70B) that is not an 8B shape: the TP=8
+# per-rank shards and the TP=1 weights.  kind: "col" = column-parallel
+# output consumed by a row pass that reads split-K slabs (QKV -> RoPE/KV write), "row" = row-parallel
+# output into the all-reduce (bf16), "gateup" = interleave16 gate|up with the fused SiLU*up.
+SHARD_SHAPES = {
+    "70b_tp8_qkv": (1280, 8192, "col"), "70b_tp8_o": (8192, 1024, "row"),
+    "70b_tp8_gate_up": (7168, 8192, "gateup"), "70b_tp8_down": (8192, 3584, "row"),
+    "70b_tp1_qkv": (10240, 8192, "col"), "70b_tp1_gate_up": (57344, 8192, "gateup"),
+    "70b_tp1_o": (8192, 8192, "col"), "70b_tp1_down": (8192, 28672, "col"),
+}
+
+
+def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
+                       prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
+    """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
+    one process (rule 24), weights rotated over >= 768 MB so every decode call streams HBM.
+
+    decode (M <= 256): lib = F.linear (+ silu_mul); "row": bf16-output kernel nf x {row-major,
+    tiled}, and split-K slabs + reduce; "col": split-K slabs (gemm-only time: the consumer reads
+    them) per (S, nf); "gateup": fused gate|up kernel per nf.  prefill (M > 256): lib vs the tile
+    kernel (bf16 / SiLU), split-K slabs S = 2, 4 (+ reduce for "row")."""
+    from ..ops import gemm
+    from ..ops.activation import silu_mul
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    for name, (N, K, kind) in SHARD_SHAPES.items():
+        if names and name not in names:
+            continue
+        copies = max(2, min(16, (768 << 20) // (N * K * 2)))
+        ws = [rnd(N, K) for _ in range(copies)]
+        wts = [gemm.tile_weight(w) for w in ws]
+        it = [0]
+
+        def nxt():
+            it[0] = (it[0] + 1) % copies
+            return it[0]
+        wbytes = N * K * 2
+        for M in Ms:
+            x = rnd(M, K)
+            fns = {}
+            if kind == "gateup":
+                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, ws[nxt()]), interleave16=True)
+                for nf in (2, 4, 8):
+                    if N % (16 * nf) == 0:
+                        fns[f"gu_nf{nf}_tiled"] = lambda nf=nf: gemm.gateup_silu(x, wts[nxt()], N, nf)
+                        fns[f"gu_nf{nf}_rm"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=True)
+            else:
+                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
+                if kind == "row":
+                    for nf in (2, 4, 8):
+                        if N % (16 * nf) == 0:
+                            fns[f"bf16_nf{nf}_rm"] = lambda nf=nf: gemm.splitk_bf16(x, ws[nxt()], N, nf)
+                            fns[f"bf16_nf{nf}_tiled"] = lambda nf=nf: gemm.splitk_bf16(x, wts[nxt()], N, nf,
+                                                                                       rowmajor=False)
+                for S in (2, 4, 8):
+                    for nf in (2, 4, 8):
+                        if K % (64 * S) or N % (16 * nf):
+                            continue
+                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                        y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+                        if kind == "row":   # the all-reduce needs the reduced bf16 output
+                            fns[f"S{S}nf{nf}_rm+red"] = (lambda S=S, nf=nf, P=P, y=y: gemm.splitk_reduce(
+                                gemm.splitk_partials(x, ws[nxt()], N, S, nf, out=P, rowmajor=True), out=y))
+                        else:
+                            fns[f"S{S}nf{nf}_rm"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
+                                x, ws[nxt()], N, S, nf, out=P, rowmajor=True))
+                            fns[f"S{S}nf{nf}_tiled"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
+                                x, wts[nxt()], N, S, nf, out=P))
+            t = interleaved(fns, rounds=5, iters=copies)
+            best = min((k for k in t if k != "lib"), key=lambda k: t[k])
+            row = {"op": "shard_shapes", "name": name, "N": N, "K": K, "kind": kind, "M": M,
+                   **{k: round(v, 1) for k, v in t.items()}, "best": best, "best_us": round(t[best], 1),
+                   "best_GBps": round(wbytes / t[best] / 1e3, 1), "speedup": round(t["lib"] / t[best], 2)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del ws, wts
+        torch.cuda.empty_cache()
+        w = rnd(N, K)
+        for M in prefill_Ms:
+            x = rnd(M, K)
+            fns = {}
+            if kind == "gateup":
+                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, w), interleave16=True)
+                fns["hip"] = lambda: gemm.prefill_gemm(x, w, "silu")
+            else:
+                fns["lib"] = lambda: torch.nn.functional.linear(x, w)
+                if N % 256 == 0:
+                    fns["hip"] = lambda: gemm.prefill_gemm(x, w)
+                    for S in (2, 4):
+                        if K % (64 * S) == 0:
+                            P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                            if kind == "row":
+                                y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+                                fns[f"hipS{S}+red"] = (lambda S=S, P=P, y=y: gemm.splitk_reduce(
+                                    gemm.prefill_gemm(x, w, "slabs", S, out=P), out=y))
+                            else:
+                                fns[f"hipS{S}"] = lambda S=S, P=P: gemm.prefill_gemm(x, w, "slabs", S, out=P)
+            t = interleaved(fns, rounds=5, iters=5)
+            best = min((k for k in t if k != "lib"), key=lambda k: t[k]) if len(t) > 1 else "lib"
+            row = {"op": "shard_shapes_prefill", "name": name, "N": N, "K": K, "kind": kind, "M": M,
+                   **{k: round(v, 1) for k, v in t.items()}, "best": best,
+                   "best_TF": round(2 * M * N * K / t[best] / 1e6, 1), "speedup": round(t["lib"] / t[best], 2)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del w
+        torch.cuda.empty_cache()
+    return out
+
+
+def bench_lm_head_stream(dev, V: int = 128256, K: int = 4096,
+                         Ms=(1, 2, 4, 8, 16, 32, 48, 64, 96, 127)) -> List[Dict]:
+    """LM head + sampler at decode sizes: hipBLASLt logits + the HIP sampler vs the 256x256 tile
+    kernel with the sampler epilogue vs the weight-streaming split-K kernel (SK_SAMPLE) per
+    (nf, row-major / tiled W, ring), W rotated so every call streams HBM.  ``same``: the streamed
+    tokens equal ops.sample over the SK_BF16 logits of the same kernel shape (bitwise)."""
+    from ..ops import gemm
+    out = []
+    copies = max(2, min(8, (2048 << 20) // (V * K * 2)))
+    ws = [((torch.rand((V, K), device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(copies)]
+    wts = [gemm.tile_weight(w) for w in ws]
+    it = [0]
+
+    def nxt():
+        it[0] = (it[0] + 1) % copies
+        return it[0]
+    for M in Ms:
+        x = torch.randn((M, K), device=dev).to(torch.bfloat16)
+        t_ = torch.full((M,), 0.5, device=dev)
+        sd = torch.arange(M, device=dev, dtype=torch.int64) * 7919 + 13
+        fns = {"lib_sampler": lambda: ops.sample(torch.nn.functional.linear(x, ws[nxt()]), t_, sd)}
+        import os
+        os.environ["PENNY_LM_STREAM"] = "0"     # ops.lm_head_sample -> the 256x256 tile kernel
+
+        def tile():
+            return ops.lm_head_sample(x, ws[nxt()], t_, sd)
+        fns["tile_fused"] = tile
+        for nf in (4, 8):
+            for rm in (True, False):
+                for r2 in (False, True):
+                    fns[f"stream_nf{nf}_{'rm' if rm else 'tiled'}{'_r2' if r2 else ''}"] = (
+                        lambda nf=nf, rm=rm, r2=r2: ops.lm_head_stream_sample(
+                            x, ws[nxt()] if rm else wts[nxt()], t_, sd, nf=nf, rowmajor=rm, ring2=r2))
+        t = interleaved(fns, rounds=5, iters=copies)
+        os.environ.pop("PENNY_LM_STREAM", None)
+        w0 = ws[0]
+        ref = ops.sample(gemm.splitk_bf16(x, w0, V, 8), t_, sd)
+        got = ops.lm_head_stream_sample(x, w0, t_, sd, nf=8, rowmajor=True)
+        best = min((k for k in t if k.startswith("stream")), key=lambda k: t[k])
+        row = {"op": "lm_head_stream", "M": M, **{k: round(v, 1) for k, v in t.items()}, "best": best,
+               "best_TBps": round(V * K * 2 / t[best] / 1e6, 2), "speedup_vs_lib": round(t["lib_sampler"] / t[best], 2),
+               "same_tokens_as_unfused_on_equal_logits": bool(torch.equal(ref, got))}
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
 def interleave16_rows(w: torch.Tensor) -> torch.Tensor:
     from ..ops.gemm import interleave16
     half = w.shape[0] // 2
@@ -1126,7 +1282,12 @@ def main(argv=None) -> int:
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
-                "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192)}[name](dev)
+                "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
+                "shard_shapes": bench_shard_shapes,
+                "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
+                "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
+                "lm_head_stream": bench_lm_head_stream,
+                "lm_head_stream_shard": lambda d: bench_lm_head_stream(d, V=16128, Ms=(1, 8, 32, 64, 127))}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
     if args.out:

@@ -108,6 +108,7 @@ class EngineConfig:
     sequence_parallel: bool = False         # TP prefills >= 1024 rows: reduce-scatter/all-gather (Megatron SP)
     async_scheduling: bool = True           # overlap host scheduling of step N+1 with GPU step N
     custom_all_reduce: bool = True          # TP decode all-reduces on the one-shot xGMI P2P kernel
+    custom_ar_self_test: bool = True        # init-time check of the custom kernels vs the exact sum
     step_ring: bool = True                  # C4 step broadcast over the node-local shm ring (else gloo)
     tp_dual_decode: bool = True             # TP graph decode as two micro-batch chains on two streams
     weights: Optional[str] = None           # safetensors dir; None -> random init
@@ -191,6 +192,7 @@ class EngineConfig:
             async_scheduling=_env_bool("PENNY_ASYNC_SCHEDULING", True),
             custom_all_reduce=_env_bool("PENNY_CUSTOM_AR", True),
             step_ring=_env_bool("PENNY_STEP_RING", True),
+            custom_ar_self_test=_env_bool("PENNY_AR_SELF_TEST", True),
             tp_dual_decode=_env_bool("PENNY_TP_DUAL_DECODE", True),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),

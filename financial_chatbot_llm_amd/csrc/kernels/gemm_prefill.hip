@@ -1014,6 +1014,13 @@ __global__ void __launch_bounds__(256) lm_sample_final_kernel(const float* __res
   }
 }
 
+PENNY_API int penny_lm_sample_final(const float* pv, const int* pi, int P, int M, int* out, int* pairs,
+                                    hipStream_t stream) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(lm_sample_final_kernel, dim3(M), dim3(256), 0, stream, pv, pi, P, out, pairs);
+  return (int)hipGetLastError();
+}
+
 // LM head + sampler fused (K11 + K12): out[m] = Gumbel-max / argmax sample of row m of
 // X [M, K] bf16 x W [V, K]^T, temps [M] f32 (<= 0: greedy), seeds [M] u64 -- the [M, V] logits are
 // never written.  workspace: M * 2 * (V / 256) floats, then as many ints.

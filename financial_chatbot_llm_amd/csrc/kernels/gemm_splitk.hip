@@ -39,6 +39,20 @@ union Frag {
   bf16x8 v;
 };
 
+// epilogues of splitk_gemm_kernel
+enum { SK_SLAB = 0, SK_SILU = 1, SK_BF16 = 2, SK_SAMPLE = 3 };
+
+// SK_SAMPLE (the streaming LM head + K12 sampler): per-row temperature (<= 0: greedy) and seed;
+// pv / pi [M, pstride] partial (best score, token) per (row, workgroup tile, wave row).  Token
+// ids are voff + local row; local rows >= vvalid (a vocab shard's padding) never win.
+struct SkSample {
+  const float* temps;
+  const unsigned long long* seeds;
+  float* pv;
+  int* pi;
+  int pstride, voff, vvalid;
+};
+
 // X image: token row r of a stage lives at byte r*128; its logical 16-B chunk c (k = 8c..8c+7) at
 // physical chunk c ^ (r & 7) ^ ((r >> 3) & 1).  A fragment read (16 consecutive rows, one logical
 // chunk) then touches 16 distinct (row parity, chunk) bank groups per 16-lane phase.
@@ -46,10 +60,16 @@ __device__ __forceinline__ int xswz(int r, int c) { return c ^ (r & 7) ^ ((r >> 
 
 // stage ring depth: as many BK=64 stages as fit in ~150 KB of LDS (one workgroup per CU), capped
 // at 8 -- a CU must keep ~50-70 KB of W in flight to stream its 1/256 share of HBM bandwidth
-template <int NF, int MT>
+// MAXB: ring depth cap -- 8 by default; 16 for the narrow configs (NF = 2-4 rows groups: 4-8 KiB of
+// W per stage) whose 8-stage ring keeps only 28-56 KiB in flight per CU.  Also capped so the counted
+// vmcnt ((NBUF - 2) * loads per stage) fits the 6-bit counter.
+template <int NF, int MT, int KB = 150, int MAXB = 8>
 struct Ring {
   static constexpr int SBYTES = (NF + MT) * 2 * 1024;
-  static constexpr int NBUF = (150 * 1024 / SBYTES) < 8 ? (150 * 1024 / SBYTES) : 8;
+  static constexpr int LOADS = (2 * NF + 2 * MT) / 4;
+  static constexpr int BY_LDS = KB * 1024 / SBYTES;
+  static constexpr int BY_VM = 63 / LOADS + 2;
+  static constexpr int NBUF = BY_LDS < MAXB ? (BY_LDS < BY_VM ? BY_LDS : BY_VM) : (MAXB < BY_VM ? MAXB : BY_VM);
 };
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>)
@@ -105,23 +125,37 @@ __device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (
   }
 }
 
-// SILU: W is the 16-row-interleaved gate|up weight (ops/gemm.py interleave16) and S == 1; the
-// epilogue writes Y[m, f] = silu(gate) * up as bf16 [M, N/2] (ldy) instead of f32 slabs -- each
-// wave owns whole (gate, up) row-group pairs, so the pair meets in one lane's registers.
+// Epilogues (EPI):
+//   SK_SLAB   f32 partial slabs P [S, M, N] (reduced by the consumer's row pass);
+//   SK_SILU   W is the 16-row-interleaved gate|up weight (ops/gemm.py interleave16) and S == 1: the
+//             epilogue writes Y[m, f] = silu(gate) * up as bf16 [M, N/2] (ldy) instead of f32 slabs --
+//             each wave owns whole (gate, up) row-group pairs, so the pair meets in one lane's registers;
+//   SK_BF16   S == 1, Y bf16 [M, N] (ldy): a row-parallel TP shard whose output goes straight into the
+//             all-reduce (no slab round trip, no reduce launch);
+//   SK_SAMPLE S == 1, W = the [V, K] vocabulary projection (or a TP rank's padded shard): no logits
+//             reach HBM -- each lane Gumbel-max-scores its bf16-rounded logits (sampler.hip's noise of
+//             (row seed, global token id)) and each wave leaves one (score, token) pair per token row,
+//             reduced per row by lm_sample_final_kernel (gemm_prefill.hip).  The weight-streaming LM
+//             head for decode batches (M <= 128), where the 256x256 tile kernel is MFMA-bound on
+//             padding rows.
 // WROW: W is the plain row-major [N, K] weight (no fragment-tiled copy): its stage pieces are
 // 8 rows x 128 B with the same source-side XOR swizzle as X, so every glds instruction still reads
 // whole 128-B lines and the fragment reads stay conflict-free.
-template <int NF, int MT, int WA, bool SILU = false, bool WROW = false>
+// RKB: LDS ring budget in KiB (150: one workgroup per CU; ~72: two co-resident workgroups, so one's
+// pipeline ramp overlaps the other's stream when a CU runs several tiles in sequence).
+template <int NF, int MT, int WA, int EPI = SK_SLAB, bool WROW = false, int RKB = 150, int MAXB = 8>
 __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restrict__ X, int ldx,
                                                              const bf16* __restrict__ Wt, int K,
                                                              float* __restrict__ P, int M, int N, int S,
-                                                             bf16* __restrict__ Y = nullptr, int ldy = 0) {
+                                                             bf16* __restrict__ Y = nullptr, int ldy = 0,
+                                                             SkSample sa = SkSample{}) {
+  constexpr bool SILU = EPI == SK_SILU;
   constexpr int WB = 4 / WA;
   constexpr int FW = NF / WA;   // W row groups per wave
   constexpr int TW = MT / WB;   // token tiles per wave
   static_assert(NF % WA == 0 && MT % WB == 0, "wave split");
   static_assert(!SILU || FW % 2 == 0, "SiLU epilogue needs (gate, up) row-group pairs per wave");
-  constexpr int NBUF = Ring<NF, MT>::NBUF;
+  constexpr int NBUF = Ring<NF, MT, RKB, MAXB>::NBUF;
   static_assert(NBUF >= 3, "ring too shallow");
   constexpr int WBYTES = NF * 2 * 1024;        // W pieces of one BK=64 stage
   constexpr int XBYTES = MT * 2 * 1024;        // X pieces (16*MT rows x 128 B)
@@ -213,6 +247,60 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
           o[r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
         }
         *reinterpret_cast<bf16x4*>(Y + (long)m * ldy + (G >> 1) * 16 + 4 * g) = o;
+      }
+    }
+    return;
+  }
+  if constexpr (EPI == SK_BF16) {
+    // lane holds W rows n = 16f + 4g + r (r = 0..3) for token 16t + col: one 8-B store per fragment
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int m = (wb * TW + t) * 16 + col;
+      if (m >= M) continue;
+#pragma unroll
+      for (int f = 0; f < FW; ++f) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[f][t][r];
+        *reinterpret_cast<bf16x4*>(Y + (long)m * ldy + n0 + (wa * FW + f) * 16 + 4 * g) = o;
+      }
+    }
+    return;
+  }
+  if constexpr (EPI == SK_SAMPLE) {
+    // token row m's 16*FW columns of this wave sit in lanes col, col+16, col+32, col+48 (g = 0..3):
+    // each scores its FW*4, two xor-shuffles inside that lane set (all active or all skipped: they
+    // share m), and lane g == 0 leaves the wave's pair
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int m = (wb * TW + t) * 16 + col;
+      if (m >= M) continue;
+      const float temp = sa.temps[m];
+      const bool greedy = !(temp > 0.f);
+      const float inv_t = greedy ? 1.f : 1.f / temp;
+      const unsigned long long seed = sa.seeds[m];
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int f = 0; f < FW; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int loc = n0 + (wa * FW + f) * 16 + 4 * g + r, idx = sa.voff + loc;
+          float v = (float)(bf16)acc[f][t][r];   // the bf16 logit the unfused path samples
+          if (!greedy) v = v * inv_t + gumbel_noise(seed, idx);
+          if (loc >= sa.vvalid) v = -INFINITY;
+          better(bv, bi, v, idx);
+        }
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        better(bv, bi, ov, oi);
+      }
+      if (g == 0) {
+        const long slot = (long)m * sa.pstride + tile * WA + wa;
+        sa.pv[slot] = bv;
+        sa.pi[slot] = bi;
       }
     }
     return;
@@ -459,7 +547,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 template <int NF, int MT, int WA>
 int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
   if (wrow)
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, false, true>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SLAB, true>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
   else
     hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
@@ -471,15 +559,55 @@ template <int NF, int MT, int WA>
 int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
   if (wrow)
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, true, 150, NF == 2 ? 16 : 8>), dim3(N / (16 * NF)), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
   else
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, true>), dim3(N / (16 * NF)), dim3(256), 0, st,
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, false, 150, NF == 2 ? 16 : 8>), dim3(N / (16 * NF)), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
   return (int)hipGetLastError();
 }
 
+template <int NF, int MT, int WA>
+int launch_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
+                hipStream_t st) {
+  if (wrow)
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, true, 150, 16>), dim3(N / (16 * NF)), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
+  else
+    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, false, 150, 16>), dim3(N / (16 * NF)), dim3(256), 0, st,
+                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
+  return (int)hipGetLastError();
+}
+
+// the streaming LM head: row-major W (wrow) or its fragment-tiled copy; ring budget 150 KiB (one
+// workgroup per CU) or 72 KiB (two)
+template <int NF, int MT, int WA>
+int launch_sample(const void* X, int ldx, const void* Wt, int K, int M, int N, int wrow, int ring2, const SkSample& sa,
+                  hipStream_t st) {
+  const dim3 grid(N / (16 * NF)), block(256);
+#define SK_SAMPLE_LAUNCH(WROW_, KB_)                                                                               \
+  hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SAMPLE, WROW_, KB_, 16>), grid, block, 0, st, (const bf16*)X, ldx, \
+                     (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)nullptr, 0, sa)
+  // the 72-KiB ring only where it still holds >= 3 stages (else the 150-KiB one)
+  constexpr bool R2 = Ring<NF, MT, 72, 16>::NBUF >= 3;
+  if constexpr (R2) {
+    if (ring2) {
+      if (wrow) SK_SAMPLE_LAUNCH(true, 72);
+      else SK_SAMPLE_LAUNCH(false, 72);
+      return (int)hipGetLastError();
+    }
+  }
+  if (wrow) SK_SAMPLE_LAUNCH(true, 150);
+  else SK_SAMPLE_LAUNCH(false, 150);
+#undef SK_SAMPLE_LAUNCH
+  return (int)hipGetLastError();
+}
+
 }  // namespace
+
+// lm_sample_final_kernel's launcher (gemm_prefill.hip): per row, the best of P (score, token) pairs
+extern "C" int penny_lm_sample_final(const float* pv, const int* pi, int P, int M, int* out, int* pairs,
+                                     hipStream_t stream);
 
 // Fused gate|up + SiLU*up for 16 < M <= 256 (K9 at mid-batch decode): W = tile_weight(interleave16
 // gate|up) [N = 2F rows], Y [M, F] bf16 with row stride ldy.  No split-K: N = 28672 already gives
@@ -488,9 +616,17 @@ int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy,
 PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
                                      int nf, int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 4 && nf != 8) || N % (16 * nf))
+  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
   const int mt = (M + 15) / 16;
+  // nf = 2 (one (gate, up) pair per workgroup, WA = 1): twice the workgroups of nf = 4 for narrow
+  // TP shards (Llama-3-70B TP=8 gate|up: N = 7168 -> 224 workgroups)
+  if (nf == 2) {   // WA = 1 -> 4 token-tile wave columns: token tiles rounded up to a multiple of 4
+    if (mt <= 4) return launch_silu<2, 4, 1>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
+    if (mt <= 8) return launch_silu<2, 8, 1>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
+    if (mt <= 12) return launch_silu<2, 12, 1>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
+    return launch_silu<2, 16, 1>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
+  }
 #define GU_CASE(MT_, WA4_, WA8_)                                                          \
   if (mt <= MT_) {                                                                      \
     if (nf == 4) return launch_silu<4, MT_, WA4_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream); \
@@ -581,4 +717,69 @@ PENNY_API int penny_splitk_reduce(const void* P, int S, int M, int N, void* Y, i
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, stream,
                      (const float*)P, S, M, N, (bf16*)Y, ldy, (const bf16*)R, ldr);
   return (int)hipGetLastError();
+}
+
+// Row-parallel decode projection with a bf16 output (no split-K): Y [M, N] (row stride ldy) =
+// X [M, K] x W [N, K]^T, one workgroup per 16*nf W rows -- the TP shards of O / down whose output
+// feeds the all-reduce directly (Llama-3-70B TP=8: N = 8192 -> 256 workgroups at nf = 2).
+// Contract (checked): N % (16*nf) == 0, nf in {2, 4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0,
+// 1 <= M <= 256.
+PENNY_API int penny_splitk_gemm_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
+                                     int nf, int wrow, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
+    return (int)hipErrorInvalidValue;
+  const int mt = (M + 15) / 16;
+#define BF_CASE(MT_, WA2_, WA4_, WA8_)                                                          \
+  if (mt <= MT_) {                                                                            \
+    if (nf == 2) return launch_bf16<2, MT_, WA2_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);  \
+    if (nf == 4) return launch_bf16<4, MT_, WA4_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);  \
+    return launch_bf16<8, MT_, WA8_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);               \
+  }
+  BF_CASE(2, 2, 2, 2)
+  BF_CASE(4, 1, 1, 2)
+  BF_CASE(6, 2, 2, 2)
+  BF_CASE(8, 1, 1, 2)
+  BF_CASE(12, 1, 1, 2)
+  BF_CASE(16, 1, 1, 2)
+#undef BF_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+// Weight-streaming LM head + sampler (K11 + K12) for decode batches, full vocabulary or a TP rank's
+// padded shard: W [Vpad, K] (row-major with wrow = 1, else tile_weight's copy) holds global rows
+// voff .. voff + vvalid - 1 then padding; per row m the Gumbel-max (temps[m] > 0) / argmax sample.
+// out [M] int32 (the token) and/or pairs [M, 2] int32 (score bits, global id: the shard's candidate).
+// workspace >= 2 * M * (Vpad / (16*nf)) * 2 floats.  ring2: the 72-KiB ring (two workgroups per CU).
+// Contract (checked): 1 <= M <= 128, Vpad % (16*nf) == 0, nf in {4, 8}, 0 < vvalid <= Vpad,
+// K % 64 == 0, ldx % 8 == 0.
+PENNY_API int penny_lm_head_stream_sample(const void* X, int ldx, const void* W, int K, int M, int Vpad, int vvalid,
+                                          int voff, const float* temps, const unsigned long long* seeds,
+                                          void* workspace, int* out, int* pairs, int nf, int wrow, int ring2,
+                                          hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 128 || (nf != 4 && nf != 8) || Vpad % (16 * nf) || vvalid <= 0 || vvalid > Vpad || voff < 0 || K % 64 ||
+      ldx % 8 || !temps || !seeds || !workspace || (!out && !pairs))
+    return (int)hipErrorInvalidValue;
+  const int tiles = Vpad / (16 * nf), mt = (M + 15) / 16;
+  // wave split per (nf, token tiles): as penny_splitk_gemm's table
+  const int wa = nf == 8 ? 2 : (mt <= 2 || (mt > 4 && mt <= 6) ? 2 : 1);
+  const int pstride = tiles * wa;
+  float* pv = static_cast<float*>(workspace);
+  int* pi = reinterpret_cast<int*>(pv + (long)M * pstride);
+  const SkSample sa{temps, seeds, pv, pi, pstride, voff, vvalid};
+  int rc;
+#define LS_CASE(MT_, WA4_)                                                                                      \
+  if (mt <= MT_) {                                                                                              \
+    if (nf == 4) rc = launch_sample<4, MT_, WA4_>(X, ldx, W, K, M, Vpad, wrow, ring2, sa, stream);              \
+    else rc = launch_sample<8, MT_, 2>(X, ldx, W, K, M, Vpad, wrow, ring2, sa, stream);                          \
+  } else
+  LS_CASE(2, 2)
+  LS_CASE(4, 1)
+  LS_CASE(6, 2)
+  LS_CASE(8, 1)
+  return (int)hipErrorInvalidValue;
+#undef LS_CASE
+  if (rc) return rc;
+  return penny_lm_sample_final(pv, pi, pstride, M, out, pairs, stream);
 }

@@ -77,6 +77,9 @@ class StepRing {
     if (create) {
       if (nslots < 2 || slot_bytes < 64 || nreaders < 1 || nreaders > kMaxReaders)
         throw std::invalid_argument("bad ring geometry");
+      // every SlotHeader (and its std::atomic seq) must sit on a 64-B line: slot payloads are
+      // rounded up to whole lines, and the rounded size is what the header records
+      slot_bytes = (slot_bytes + 63) & ~uint64_t(63);
       bytes_ = sizeof(Header) + nslots * (sizeof(SlotHeader) + slot_bytes);
       shm_unlink(name.c_str());
       fd_ = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
@@ -118,6 +121,16 @@ class StepRing {
       munmap(base_, bytes_);
       ::close(fd_);
       throw std::runtime_error("ring " + name + " has a bad magic word");
+    } else {
+      // the mapping must hold the geometry the header claims, with line-aligned slots
+      const uint64_t ns = hdr_->nslots, sb = hdr_->slot_bytes;
+      const bool ok = ns >= 2 && sb >= 64 && sb % 64 == 0 && hdr_->nreaders >= 1 && hdr_->nreaders <= kMaxReaders &&
+                      bytes_ >= sizeof(Header) + ns * (sizeof(SlotHeader) + sb);
+      if (!ok) {
+        munmap(base_, bytes_);
+        ::close(fd_);
+        throw std::runtime_error("ring " + name + " has an inconsistent geometry");
+      }
     }
   }
 

@@ -90,6 +90,17 @@ class ContextParallelPrefill:
             except StopIteration:
                 self.active = None
                 eng = self.engine
+                if seq.finished:
+                    # aborted while the pass ran (Scheduler.abort cannot see it: the sequence is in
+                    # neither queue, and its blocks were still being written by the K/V sink).  The
+                    # followers ran the whole collective pass with us; now the blocks go back to the
+                    # pool and the sequence never reaches the scheduler.
+                    eng.bm.free(seq)
+                    seq.block_table = []
+                    self.stats["cp_aborted"] = self.stats.get("cp_aborted", 0) + 1
+                    logger.info(f"context-parallel prefill of {S} tokens finished after its request was aborted: "
+                                "KV blocks freed")
+                    return
                 seq.num_computed = P + S
                 seq.num_prefilled += S
                 eng.bm.commit(seq)

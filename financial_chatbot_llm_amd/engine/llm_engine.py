@@ -99,6 +99,11 @@ class LLMEngine:
                     comm.enable_second_channel()     # the second decode micro-batch chain's AR
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
+                comm.AR_STATUS.update(custom=False, self_test=f"unavailable: {e}")
+            # first contact: the custom kernels must reproduce the exact sum on THIS node before any
+            # token depends on them; any rank's failure sends every rank to RCCL
+            if comm.custom_all_reduce() is not None and getattr(cfg, "custom_ar_self_test", True):
+                comm.verify_custom_all_reduce()
         if self.ps.tp_size > 1 and getattr(cfg, "step_ring", True):
             comm.enable_step_channel()      # collective too; None -> gloo C4
         self.profiler = StepProfiler(rank=self.ps.rank)

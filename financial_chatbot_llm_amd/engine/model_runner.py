@@ -412,6 +412,10 @@ class ModelRunner:
         m = self.model
         return getattr(m, "tp_size", 1) == 1 and hasattr(m, "lm_weight") and ops.fused_lm_head_ok(h, m.lm_weight())
 
+    def _lm_tiled(self):
+        f = getattr(self.model, "lm_tiled", None)
+        return f() if f is not None else None
+
     def _shard_sampling(self) -> bool:
         """TP: rows without top-k / top-p are sampled vocab-parallel (``sample_vocab_parallel``:
         [B, 2] candidates all-gathered instead of the [B, V] logits); ``PENNY_VOCAB_PARALLEL_SAMPLE=0``
@@ -434,7 +438,8 @@ class ModelRunner:
             return self.model.sample_vocab_parallel(hs, self._to_dev(si.temps), self._to_dev(si.seeds))
         if not self._has_filters(si) and self._fused_sampling(hs):
             self.stats["fused_lm_head_steps"] = self.stats.get("fused_lm_head_steps", 0) + 1
-            return ops.lm_head_sample(hs, self.model.lm_weight(), self._to_dev(si.temps), self._to_dev(si.seeds))
+            return ops.lm_head_sample(hs, self.model.lm_weight(), self._to_dev(si.temps), self._to_dev(si.seeds),
+                                      wt=self._lm_tiled())
         return self.sample(self.model.logits(hs), si)
 
     def sample(self, logits: torch.Tensor, si: StepInputs) -> torch.Tensor:
@@ -547,6 +552,19 @@ class ModelRunner:
                               and getattr(m.cfg, "arch", "") == "llama" and comm.custom_all_reduce() is not None
                               and getattr(comm, "_CUSTOM_AR_2", None) is not None
                               and os.environ.get("PENNY_TP_DUAL_DECODE", "1") != "0")
+            if self._dual and self.cascade:
+                # the two chains carry no cascade plan (forward_decode_dual): never drop it silently
+                logger.warning("TP dual decode disabled: cascade attention is on")
+                self._dual = False
+            if self._dual:
+                # each chain's all-reduce must fit ITS custom instance: a half batch falling back to
+                # RCCL would put two streams' RCCL collectives on one communicator inside one graph
+                need = ((self.max_decode_batch + 1) // 2) * m.cfg.hidden_size * 2
+                cap = min(comm.custom_all_reduce().max_bytes, comm._CUSTOM_AR_2.max_bytes)
+                if need > cap:
+                    logger.warning(f"TP dual decode disabled: a half batch all-reduces {need} B > the custom "
+                                   f"all-reduce's {cap} B")
+                    self._dual = False
             if self._dual:
                 self.decode_ws2 = DecodeWorkspace.create(self._max_decode_ws, m.hq, m.D, self.max_model_len,
                                                          self.device)
@@ -570,7 +588,7 @@ class ModelRunner:
         if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
             return self.model.sample_vocab_parallel(h, s["temps"][:B], s["seeds"][:B])
         if self._fused_sampling(h):
-            return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B])
+            return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B], wt=self._lm_tiled())
         logits = self.model.logits(h)
         # the top-k/top-p threshold kernel is always in the graph: unfiltered rows (k=0, p=1) exit
         # after reading their parameters

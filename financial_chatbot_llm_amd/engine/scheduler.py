@@ -109,7 +109,10 @@ class Scheduler:
         # short_first: aged long-output prompts keep priority over fresh long ones but no longer
         # over short-output (decide-class) prompts, which are bounded in size (admission classes
         # 0 preempted, 1 short, 2 aged long, 3 rest; off: short and aged share class 1)
-        self.short_first = short_first
+        # The reservation is only meaningful with short_first: otherwise aged long-output prompts
+        # share class 1 with the short ones and, sorted by arrival, could spend the reserved tokens
+        #  -- so a reserve turns short_first on.
+        self.short_first = short_first or short_reserve_tokens > 0
         # TTFT-tail anatomy: steps that ended with a short-output prompt still waiting, by what
         # stopped admission ("budget" / "grow" / "seqs" / "pending") and where those steps'
         # tokens went (decode rows, speculative chunks, continuing prefills, admitted prompts)

@@ -157,6 +157,25 @@ class DecoderModel:
             if name.endswith((".qkv", ".o", ".down", ".gate_up")) and uses_tiled_weight(*t.shape):
                 self.wt[name] = tile_weight(t)
         self._pad_vocab_shard()
+        lm = self._lm_pad
+        if lm is not None and lm.shape[0] % 64 == 0 and lm.shape[1] % 64 == 0 and self._tile_lm_head():
+            # the decode-size streaming LM head + sampler reads 1-KiB fragment pieces (3-7 % faster
+            # than the row-major stream, profiles/r5_lm_head_stream.jsonl)
+            self.wt["lm_head"] = tile_weight(lm)
+
+    def _tile_lm_head(self) -> bool:
+        """A fragment-tiled LM-head copy costs its size in HBM: made when the weights use at most 40 %
+        of the device (Llama-3-8B, any TP=8 shard, Mixtral fp8), not for Llama-3-70B at TP=1, whose
+        KV pool is already smaller than its working set.  ``PENNY_LM_TILED=0/1`` overrides."""
+        mode = os.environ.get("PENNY_LM_TILED", "auto")
+        if mode in ("0", "1"):
+            return mode == "1"
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        return self.num_bytes() <= 0.4 * total
+
+    def lm_tiled(self) -> Optional[torch.Tensor]:
+        """The fragment-tiled copy of the (padded) LM-head weight, if one was made."""
+        return self.wt.get("lm_head")
 
     def _pad_vocab_shard(self) -> None:
         """Under TP the LM-head shard (V/tp rows: 16,032 for Llama-3 at TP=8) lives in a buffer padded
@@ -444,7 +463,7 @@ class DecoderModel:
         w = self.lm_weight()
         pad = getattr(self, "_lm_pad", None)
         if pad is not None and ops.fused_lm_head_ok(h, pad):
-            pairs = ops.lm_head_sample_shard(h, pad, w.shape[0], self.vocab_start, temps, seeds)
+            pairs = ops.lm_head_sample_shard(h, pad, w.shape[0], self.vocab_start, temps, seeds, wt=self.lm_tiled())
         else:
             pairs = ops.sample_shard(linear(h, w), temps, seeds, self.vocab_start, self.cfg.vocab_size)
         return ops.pick_pairs(comm.tp_all_gather_pairs(pairs))

@@ -10,7 +10,8 @@ from .attention import (KV_BS, CascadeInputs, DecodeWorkspace, decode, default_s
 from .embedding import embedding
 from .norm import layer_norm, rms_norm
 from .retrieval import filtered_topk
-from .sampling import (apply_top_k_top_p, fused_lm_head_ok, lm_head_sample, lm_head_sample_shard, pick_pairs, sample,
+from .sampling import (apply_top_k_top_p, fused_lm_head_ok, lm_head_sample, lm_head_sample_shard, lm_head_stream_sample,
+                       pick_pairs, sample,
                        sample_shard)
 
 __all__ = ["gelu_", "silu_mul", "KV_BS", "DecodeWorkspace", "decode", "default_scale", "prefill", "rope_cos_sin",

@@ -34,6 +34,10 @@ _SIGS = {
     "penny_splitk_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_vw_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_reduce": [P, c_int, c_int, c_int, P, c_int, P, c_int, P],
+    "penny_splitk_gemm_bf16": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
+    "penny_lm_head_stream_sample": [P, c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, c_int,
+                                    c_int, P],
+    "penny_lm_sample_final": [P, P, c_int, c_int, P, P, P],
     "penny_gateup_silu_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gemm_prefill": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
                            P, c_long, P, c_int, c_int, P],

@@ -108,6 +108,18 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
         cfg = splitk_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if cfg is not None:
             return Slabs(splitk_partials(x, src, N_, *cfg, rowmajor=rowmajor))
+    if not slabs and epilogue is None and residual is None and N.use_native(x) and x.stride(1) == 1 \
+            and x.stride(0) % 8 == 0:
+        cfg = bf16_config(M, N_, K)
+        if cfg is not None:
+            # row-parallel TP shard (O / down): bf16 straight into the all-reduce -- one launch with
+            # no K split, or split-K slabs + the reduce where the shard is too narrow for that
+            S, nf, rm = cfg
+            rm = rm or wt is None
+            ww = w if rm else wt
+            if S == 1:
+                return splitk_bf16(x, ww, N_, nf, rowmajor=rm)
+            return splitk_reduce(splitk_partials(x, ww, N_, S, nf, rowmajor=rm))
     if epilogue == "silu" and src is not None and residual is None:
         nf = gateup_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if nf is not None:
@@ -180,14 +192,59 @@ SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
     # Llama-3-70B (TP=1), streamed row-major (profiles/r1_splitk_70b.jsonl): down 1.2-1.9x hipBLASLt
     # at M = 32..256; O 1.1-1.5x from M = 96 (S = 0: the library is as fast below that)
-    (8192, 28672): [(16, 4, 8), (48, 2, 4), (128, 8, 8), (256, 4, 8)],
-    (8192, 8192): [(64, 0, 0), (256, 4, 8)],
+    # r5 re-measure at HEAD (profiles/r5_shard_shapes.jsonl, row-major W): down 1.2-2.1x, O 1.2-1.5x,
+    # QKV 1.1-1.2x at M = 1..256 (QKV: S = 2 above 32 rows keeps the RoPE pass's slab read small)
+    (8192, 28672): [(8, 8, 2), (256, 4, 8)],
+    (8192, 8192): [(32, 8, 2), (128, 8, 8), (256, 4, 8)],
+    (10240, 8192): [(32, 8, 2), (256, 2, 8)],
     # Llama-3-70B TP=8 per-rank QKV shard (column-parallel: the RoPE/KV-write pass consumes the
-    # slabs, no all-reduce in between): 1.6-2.4x hipBLASLt at M = 16..256 (r1_splitk_70b_tp8.jsonl)
+    # slabs, no all-reduce in between): 1.4-2.9x hipBLASLt at M = 1..256 (r5_shard_shapes.jsonl)
     (1280, 8192): [(256, 8, 4)],
 }
-# shapes whose row-major stream measured as fast as the tiled copy: never tiled (70B: 48 GB saved)
-TILE_FREE = {(8192, 28672), (8192, 8192), (1280, 8192)}
+# shapes whose row-major stream measured within a few % of the tiled copy: never tiled (70B: 61 GB
+# saved at TP=1, where HBM is the KV pool's)
+TILE_FREE = {(8192, 28672), (8192, 8192), (1280, 8192), (10240, 8192)}
+
+
+# (N, K) -> [(max M, S, nf, rowmajor), ...]: decode-size projections whose caller wants a bf16 output
+# (no slabs: the row-parallel TP shards of O / down, whose output goes straight into the
+# all-reduce): S = 1 -> the split-K kernel without a K split and the SK_BF16 epilogue
+# (penny_splitk_gemm_bf16), S > 1 -> split-K slabs + penny_splitk_reduce.  Measured against hipBLASLt
+# with W streamed from HBM (bench/kernels.py shard_shapes, profiles/r5_shard_shapes*.jsonl):
+# Llama-3-70B TP=8 O 1.5-2.0x, down 1.1-1.6x at M = 1..256.
+DECODE_BF16: Dict[Tuple[int, int], List[Tuple[int, int, int, bool]]] = {
+    (8192, 1024): [(32, 1, 4, True), (256, 1, 2, True)],                                        # 70B TP=8 O
+    (8192, 3584): [(64, 1, 2, True), (96, 2, 4, True), (128, 4, 8, True), (256, 2, 4, True)],   # 70B TP=8 down
+}
+
+
+def bf16_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int, bool]]:
+    """(S, nf, rowmajor) for the bf16-output decode GEMM at this shape, or None (``PENNY_SPLITK=0``
+    disables; ``PENNY_SPLITK=force`` takes it for any shape the kernel accepts)."""
+    mode = os.environ.get("PENNY_SPLITK", "1")
+    if mode == "0" or M > 256 or K % 64:
+        return None
+    for max_m, S, nf, rm in DECODE_BF16.get((N_, K), ()):
+        if M <= max_m:
+            return (S, nf, rm) if nf > 0 and K % (64 * S) == 0 else None
+    if mode == "force":
+        for nf in (2, 4):
+            if N_ % (16 * nf) == 0:
+                return 1, nf, True
+    return None
+
+
+def splitk_bf16(x: torch.Tensor, w: torch.Tensor, N_: int, nf: int, rowmajor: bool = True,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 y = x @ w.T on the decode split-K kernel without a K split (``w`` row-major [N, K], or
+    ``tile_weight``'s copy with ``rowmajor=False``)."""
+    M, K = x.shape
+    if not N.use_native(x):
+        return F.linear(x.float(), (w if rowmajor else untile_weight(w)).float()).to(x.dtype)
+    y = out if out is not None else torch.empty((M, N_), dtype=x.dtype, device=x.device)
+    N.call("penny_splitk_gemm_bf16", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), y.stride(0), M, N_, nf,
+           int(rowmajor), N.stream())
+    return y
 
 
 # "tiled": the decode kernels stream a fragment-tiled copy of each measured projection (made once

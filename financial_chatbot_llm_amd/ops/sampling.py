@@ -2,13 +2,24 @@
 per-row top-k / top-p filters (HIP radix-select threshold, graph-capturable; ``sampler.hip``)."""
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
 from . import _native as N
 
 SPLITS = 16  # vocab slices per row in the HIP sampler (SAMPLE_SPLITS)
+
+
+def _aligned_rows(logits: torch.Tensor) -> torch.Tensor:
+    """The HIP samplers load 16-B vectors from each row: a row stride that is not a multiple of 8
+    elements (a vocab shard of odd width, e.g. V/tp) is copied into a buffer whose stride is."""
+    if logits.stride(1) == 1 and logits.stride(0) % 8 == 0:
+        return logits
+    B, V = logits.shape
+    buf = torch.empty((B, -(-V // 8) * 8), dtype=logits.dtype, device=logits.device)
+    buf[:, :V].copy_(logits)
+    return buf[:, :V]
 
 
 def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
@@ -26,7 +37,7 @@ def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor
     filt = top_k is not None and top_p is not None
     if N.use_native(logits):
         out = torch.empty((B,), dtype=torch.int32, device=logits.device) if out is None else out
-        assert logits.stride(1) == 1 and logits.stride(0) % 8 == 0
+        logits = _aligned_rows(logits)
         ws = torch.empty((B * SPLITS * 2 + B,), dtype=torch.float32, device=logits.device)
         tk = top_k.to(torch.int32).contiguous() if filt else None
         tp = top_p.to(torch.float32).contiguous() if filt else None
@@ -53,17 +64,37 @@ def sample(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor
     return res.to(logits.device)
 
 
-# Fused LM head + sampler (K11 + K12, ``gemm_prefill.hip`` EPI_SAMPLE): the vocabulary projection
-# runs on the 256x256 MFMA tile kernel and every lane Gumbel-max-scores its logits in registers,
-# so the [M, V] logits never reach HBM and the separate sampler pass disappears.  Its cost is
-# nearly flat in M (two rounds of 501 vocab tiles over 256 CUs for Llama-3: 243-265 us at M = 1-160,
-# 306 us at 256), while hipBLASLt + the sampler grows with M (190 us at M = 1, 266 at 128, 355 at
-# 256): the fused path is taken from FUSED_LM_HEAD_MIN_M rows, where it ties (M = 128) or wins
-# 8-16 % (M = 160-256) (bench/kernels.py lm_head_fused, profiles/r3_lm_head_fused_vs_hipblaslt.jsonl).
-# Below that the 256-row tile's MFMA work and the 1.05 GB weight stream share each CU's time
-# (4.2 TB/s) and the library's streaming GEMM wins.  ``PENNY_FUSED_LM_HEAD=0`` disables it,
-# ``=force`` takes it at every M.
+# Fused LM head + sampler (K11 + K12): no [M, V] logits in HBM and no separate sampler pass -- every
+# lane Gumbel-max-scores its logits in registers.  Two kernels, by rows:
+#   * M >= FUSED_LM_HEAD_MIN_M: the 256x256 MFMA tile kernel (``gemm_prefill.hip`` EPI_SAMPLE), whose
+#     cost is nearly flat in M (two rounds of 501 vocab tiles over 256 CUs for Llama-3: 265 us at
+#     M = 128-160, 306 us at 256) while hipBLASLt + the sampler grows with M (266 at 128, 355 at 256)
+#     (profiles/r3_lm_head_fused_vs_hipblaslt.jsonl);
+#   * M < FUSED_LM_HEAD_MIN_M (decode steps): the weight-streaming split-K kernel
+#     (``gemm_splitk.hip`` SK_SAMPLE, ``penny_lm_head_stream_sample``) -- 128 vocab rows per
+#     workgroup streamed through an LDS ring, all M rows per workgroup, the sampler in its
+#     epilogue; below 128 rows the 256-row tile is MFMA-bound on padding rows (4.2 TB/s) and this
+#     is the weight stream (profiles/r5_lm_head_stream.jsonl).
+# ``PENNY_FUSED_LM_HEAD=0`` disables both (hipBLASLt logits + the sampler), ``=force`` takes the tile
+# kernel at every M; ``PENNY_LM_STREAM=0`` drops the streaming kernel only.
 FUSED_LM_HEAD_MIN_M = 128
+STREAM_MAX_M = 127
+# (max M, nf, 72-KiB ring) of the streaming kernel, first match wins (bench/kernels.py lm_head_stream,
+# profiles/r5_lm_head_stream*.jsonl): 64-row vocab tiles and two workgroups per CU up to 64 rows,
+# 128-row tiles above (half the X re-reads per vocab row)
+STREAM_TABLE = ((64, 4, True), (STREAM_MAX_M, 8, True))
+
+
+def stream_cfg(M: int) -> Tuple[int, bool]:
+    for max_m, nf, r2 in STREAM_TABLE:
+        if M <= max_m:
+            return nf, r2
+    return STREAM_TABLE[-1][1:]
+
+
+def _stream_ok(M: int) -> bool:
+    import os
+    return M <= STREAM_MAX_M and os.environ.get("PENNY_LM_STREAM", "1") != "0"
 
 
 def fused_lm_head_ok(h: torch.Tensor, w: torch.Tensor) -> bool:
@@ -75,23 +106,57 @@ def fused_lm_head_ok(h: torch.Tensor, w: torch.Tensor) -> bool:
     V = w.shape[0]
     if V % 256 or K % 64 or h.stride(1) != 1 or h.stride(0) % 8 or not w.is_contiguous():
         return False
-    return mode == "force" or M >= FUSED_LM_HEAD_MIN_M
+    return mode == "force" or M >= FUSED_LM_HEAD_MIN_M or _stream_ok(M)
+
+
+def lm_head_stream_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
+                          vvalid: Optional[int] = None, voff: int = 0, pairs: bool = False,
+                          out: Optional[torch.Tensor] = None, nf: Optional[int] = None,
+                          rowmajor: Optional[bool] = None, ring2: Optional[bool] = None) -> torch.Tensor:
+    """The weight-streaming fused LM head + sampler (M <= 128 rows): ``w`` [Vpad, K] row-major (or,
+    ``rowmajor=False``, its ``ops.gemm.tile_weight`` copy of the [Vpad, K] weight), global rows
+    voff .. voff+vvalid-1 then padding.  Returns int32 tokens [M], or (``pairs``) the [M, 2]
+    (score bits, global id) shard candidates of :func:`sample_shard`."""
+    M, K = h.shape
+    Vpad = w.shape[0] * (16 if w.dim() == 4 else 1)
+    vvalid = Vpad if vvalid is None else vvalid
+    d_nf, d_r2 = stream_cfg(M)
+    nf = d_nf if nf is None else nf
+    rowmajor = (w.dim() == 2) if rowmajor is None else rowmajor
+    ring2 = d_r2 if ring2 is None else ring2
+    P = Vpad // (16 * nf) * 2
+    ws = torch.empty((2 * M * P,), dtype=torch.float32, device=h.device)
+    temps, sd = temperatures.to(torch.float32).contiguous(), seeds.contiguous()   # alive across the launch
+    if pairs:
+        res = torch.empty((M, 2), dtype=torch.int32, device=h.device)
+        o, pr = None, res
+    else:
+        res = torch.empty((M,), dtype=torch.int32, device=h.device) if out is None else out
+        o, pr = res, None
+    N.call("penny_lm_head_stream_sample", N.ptr(h), h.stride(0), N.ptr(w), K, M, Vpad, int(vvalid), int(voff),
+           N.ptr(temps), N.ptr(sd), N.ptr(ws), N.ptr(o), N.ptr(pr), int(nf), int(rowmajor), int(ring2), N.stream())
+    return res
 
 
 def lm_head_sample(h: torch.Tensor, w: torch.Tensor, temperatures: torch.Tensor, seeds: torch.Tensor,
-                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sample one token per row of ``h`` [M, K] from softmax((h @ w.T) / T) (T <= 0: greedy) without
     materialising the logits.  Same noise as :func:`sample` (counter-based on (seed, token id)),
     scored on the bf16-rounded logits, so for equal logits both paths pick the same token.  The
-    tile GEMM and hipBLASLt accumulate in different orders, though, so a row whose two best scores
+    MFMA kernels and hipBLASLt accumulate in different orders, though, so a row whose two best scores
     lie within logit rounding can differ between the paths (tokens are reproducible up to logit
     rounding; the rate is measured by tests/test_kernels_gpu.py::test_fused_vs_unfused_sampling_
-    token_agreement).  No top-k / top-p (those rows need the whole distribution: use ``sample``)."""
+    token_agreement).  No top-k / top-p (those rows need the whole distribution: use ``sample``).
+    ``wt``: the fragment-tiled copy of ``w`` (``ops.gemm.tile_weight``), streamed instead of ``w`` by
+    the decode-size kernel when given."""
+    import os
     M, K = h.shape
     V = w.shape[0]
     if not N.use_native(h):
         import torch.nn.functional as F
         return sample(F.linear(h.float(), w.float()).to(h.dtype), temperatures, seeds, out=out)
+    if _stream_ok(M) and os.environ.get("PENNY_FUSED_LM_HEAD") != "force" and V % (16 * stream_cfg(M)[0]) == 0:
+        return lm_head_stream_sample(h, wt if wt is not None else w, temperatures, seeds, out=out)
     out = torch.empty((M,), dtype=torch.int32, device=h.device) if out is None else out
     ws = torch.empty((2 * M * 2 * (V // 256),), dtype=torch.float32, device=h.device)
     temps, sd = temperatures.to(torch.float32).contiguous(), seeds.contiguous()   # alive across the launch
@@ -113,7 +178,7 @@ def sample_shard(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.
     bits, global id) of each row's Gumbel-max (T <= 0: argmax) winner within the shard."""
     B, Vs = logits.shape
     if N.use_native(logits):
-        assert logits.stride(1) == 1 and logits.stride(0) % 8 == 0
+        logits = _aligned_rows(logits)           # ADVICE r4: any shard width, no assert on the TP step
         pairs = torch.empty((B, 2), dtype=torch.int32, device=logits.device)
         ws = torch.empty((2 * B * SPLITS,), dtype=torch.float32, device=logits.device)
         N.call("penny_sample_shard", N.ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
@@ -138,11 +203,15 @@ def sample_shard(logits: torch.Tensor, temperatures: torch.Tensor, seeds: torch.
 
 
 def lm_head_sample_shard(h: torch.Tensor, w_pad: torch.Tensor, vvalid: int, voff: int, temperatures: torch.Tensor,
-                         seeds: torch.Tensor) -> torch.Tensor:
+                         seeds: torch.Tensor, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused LM head + sampler on one vocab shard: ``w_pad`` [Vpad, K] (Vpad % 256 == 0) holds global
     rows voff .. voff+vvalid-1 then padding -> pairs [M, 2] as :func:`sample_shard`."""
+    import os
     M, K = h.shape
     Vpad = w_pad.shape[0]
+    if _stream_ok(M) and os.environ.get("PENNY_FUSED_LM_HEAD") != "force" and Vpad % (16 * stream_cfg(M)[0]) == 0:
+        return lm_head_stream_sample(h, wt if wt is not None else w_pad, temperatures, seeds, vvalid=vvalid,
+                                     voff=voff, pairs=True)
     pairs = torch.empty((M, 2), dtype=torch.int32, device=h.device)
     ws = torch.empty((2 * M * 2 * (Vpad // 256),), dtype=torch.float32, device=h.device)
     temps, sd = temperatures.to(torch.float32).contiguous(), seeds.contiguous()   # alive across the launch

@@ -92,6 +92,34 @@ def _ar_instance():
     return _CUSTOM_AR_2 if _CHANNEL == 1 else _CUSTOM_AR
 
 
+# what the TP group's custom all-reduce ended up as: reported in the bench JSON per rank
+AR_STATUS = {"custom": False, "self_test": "not run"}
+
+
+def verify_custom_all_reduce() -> bool:
+    """Init-time first contact (every TP rank together): self-test each enabled custom instance
+    against the exact sum (``custom_ar.self_test``: one-shot, two-shot, all-gather, bounded-wait
+    flag).  On any rank's mismatch or expired wait EVERY rank disables the custom path and RCCL
+    carries all TP collectives for the process lifetime.  Returns whether the custom path stays."""
+    import logging
+    log = logging.getLogger(__name__)
+    if _CUSTOM_AR is None:
+        AR_STATUS.update(custom=False)
+        return False
+    for k, ar in ((0, _CUSTOM_AR), (1, _CUSTOM_AR_2)):
+        if ar is None:
+            continue
+        ok, why = ar.self_test()
+        if not ok:
+            log.warning(f"custom all-reduce instance {k} failed its self-test ({why}); RCCL carries every TP "
+                        "collective from now on")
+            disable_custom_all_reduce()
+            AR_STATUS.update(custom=False, self_test=f"failed: {why}")
+            return False
+    AR_STATUS.update(custom=True, self_test="ok")
+    return True
+
+
 def disable_custom_all_reduce() -> None:
     global _CUSTOM_AR, _CUSTOM_AR_2
     for ar in (_CUSTOM_AR_2, _CUSTOM_AR):

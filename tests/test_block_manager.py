@@ -384,3 +384,13 @@ def test_short_wait_records_kv_pool_exhaustion():
     sch.schedule()
     assert decide in sch.waiting
     assert sch.short_wait["grow"] >= 1 and sch.short_wait["budget"] == 0
+
+
+def test_short_reserve_implies_short_first():
+    """with a short-output reservation, aged long-output prompts must not share the
+    short class (they could spend the reserve); the reserve turns short_first on."""
+    from financial_chatbot_llm_amd.engine.block_manager import make_block_manager
+    from financial_chatbot_llm_amd.engine.scheduler import Scheduler
+    bm = make_block_manager(64, 64, True)
+    assert Scheduler(bm, 8, 512, 4096, short_reserve_tokens=256).short_first
+    assert not Scheduler(bm, 8, 512, 4096).short_first

@@ -189,3 +189,68 @@ def test_cp_prefill_interleaves_decode_and_reuses_the_prefix_cache():
     for (k, v), (rk, rv) in zip(to_torch(kv2), ref_kv):
         assert torch.allclose(k, rk, atol=3e-2, rtol=3e-2), (k - rk).abs().max()
         assert torch.allclose(v, rv, atol=3e-2, rtol=3e-2), (v - rv).abs().max()
+
+
+def _worker_abort(rank, world, port, q):
+    """Leader: abort the long request while its CP pass is in progress (one layer per step)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from financial_chatbot_llm_amd.engine import SamplingParams
+        from financial_chatbot_llm_amd.engine.llm_engine import LLMEngine
+        from financial_chatbot_llm_amd.parallel.dist import init_cp_groups, init_distributed, shutdown
+        init_distributed(tp_size=1, backend="gloo", device_type="cpu")
+        init_cp_groups(world)
+        cfg = _cfg(world)
+        cfg.cp_layers_per_step = 1
+        eng = LLMEngine(cfg)
+        if rank == 0:
+            free0 = eng.bm.num_free()
+            long_ = eng.add_request("long", PROMPT, SamplingParams(temperature=0.0, max_tokens=50, ignore_eos=True))
+            eng.step()
+            mid = eng.cp.active is not None            # the pass is in progress
+            eng.abort("long")
+            steps = 0
+            while eng.has_work() and steps < 200:
+                eng.step()
+                steps += 1
+            # the same replica still serves: another long prompt goes through CP afterwards
+            out = eng.generate([PROMPT2], SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True))
+            stats = eng.stats()
+            eng.stop_followers()
+            q.put((rank, mid, len(long_.output_ids), long_ in eng.scheduler.running,
+                   stats.get("cp_aborted", 0), (free0, eng.bm.num_free()), len(out[0])))
+        else:
+            eng.cp_follower_loop()
+            q.put((rank, None, None, None, None, None, None))
+        shutdown()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc(), None, None, None, None))
+
+
+@pytest.mark.timeout(300)
+def test_cp_prefill_abort_mid_pass_frees_blocks():
+    """a request aborted while its context-parallel pass runs must not be handed to the
+    scheduler when the pass ends (it would decode to max_tokens for nobody) and its KV blocks go back
+    to the pool; the followers still finish the collective pass, and the replica keeps serving."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_abort, args=(r, world, port, qq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = qq.get(timeout=280)
+        res[item[0]] = item[1:]
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert not (isinstance(v[0], str) and v[0] == "ERR"), v[1]
+    mid, n_out, running, aborted, (free0, free1), n2 = res[0]
+    assert mid and aborted == 1
+    assert n_out == 0 and not running
+    assert free1 == free0                          # nothing held by the aborted sequence
+    assert n2 == 2

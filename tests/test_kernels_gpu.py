@@ -1183,11 +1183,13 @@ def test_topp_threshold_is_bitwise_repeatable():
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("M,V,K", [(1, 2048, 512), (37, 4096, 1024), (256, 2048, 512), (300, 1024, 256),
                                    (128, 128256, 4096)])
-def test_fused_lm_head_sampler_matches_logits_then_sampler(M, V, K):
+def test_fused_lm_head_sampler_matches_logits_then_sampler(M, V, K, monkeypatch):
     """Same tile accumulation as the bf16 tile GEMM -> identical bf16 logits -> the fused sample must
     equal ops.sample on those logits bit for bit (greedy and Gumbel rows); greedy rows also hold
-    the fp32 reference's max logit up to bf16 rounding."""
+    the fp32 reference's max logit up to bf16 rounding.  (The tile kernel at every M here: below
+    128 rows ops.lm_head_sample takes the streaming kernel, tested below.)"""
     from financial_chatbot_llm_amd.ops import gemm
+    monkeypatch.setenv("PENNY_LM_STREAM", "0")
     g = torch.Generator().manual_seed(M + V)
     x, w = rnd(M, K, gen=g).to(DEV), rnd(V, K, scale=0.05, gen=g).to(DEV)
     temps = torch.tensor([0.0 if i % 3 == 0 else (0.7 if i % 3 == 1 else 1.3) for i in range(M)], device=DEV)
@@ -1204,6 +1206,120 @@ def test_fused_lm_head_sampler_matches_logits_then_sampler(M, V, K):
     if M > 1:
         one = ops.lm_head_sample(x[1:2].contiguous(), w, temps[1:2].contiguous(), seeds[1:2].contiguous())
         assert int(one[0]) == int(got[1])
+
+
+@pytest.mark.parametrize("M,V,K,nf,rowmajor,ring2", [(1, 2048, 512, 8, True, False), (37, 4096, 1024, 4, True, True),
+                                                     (64, 4096, 1024, 8, False, False), (127, 2048, 512, 4, False, True),
+                                                     (1, 128256, 4096, 8, True, False),
+                                                     (100, 128256, 4096, 8, True, False)])
+def test_lm_head_stream_sampler_matches_logits_then_sampler(M, V, K, nf, rowmajor, ring2):
+    """Weight-streaming LM head + sampler (gemm_splitk.hip SK_SAMPLE, M <= 128): its accumulators are
+    the SK_BF16 kernel's of the same shape -> identical bf16 logits -> the sample equals ops.sample
+    on those logits bit for bit; the logits themselves match the fp32 reference; greedy rows pick
+    the fp32 max up to bf16 rounding; a row's token does not depend on the other rows."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M * 3 + V)
+    x, w = rnd(M, K, gen=g).to(DEV), rnd(V, K, scale=0.05, gen=g).to(DEV)
+    wk = w if rowmajor else gemm.tile_weight(w)
+    temps = torch.tensor([0.0 if i % 3 == 0 else (0.7 if i % 3 == 1 else 1.3) for i in range(M)], device=DEV)
+    seeds = (torch.arange(M, dtype=torch.int64) * 7919 + 5).to(DEV)
+    got = ops.lm_head_stream_sample(x, wk, temps, seeds, nf=nf, rowmajor=rowmajor, ring2=ring2)
+    logits = gemm.splitk_bf16(x, wk, V, nf, rowmajor=rowmajor)
+    ref = x.float() @ w.float().t()
+    close(logits, ref, atol=3e-2)
+    assert torch.equal(got.cpu(), ops.sample(logits, temps, seeds).cpu())
+    greedy = (temps <= 0).nonzero().flatten()
+    picked = ref[greedy, got[greedy].long()]
+    assert bool((picked >= ref[greedy].max(-1).values - 2e-2 * ref.abs().max()).all())
+    if M > 1:
+        one = ops.lm_head_stream_sample(x[1:2].contiguous(), wk, temps[1:2].contiguous(), seeds[1:2].contiguous(),
+                                        nf=nf, rowmajor=rowmajor, ring2=ring2)
+        assert int(one[0]) == int(got[1])
+    # the decode-size default route (ops.lm_head_sample below 128 rows) is this kernel
+    if M <= 127 and V % 128 == 0:
+        assert torch.equal(ops.lm_head_sample(x, w, temps, seeds).cpu(),
+                           ops.sample(gemm.splitk_bf16(x, w, V, 8), temps, seeds).cpu())
+
+
+@pytest.mark.parametrize("M", [1, 33, 127])
+def test_lm_head_stream_vocab_shard_pairs(M):
+    """Vocab-parallel form: a TP rank's padded LM-head shard (Llama-3 at TP=8: 16,032 rows in a
+    16,128-row buffer) -> per-row (score, GLOBAL id) candidates equal to sample_shard over the same
+    kernel's logits of the unpadded rows; padding rows never win."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + 17)
+    K, rows, Vpad, voff, vtot = 4096, 16032, 16128, 16032 * 3, 128256
+    x = rnd(M, K, gen=g).to(DEV)
+    wp = torch.zeros(Vpad, K, dtype=torch.bfloat16)
+    wp[:rows] = rnd(rows, K, scale=0.05, gen=g)
+    wp = wp.to(DEV)
+    temps = torch.full((M,), 0.5, device=DEV)
+    temps[::4] = 0.0
+    seeds = (torch.arange(M, dtype=torch.int64) * 31 + 1).to(DEV)
+    pairs = ops.lm_head_stream_sample(x, wp, temps, seeds, vvalid=rows, voff=voff, pairs=True)
+    logits = gemm.splitk_bf16(x, wp, Vpad, 8)[:, :rows].contiguous()
+    want = ops.sample_shard(logits, temps, seeds, voff, vtot)
+    assert torch.equal(pairs.cpu(), want.cpu())
+    assert bool(((pairs[:, 1] >= voff) & (pairs[:, 1] < voff + rows)).all())
+    # the shard entry point routes decode sizes to the streaming kernel
+    assert torch.equal(ops.lm_head_sample_shard(x, wp, rows, voff, temps, seeds).cpu(), pairs.cpu())
+
+
+@pytest.mark.parametrize("M", [1, 37, 128, 256])
+@pytest.mark.parametrize("N_,K,nf", [(8192, 1024, 2), (8192, 3584, 2), (8192, 3584, 4), (512, 1024, 8)])
+def test_splitk_bf16_gemm_tp_row_shards(M, N_, K, nf):
+    """bf16-output decode GEMM (SK_BF16, no K split) at the Llama-3-70B TP=8 row-parallel shard
+    shapes (O [8192, 1024], down [8192, 3584]) vs the fp32 reference; row-major and tiled W agree
+    bitwise; a strided X and a strided output are honoured."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + N_ + K)
+    x = rnd(M, K, gen=g).to(DEV)
+    w = rnd(N_, K, scale=0.02, gen=g).to(DEV)
+    y = gemm.splitk_bf16(x, w, N_, nf)
+    close(y, x.float() @ w.float().t(), atol=3e-2)
+    assert torch.equal(gemm.splitk_bf16(x, gemm.tile_weight(w), N_, nf, rowmajor=False), y)
+    xw = torch.zeros(M, K + 64, dtype=torch.bfloat16, device=DEV)
+    xw[:, 64:] = x
+    out = torch.zeros(M, N_ + 8, dtype=torch.bfloat16, device=DEV)
+    gemm.splitk_bf16(xw[:, 64:], w, N_, nf, out=out[:, :N_])
+    assert torch.equal(out[:, :N_], y) and bool((out[:, N_:] == 0).all())
+
+
+@pytest.mark.parametrize("M", [1, 64, 200])
+def test_gateup_silu_nf2_tp8_shard(M):
+    """The fused gate|up + SiLU kernel at nf = 2 on the Llama-3-70B TP=8 gate|up shard (interleave16
+    of 2 x 3584 rows, K = 8192) vs the fp32 reference; row-major == tiled bitwise."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M + 2)
+    Fr, K = 3584, 8192
+    x = rnd(M, K, gen=g)
+    gate, up = rnd(Fr, K, scale=0.02, gen=g), rnd(Fr, K, scale=0.02, gen=g)
+    wi = gemm.interleave16(gate, up).to(DEV).contiguous()
+    y = gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, 2, rowmajor=True)
+    assert torch.equal(gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, 2), y)
+    xd = x.to(DEV).float()
+    gf, uf = xd @ gate.to(DEV).float().t(), xd @ up.to(DEV).float().t()
+    close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
+
+
+@pytest.mark.parametrize("Vs", [16033, 1001])
+def test_sample_shard_any_width(Vs):
+    """a vocab shard whose width is not a multiple of 8 (row stride V/tp) samples on the
+    device (an aligned copy) instead of asserting; greedy rows equal the argmax, and the result
+    equals the aligned-buffer call bit for bit."""
+    g = torch.Generator().manual_seed(Vs)
+    B = 9
+    logits = rnd(B, Vs, gen=g).to(DEV)
+    temps = torch.full((B,), 0.8, device=DEV)
+    temps[::3] = 0.0
+    seeds = (torch.arange(B, dtype=torch.int64) + 3).to(DEV)
+    pairs = ops.sample_shard(logits, temps, seeds, 5 * Vs, 8 * Vs)
+    buf = torch.zeros(B, Vs + 8 - Vs % 8, dtype=torch.bfloat16, device=DEV)
+    buf[:, :Vs] = logits
+    assert torch.equal(pairs.cpu(), ops.sample_shard(buf[:, :Vs], temps, seeds, 5 * Vs, 8 * Vs).cpu())
+    greedy = (temps <= 0).nonzero().flatten()
+    assert torch.equal(pairs[greedy, 1].cpu().long() - 5 * Vs, logits[greedy].float().argmax(-1).cpu())
+    assert ops.sample(logits, temps, seeds).shape == (B,)
 
 
 @pytest.mark.parametrize("M", [127, 128])

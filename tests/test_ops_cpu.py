@@ -152,10 +152,15 @@ def test_decode_gemm_dispatch_tables(monkeypatch):
     assert gemm.splitk_config(300, 6144, 4096) is None              # prefill size: hipBLASLt
     assert gemm.gateup_config(128, 28672, 4096) == 8 and gemm.gateup_config(200, 28672, 4096) is None
     assert gemm.uses_tiled_weight(6144, 4096) and gemm.uses_tiled_weight(28672, 4096)
-    # Llama-3-70B: library below the measured crossover (S = 0), row-major stream above, no copies
-    assert gemm.splitk_config(32, 8192, 8192) is None and gemm.splitk_config(128, 8192, 8192) == (4, 8)
-    assert gemm.splitk_config(128, 8192, 28672) == (8, 8)
-    assert not gemm.uses_tiled_weight(8192, 28672) and not gemm.uses_tiled_weight(8192, 8192)
+    # Llama-3-70B TP=1 (r5 re-measure): split-K on the row-major stream at every decode M, no copies
+    assert gemm.splitk_config(32, 8192, 8192) == (8, 2) and gemm.splitk_config(128, 8192, 8192) == (8, 8)
+    assert gemm.splitk_config(128, 8192, 28672) == (4, 8) and gemm.splitk_config(4, 8192, 28672) == (8, 2)
+    assert gemm.splitk_config(16, 10240, 8192) == (8, 2) and gemm.splitk_config(200, 10240, 8192) == (2, 8)
+    assert not any(gemm.uses_tiled_weight(*s) for s in ((8192, 28672), (8192, 8192), (10240, 8192)))
+    # Llama-3-70B TP=8 row-parallel shards: bf16 output for the all-reduce (no K split, then slabs)
+    assert gemm.bf16_config(1, 8192, 1024) == (1, 4, True) and gemm.bf16_config(200, 8192, 1024) == (1, 2, True)
+    assert gemm.bf16_config(64, 8192, 3584) == (1, 2, True) and gemm.bf16_config(128, 8192, 3584) == (4, 8, True)
+    assert gemm.bf16_config(300, 8192, 3584) is None and gemm.bf16_config(8, 4096, 4096) is None
     # unmeasured shapes stay on the library without copies unless forced
     assert gemm.splitk_config(64, 1536, 256) is None and not gemm.uses_tiled_weight(1536, 256)
     monkeypatch.setenv("PENNY_SPLITK", "force")

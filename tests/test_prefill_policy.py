@@ -46,8 +46,9 @@ def test_residual_sum_norm_equals_add_then_norm():
 
 
 def test_fused_lm_head_gating(monkeypatch):
-    """The fused LM head + sampler is taken on the device only, from FUSED_LM_HEAD_MIN_M rows, for a
-    vocabulary that tiles by 256 (PENNY_FUSED_LM_HEAD=0 / force override)."""
+    """The fused LM head + sampler is taken on the device only, for a vocabulary that tiles by 256:
+    the tile kernel from FUSED_LM_HEAD_MIN_M rows, the weight-streaming kernel below (off with
+    PENNY_LM_STREAM=0); PENNY_FUSED_LM_HEAD=0 / force override."""
     from financial_chatbot_llm_amd.ops import sampling
     w = torch.zeros(512, 128, dtype=torch.bfloat16)
     h = torch.zeros(200, 128, dtype=torch.bfloat16)
@@ -55,7 +56,11 @@ def test_fused_lm_head_gating(monkeypatch):
     assert not sampling.fused_lm_head_ok(h, w)                 # CPU tensors: no native kernel
     monkeypatch.setattr(sampling.N, "use_native", lambda t: True)
     assert sampling.fused_lm_head_ok(h, w)
+    assert sampling.fused_lm_head_ok(h[:sampling.FUSED_LM_HEAD_MIN_M - 1], w)     # streaming kernel
+    assert sampling.stream_cfg(1) == (4, True) and sampling.stream_cfg(127)[0] == 8
+    monkeypatch.setenv("PENNY_LM_STREAM", "0")
     assert not sampling.fused_lm_head_ok(h[:sampling.FUSED_LM_HEAD_MIN_M - 1], w)
+    monkeypatch.delenv("PENNY_LM_STREAM")
     assert not sampling.fused_lm_head_ok(h, torch.zeros(500, 128, dtype=torch.bfloat16))   # V % 256
     monkeypatch.setenv("PENNY_FUSED_LM_HEAD", "force")
     assert sampling.fused_lm_head_ok(h[:1], w)

@@ -155,3 +155,19 @@ def test_followers_replay_bit_identical_steps_through_the_ring(mode):
         assert all(res[r] is True for r in range(1, world))
     else:
         assert all(res[r] == "timeout" for r in range(1, world))
+
+
+def test_ring_slot_size_rounded_to_whole_lines():
+    """a slot size that is not a multiple of 64 would misalign every SlotHeader after
+    slot 0 (its atomic seq loses single-copy atomicity); the ring rounds it up to whole 64-B lines
+    and records the rounded size, so writer and readers agree on the geometry."""
+    w = rt.StepRing(_name("odd"), True, 3, 100, 1)
+    assert w.slot_bytes == 128
+    r = rt.StepRing(w.name, False, 0, 0, 0)
+    assert r.slot_bytes == 128 and r.nslots == 3
+    msgs = [np.arange(n, dtype=np.uint8) for n in (0, 1, 100, 127, 128, 64)]
+    for m in msgs:
+        assert w.put(m, 5.0)
+        got = r.get(0, 5.0)
+        assert bytes(got) == m.tobytes()
+    assert not w.put(np.zeros(129, dtype=np.uint8), 5.0)   # larger than the rounded slot: refused
