@@ -125,11 +125,21 @@ async def run(args, ps):
     if args.tp > 1 and not ps.is_tp_leader:
         # TP follower: the same engine shard, warmed up (graph capture) in lockstep with its leader,
         # then replays every step the leader broadcasts until the leader's engine shuts down
+        import resource
         from financial_chatbot_llm_amd.engine.llm_engine import LLMEngine
+        from financial_chatbot_llm_amd.parallel import comm
         eng = LLMEngine(ecfg)
         eng.warmup()
+        ru0, t0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
         eng.follower_loop()
-        return None
+        ru1, el = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter() - t0
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        st = eng.stats()
+        return {"follower": True, "host": {"rank": ps.rank, "follower": True, "cpu_s": round(cpu_s, 2),
+                                           "cpu_util": round(cpu_s / max(el, 1e-9), 2),
+                                           "gpu_step_s": st.get("gpu_step_s", 0.0),
+                                           "gpu_idle_between_steps_s": st.get("gpu_idle_between_steps_s", 0.0),
+                                           "custom_all_reduce": dict(comm.AR_STATUS)}}
 
     def sync() -> None:
         if on_gpu:
@@ -182,6 +192,9 @@ async def run(args, ps):
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    import resource
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    ruc0 = resource.getrusage(resource.RUSAGE_CHILDREN)
     t_start = time.perf_counter()
     results = []
     if args.arrival == "closed":
@@ -198,6 +211,10 @@ async def run(args, ps):
     sync()
     barrier()
     elapsed = time.perf_counter() - t_start
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    ruc1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    cpu_child_s = (ruc1.ru_utime - ruc0.ru_utime) + (ruc1.ru_stime - ruc0.ru_stime)
     if prof is not None:
         prof.disable()
         os.makedirs(os.environ["PENNY_PYPROFILE"], exist_ok=True)
@@ -224,7 +241,19 @@ async def run(args, ps):
         return round(1e3 * v[min(len(v) - 1, int(q * len(v)))], 1) if v else None
     latency = {p: {k: {"p50": pct(v, 0.5), "p99": pct(v, 0.99)} for k, v in lat.items()}
                for p, lat in llm.latency.items()}
+    # the host budget of this rank (N engine processes share one host in the dpN
+    # run) and where the GPU's non-busy time went: device step time vs wall, idle between steps
+    from financial_chatbot_llm_amd.parallel import comm
+    nturns = max(sum(r.turns for r in results), 1)
+    gpu_step = stats.get("gpu_step_s", 0.0) - stats0.get("gpu_step_s", 0.0)
+    host = {"rank": ps.rank, "cpu_s": round(cpu_s, 2), "cpu_s_per_turn": round(cpu_s / nturns, 4),
+            "cpu_s_children": round(cpu_child_s, 2), "cpu_util": round(cpu_s / max(elapsed, 1e-9), 2),
+            "gpu_step_s": round(gpu_step, 2), "gpu_busy_frac": round(gpu_step / max(elapsed, 1e-9), 3),
+            "gpu_idle_between_steps_s": round(stats.get("gpu_idle_between_steps_s", 0.0)
+                                              - stats0.get("gpu_idle_between_steps_s", 0.0), 3),
+            "custom_all_reduce": dict(comm.AR_STATUS) if args.tp > 1 else None}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
+            "host": host,
             "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
             "stages": stages, "engine": stats, "tokens": tokens, "latency": latency,
             "plots_ok": sum(r.plots_ok for r in results), "plots_failed": sum(r.plots_failed for r in results)}
@@ -267,11 +296,13 @@ def main(argv=None) -> int:
     res = asyncio.run(run(args, ps))
     if ps.world_size > 1:
         # every rank joins (TP followers contribute None); the replicas' results are the leaders'
-        allr = [None] * ps.world_size
-        dist.all_gather_object(allr, res)
-        allr = [r for r in allr if r is not None]
+        every = [None] * ps.world_size
+        dist.all_gather_object(every, res)
+        allr = [r for r in every if r is not None and not r.get("follower")]
+        hosts = [r["host"] for r in every if r is not None]
     else:
         allr = [res]
+        hosts = [res["host"]]
     if ps.rank == 0:
         tmax = max(r["elapsed"] for r in allr)
         turns = sum(r["turns"] - r["errors"] for r in allr)    # completed turns: errored ones do not count
@@ -311,6 +342,10 @@ def main(argv=None) -> int:
             # per LLM call, engine side: queued before admission / admission -> first token / total
             "engine_call_latency_ms_rank0": allr[0]["latency"],
             "engine_rank0": allr[0]["engine"],
+            "host": {"cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+                     "world_size": ps.world_size, "backend": ps.backend,
+                     "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                     "ranks": hosts},
         }
         line = json.dumps(out)
         print(line, flush=True)

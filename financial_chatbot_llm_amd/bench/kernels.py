@@ -268,20 +268,9 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         ln = ops.attention.prefill_lean_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv)
         ld = torch.from_numpy(ln).to(dev) if ln is not None else None
         lc = (int(ln[0, 1]), int(ln[0, 2]), int(ln[0, 3])) if ln is not None else None
-        # finer lean balance targets: the per-CU share computed as if the chip had 2x / 4x the CUs
-        fine = {}
-        for mult in (2, 4):
-            lf = ops.attention.prefill_lean_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv, cus=256 * mult)
-            fine[mult] = ((torch.from_numpy(lf).to(dev), (int(lf[0, 1]), int(lf[0, 2]), int(lf[0, 3])))
-                          if lf is not None else (wd, None))
 
         def run(v):
             def f():
-                if isinstance(v, str) and v.startswith("fine"):
-                    ops.attention.prefill_variant(4)
-                    wk, lk = fine[int(v[4:])]
-                    ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wk, lean=lk)
-                    return
                 if isinstance(v, str):
                     ops.attention.prefill_variant(int(v.split("_")[1]))
                     ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
@@ -290,8 +279,8 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2": 0, "pf2_sb": 4, "pp": 1, "pp_valu": 2, "pp_prio": 3, "pp_lean": "lean_1",
-                    "pf2_sb_lean": "lean_4", "pf2_sb_lean_x2": "fine2", "pf2_sb_lean_x4": "fine4"}
+        variants = {"pf2": 0, "pf2_sb": 4, "pf2_fold": 5, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
+                    "pf2_fold_lean": "lean_5", "pf2_foldq_lean": "lean_6"}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():
@@ -718,63 +707,6 @@ def bench_gateup(dev, N: int = 28672, K: int = 4096) -> List[Dict]:
         out.append(row)
     del ws, wts
     torch.cuda.empty_cache()
-    return out
-
-
-def bench_vw(dev) -> List[Dict]:
-    """Weight-in-VGPR decode kernel (splitk_vw) vs the LDS-ring split-K / gate|up kernels the
-    serving tables use, on the Llama-3-8B decode projections at M = 32..128 (W rotated over
-    >= 768 MB so every call streams HBM).  Each row: current config, vw configs, TB/s of W."""
-    from ..ops import gemm
-    out = []
-    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336), "gateup": (28672, 4096)}
-    for name, (N, K) in shapes.items():
-        copies = max(2, (768 << 20) // (N * K * 2))
-        wts = [gemm.tile_weight(torch.randn((N, K), device=dev).to(torch.bfloat16)) for _ in range(copies)]
-        it = [0]
-
-        def nxt():
-            it[0] = (it[0] + 1) % copies
-            return it[0]
-
-        wbytes = N * K * 2
-        for M in (32, 64, 96, 128):
-            x = torch.randn((M, K), device=dev).to(torch.bfloat16)
-            row = {"op": "vw", "name": name, "M": M}
-            if name == "gateup":
-                y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
-                cur = timeit(lambda: gemm.gateup_silu(x, wts[nxt()], N, 8, out=y), iters=copies * 2)
-                row["lds_ring_us"] = round(cur, 1)
-                us = timeit(lambda: gemm.splitk_vw(x, wts[nxt()], N, 1, 8, silu=True), iters=copies * 2)
-                row["vw_nf8_us"] = round(us, 1)
-                row["vw_TBps"] = round(wbytes / us / 1e6, 2)
-                row["lds_ring_TBps"] = round(wbytes / cur / 1e6, 2)
-                row["speedup"] = round(cur / us, 3)
-            else:
-                S0, nf0 = gemm.splitk_config(M, N, K) or (4, 4)
-                P0 = torch.empty((S0, M, N), dtype=torch.float32, device=dev)
-                cur = timeit(lambda: gemm.splitk_partials(x, wts[nxt()], N, S0, nf0, out=P0), iters=copies * 2)
-                row["lds_ring"] = [S0, nf0]
-                row["lds_ring_us"] = round(cur, 1)
-                row["lds_ring_TBps"] = round(wbytes / cur / 1e6, 2)
-                best = None
-                for S in (1, 2, 4, 8):
-                    for nf in (4, 8, 12):
-                        if K % (64 * S) or N % (16 * nf):
-                            continue
-                        us = timeit(lambda: gemm.splitk_vw(x, wts[nxt()], N, S, nf), iters=copies * 2)
-                        # the consumer reads S slabs: charge their extra bytes at 5 TB/s
-                        cost = us + (S - S0) * M * N * 4 / 5e6
-                        row[f"vw_s{S}nf{nf}_us"] = round(us, 1)
-                        if best is None or cost < best[1]:
-                            best = ((S, nf), cost, us)
-                row["vw_best"] = list(best[0])
-                row["vw_best_us"] = round(best[2], 1)
-                row["vw_TBps"] = round(wbytes / best[2] / 1e6, 2)
-                row["speedup_incl_slabs"] = round(cur / best[1], 3)
-            out.append(row)
-        del wts
-        torch.cuda.empty_cache()
     return out
 
 
@@ -1276,7 +1208,7 @@ def main(argv=None) -> int:
         res += {"decode": bench_decode, "decode_mixed": bench_decode_mixed, "decode_lean": bench_decode_lean, "prefill": bench_prefill, "prefill_mixed": bench_prefill_mixed, "prefill_spec_split": bench_prefill_spec_split, "elementwise": bench_elementwise,
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query, "gemm_tail": bench_gemm_tail,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
-                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "vw": bench_vw, "moe": bench_moe,
+                "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
                 "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]),
                 "prefill_policy_small": lambda d: bench_prefill_policy(d, [512, 768, 1024, 1280, 1536]), "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),

@@ -54,6 +54,19 @@ __device__ __forceinline__ float rowgroup_max(float v) {
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
+// rowgroup_max without the canonicalising v_max_f32 x, x, x hipcc puts in front of fmaxf on each
+// permlane result (4 extra VALU per call): the operands are finite scores or -inf, never sNaN
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float rowgroup_max_raw(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax_raw(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 __device__ __forceinline__ float rowgroup_sum(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
@@ -205,6 +218,141 @@ __device__ __forceinline__ void attend_block(const uint4* __restrict__ kl, const
       o[0][dt] = mfma16(vf.v, pf[0][st].v, o[0][dt]);
       o[1][dt] = mfma16(vf.v, pf[1][st].v, o[1][dt]);
     }
+  }
+}
+
+// attend_block with the softmax's VALU work cut (prefill2 FOLD, the default big-tile path).  Per block
+// and wave the plain form issues ~170 VALU instructions beside its 64 MFMAs (32 v_exp, 32 FMAs of
+// scale-and-subtract, a 16-deep serial add chain per column tile for the row sums, 32 max) -- with
+// two waves per SIMD the issue slots, not the matrix pipe, bound the loop
+// (profiles/r4_prefill_attn_mfma_busy_pmc.md: 31 % MFMA-busy, 4.3 VALU per MFMA).  Here:
+//   * Q arrives prescaled by scale*log2(e) (the caller's qf), and each S^T accumulator chain STARTS
+//     at -m (the running max, log2 units), so the MFMAs leave s' = s*c - m ready for v_exp: no
+//     per-score FMA.  A block whose max rises by more than 8 (or the row's first live block, m still
+//     -inf: chains start at 0) takes the rare branch that moves m and subtracts the rise from its
+//     scores (T13's defer-max, the decision taken BEFORE any of this block's P is formed, and O and
+//     the row sums rescaled together);
+//   * the row sums come out of the matrix pipe: one extra MFMA per (column tile, k-step) with an
+//     all-ones A operand (16 identical rows of sum_k P[q][k]) accumulates l in f32x4 `la` -- of the
+//     bf16-rounded P that the P.V product uses, so numerator and denominator see the same p;
+//   * the 4 lanes of a row group hold the same l, so no cross-lane reduction at the end.
+// 68 MFMAs and ~100 VALU per block and wave instead of 64 and ~170.
+// QPRE = false keeps Q exact (no extra rounding of q*c): the chains start at 0 and each score takes
+// one FMA (s*c - m) before its v_exp, as in attend_block; the row-sum MFMAs and the lean max / grow
+// logic are the same.  QPRE = true is the prescaled-Q form above: ~32 fewer VALU per block, but
+// bf16(q*c) perturbs each score by ~2^-9 of |s*c|, which shows on very peaky rows (scores of std
+// ~17 log2 units: max error 0.08 vs the fp32 reference where the exact form holds 0.02) -- opt-in.
+template <int D, int MASK, bool SB = false, bool QPRE = false>
+__device__ __forceinline__ void attend_block_fold(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
+                                                  const Frag (&qf)[2][D / 32], f32x4 (&o)[2][D / 16],
+                                                  float (&m)[2], f32x4 (&la)[2], bool causal, int j, int ctx,
+                                                  const int (&qpos)[2], float scale_log2, int lane, int g,
+                                                  bool need_mask = false) {
+  constexpr int KC = D / 32;
+  constexpr int DT = D / 16;
+  Frag kfa[4 * KC], vfa[2 * DT];
+#pragma unroll
+  for (int f = 0; f < 4 * KC; ++f) kfa[f].u = kl[f * 64 + lane];
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+  // chains start at -m: the MFMAs deliver s*c - m (m = -inf, a row's first live block: start at 0,
+  // and any finite max is a "rise")
+  float m0[2], thr[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const bool fresh = m[ct] == -INFINITY;
+    m0[ct] = (fresh || !QPRE) ? 0.f : -m[ct];
+    thr[ct] = fresh ? -INFINITY : 8.f;
+  }
+  f32x4 sc[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    sc[0][t] = f32x4{m0[0], m0[0], m0[0], m0[0]};
+    sc[1][t] = f32x4{m0[1], m0[1], m0[1], m0[1]};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      sc[0][t] = mfma16(kfa[t * KC + c].v, qf[0][c].v, sc[0][t]);
+      sc[1][t] = mfma16(kfa[t * KC + c].v, qf[1][c].v, sc[1][t]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < 2 * DT; ++f) vfa[f].u = vl[f * 64 + lane];
+  if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+
+  if (MASK == 1 || (MASK == 2 && need_mask)) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = j * KV_BS + 16 * t + 4 * g + r;
+          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));
+          sc[ct][t][r] = ok ? sc[ct][t][r] : -INFINITY;
+        }
+  }
+  Frag pf[2][2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[ct][t][r]);
+    mt = rowgroup_max_raw(mt);              // QPRE: max of s*c - m; else max of s
+    if constexpr (!QPRE) mt = m[ct] == -INFINITY ? mt * scale_log2 : mt * scale_log2 - m[ct];
+    const bool grow = mt > thr[ct];
+    if (__any(grow)) {
+      const bool first = m[ct] == -INFINITY;
+      const float rise = grow ? mt : 0.f;
+      if (grow) {
+        const float alpha = first ? 1.f : fast_exp2(-rise);   // first: O and l are still 0
+        la[ct] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
+        m[ct] = first ? rise : m[ct] + rise;
+      }
+      if constexpr (QPRE) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[ct][t][r] -= rise;
+      }
+    }
+    if constexpr (QPRE) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[ct][t][r] = fast_exp2(sc[ct][t][r]);
+    } else {
+      const float mref = m[ct] == -INFINITY ? 0.f : m[ct];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[ct][t][r] = fast_exp2(fmaf(sc[ct][t][r], scale_log2, -mref));
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
+        pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
+      }
+  }
+  // ---- O^T += V^T . P^T, and l += 1 . P^T on the matrix pipe --------------------------------
+  Frag ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);   // bf16 1.0 x 8
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      o[0][dt] = mfma16(vfa[dt * 2 + st].v, pf[0][st].v, o[0][dt]);
+      o[1][dt] = mfma16(vfa[dt * 2 + st].v, pf[1][st].v, o[1][dt]);
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    la[0] = mfma16(ones.v, pf[0][st].v, la[0]);
+    la[1] = mfma16(ones.v, pf[1][st].v, la[1]);
   }
 }
 
@@ -834,7 +982,7 @@ struct PrefillLean {
   float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
 };
 
-template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false>
+template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false, int FOLD = 0>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -912,6 +1060,16 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     for (int c = 0; c < KC; ++c)
       qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
   }
+  if constexpr (FOLD == 2) {
+    // Q prescaled by scale * log2(e) once per tile (one bf16 rounding of q*c): the block loop's
+    // scores then need no per-score multiply (attend_block_fold)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int c = 0; c < KC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[ct][c].v[e] = (bf16)((float)qf[ct][c].v[e] * scale_log2);
+  }
   // Retire the Q loads (and the prologue) with a wait the compiler's waitcnt pass can SEE: it
   // then knows qf is resident and does not re-insert a vmcnt(0) at every loop iteration (an
   // inline-asm wait is opaque to it).  vmcnt(0), expcnt/lgkmcnt untouched.
@@ -919,10 +1077,12 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 
   f32x4 o[2][DT];
   float m[2], l[2];
+  f32x4 la[2];      // FOLD: row sums from the matrix pipe
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     m[ct] = -INFINITY;
     l[ct] = 0.f;
+    la[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -945,305 +1105,17 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE);
     const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    attend_block<D, 2, PREF, SB>(kl, vl, qf, o, m, l, causal, ja, ctx, qpos, scale_log2, lane, g,
-                             __builtin_amdgcn_readfirstlane((int)!full) != 0);
+    if constexpr (FOLD != 0)
+      attend_block_fold<D, 2, SB, FOLD == 2>(kl, vl, qf, o, m, la, causal, ja, ctx, qpos, scale_log2, lane, g,
+                                             __builtin_amdgcn_readfirstlane((int)!full) != 0);
+    else
+      attend_block<D, 2, PREF, SB>(kl, vl, qf, o, m, l, causal, ja, ctx, qpos, scale_log2, lane, g,
+                                   __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
-    float lt = l[ct];
-    lt = rowgroup_sum(lt);
-    if (slot >= 0) {                          // a chunk of a split walk: partial state for the merge
-      const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = o[ct][dt];
-      if (g == 0) {
-        lean.part_ml[2 * pr] = m[ct];
-        lean.part_ml[2 * pr + 1] = lt;
-      }
-      continue;
-    }
-    if (tok[ct] >= qlen) continue;
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      bf16x4 v4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
-    }
-    if (lse != nullptr && g == 0)
-      lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Ping-pong prefill (prefill3_kernel): the 8-wave tile of prefill2 with its two SIMD partners
-// half a block apart.
-// ------------------------------------------------------------------------------------------
-// In prefill2 every wave runs {QK^T MFMAs, softmax VALU, P.V MFMAs} per block between the same
-// two barriers, so the two waves sharing a SIMD (w and w + 4) reach their softmax together and
-// the matrix pipe idles through it (about half of every block: ~1.0 PF/s).  Here a block is two
-// barrier-separated halves and the waves 4-7 (group B) run one half behind waves 0-3 (group A):
-//   half 1 of block i: A = QKS(i) (K frags, 32 MFMAs, softmax) | B = PV(i-1) (32 MFMAs)
-//   half 2 of block i: A = PV(i)                               | B = QKS(i)
-// so on every SIMD one wave's softmax runs beside its partner's P.V MFMAs.  Both groups execute
-// the same barrier sequence (2 per block + 1), so the LDS protocol is written in barrier indices:
-// block i is published by barrier 2i (each wave's counted vmcnt for its own pieces before it).
-// The last reader of block i's buffer is B's PV(i) (between barriers 2i+2 and 2i+3; an
-// lgkmcnt(0) precedes every barrier), and block i+3 refills it after barrier 2i+3.  VPRE: V(i)
-// is read into registers inside QKS(i) instead (its LDS latency under the softmax; costs 64
-// VGPRs across the softmax -- spills at D = 128).
-// LSUM: the softmax row sums come from 4 extra MFMAs against an all-ones A fragment (the P.V
-// product with a V column of ones) instead of 32 VALU adds per lane and block.
-template <int D, bool LSUM, bool VPRE>
-__device__ __forceinline__ void pp_qks(const uint4* __restrict__ kl, const uint4* __restrict__ vl,
-                                       const Frag (&qf)[2][D / 32], Frag (&vf)[D / 8], f32x4 (&o)[2][D / 16],
-                                       float (&m)[2], float (&l)[2], f32x4 (&lacc)[2], Frag (&pf)[2][2], bool causal,
-                                       int j, int ctx, const int (&qpos)[2], float scale_log2, int lane, int g,
-                                       bool need_mask) {
-  constexpr int KC = D / 32, DT = D / 16;
-  f32x4 sc[2][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    Frag kf[KC];          // one 16-key row group at a time: 16 VGPRs, not 64
-#pragma unroll
-    for (int c = 0; c < KC; ++c) kf[c].u = kl[(t * KC + c) * 64 + lane];
-    sc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    sc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-      sc[0][t] = mfma16(kf[c].v, qf[0][c].v, sc[0][t]);
-      sc[1][t] = mfma16(kf[c].v, qf[1][c].v, sc[1][t]);
-    }
-  }
-  // V fragments for PV: in flight during the softmax (read after the K fragments are consumed, so
-  // the two sets are never live together -- the scheduling barrier keeps hipcc from hoisting them)
-  if constexpr (VPRE) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int f = 0; f < 2 * DT; ++f) vf[f].u = vl[f * 64 + lane];
-  }
-  if (need_mask) {
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = j * KV_BS + 16 * t + 4 * g + r;
-          const bool ok = (key < ctx) & ((!causal) | (key <= qpos[ct]));
-          sc[ct][t][r] = ok ? sc[ct][t][r] : -INFINITY;
-        }
-  }
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    float mt = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mt = fmaxf(mt, sc[ct][t][r]);
-    mt = rowgroup_max(mt) * scale_log2;
-    const bool grow = mt > m[ct] + 8.f;      // deferred rescale, as attend_block
-    if (__any(grow)) {
-      const float mn = grow ? mt : m[ct];
-      const float alpha = grow ? fast_exp2(m[ct] - mn) : 1.f;
-      if constexpr (LSUM) lacc[ct] *= alpha;
-      else l[ct] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[ct][dt] *= alpha;
-      m[ct] = mn;
-    }
-    const float mref = (m[ct] == -INFINITY) ? 0.f : m[ct];
-    float ls = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = fast_exp2(fmaf(sc[ct][t][r], scale_log2, -mref));
-        sc[ct][t][r] = p;
-        if constexpr (!LSUM) ls += p;
-      }
-    if constexpr (!LSUM) l[ct] += ls;
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pf[ct][st].v[r] = (bf16)sc[ct][2 * st][r];
-        pf[ct][st].v[4 + r] = (bf16)sc[ct][2 * st + 1][r];
-      }
-  }
-}
-
-template <int D, bool LSUM, bool VPRE>
-__device__ __forceinline__ void pp_pv(const uint4* __restrict__ vl, Frag (&vf)[D / 8], f32x4 (&o)[2][D / 16],
-                                      f32x4 (&lacc)[2], const Frag (&pf)[2][2], int lane) {
-  constexpr int DT = D / 16;
-  if constexpr (!VPRE) {
-#pragma unroll
-    for (int f = 0; f < 2 * DT; ++f) vf[f].u = vl[f * 64 + lane];
-  }
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      o[0][dt] = mfma16(vf[dt * 2 + st].v, pf[0][st].v, o[0][dt]);
-      o[1][dt] = mfma16(vf[dt * 2 + st].v, pf[1][st].v, o[1][dt]);
-    }
-  if constexpr (LSUM) {
-    Frag ones;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ones.v[i] = (bf16)1.f;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      lacc[0] = mfma16(ones.v, pf[0][st].v, lacc[0]);
-      lacc[1] = mfma16(ones.v, pf[1][st].v, lacc[1]);
-    }
-  }
-}
-
-// 16 B per lane global -> LDS (M0 = this wave's LDS destination), opaque to the waitcnt pass
-__device__ __forceinline__ void glds16_untracked(const char* gptr, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gptr), "s"(lds_addr)
-               : "memory");
-}
-
-__device__ __forceinline__ void lgkm0_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-
-template <int D, bool HEAD_FAST, bool LSUM, bool PRIO, bool VPRE = false>
-__global__ void __launch_bounds__(512, 1) prefill3_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
-    float* __restrict__ lse, const int* __restrict__ work, PrefillLean lean) {
-  constexpr int NW = 8, NBUF = 3;
-  constexpr int KC = D / 32, DT = D / 16;
-  constexpr int TILE = KV_BS * D * 2;
-  constexpr int PIECES = TILE / 1024 / NW;
-  constexpr int LOADS = 2 * PIECES;
-  static_assert(PIECES >= 1 && TILE % (1024 * NW) == 0, "tile must split evenly over the waves");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
-
-  const int item = HEAD_FAST ? blockIdx.y : blockIdx.x;
-  const int* li = lean.items ? lean.items + 6 * item : nullptr;
-  const int s = li ? li[0] : (work ? work[2 * item] : blockIdx.z);
-  const int h = HEAD_FAST ? blockIdx.x : blockIdx.y;
-  const int tile = li ? li[1] : (work ? work[2 * item + 1] : (HEAD_FAST ? gridDim.y : gridDim.x) - 1 - item);
-  const int G = Hq / Hkv;
-  const int TQ = NW * 32 / G;
-  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
-  const int tok0 = tile * TQ;
-  if (tok0 >= qlen) return;
-  const int ctx = ctx_lens[s];
-  const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool grpB = w >= 4;                   // SIMD partners: waves w and w + 4
-  if (PRIO && grpB) __builtin_amdgcn_s_setprio(1);   // the younger half wins VALU arbitration
-
-  const int last_tok = min(tok0 + TQ, qlen) - 1;
-  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
-  const int nblk_tile = (kv_end + KV_BS - 1) / KV_BS;
-  // this workgroup's KV blocks [jb, jb + nblk) of the tile (lean: one chunk of its walk)
-  const int jb = li ? li[2] : 0;
-  const int nblk = li ? min(li[3], nblk_tile) - jb : nblk_tile;
-  const int slot = li ? li[4] : -1;
-  PENNY_DASSERT(nblk >= 1);
-  const int* bt = block_tables + (long)s * max_blocks + jb;
-
-  // The LDS-DMA is issued from inline asm, invisible to hipcc's waitcnt pass: with the builtin it
-  // could not prove the P.V fragment reads do not alias the block just staged and drained vmcnt(0)
-  // before them every block (the staged prefetch then never overlapped the math).  The counted
-  // vmcnt + barrier protocol below is the only wait on these loads.
-  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  auto stage = [&](int j) {                   // j: local block index (buffer j % NBUF)
-    const long phys = bt[j];
-    PENNY_DASSERT(phys >= 0);
-    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
-    const unsigned kl = lds0 + (j % NBUF) * 2 * TILE;
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const int piece = w * PIECES + i;
-      glds16_untracked(kb + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(kl + piece * 1024));
-      glds16_untracked(vb + piece * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(kl + TILE + piece * 1024));
-    }
-  };
-  stage(0);
-  if (nblk > 1) stage(1);
-
-  int tok[2], head[2], qpos[2];
-  Frag qf[2][KC];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const int r = w * 32 + ct * 16 + col;
-    tok[ct] = tok0 + r / G;
-    head[ct] = h * G + r % G;
-    const bool valid = tok[ct] < qlen;
-    qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
-    const bf16* qrow = q + ((long)(q0 + (valid ? tok[ct] : 0)) * Hq + head[ct]) * D;
-#pragma unroll
-    for (int c = 0; c < KC; ++c)
-      qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): Q and the prologue blocks (visible wait)
-
-  f32x4 o[2][DT], lacc[2];
-  float m[2], l[2];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    m[ct] = -INFINITY;
-    l[ct] = 0.f;
-    lacc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[ct][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  Frag vf[2 * DT], pf[2][2];
-
-  const int wave_tok0 = tok0 + (w * 32) / G;
-  const bool wave_live = wave_tok0 < qlen;
-  const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
-  const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
-  auto act = [&](int j) { return wave_live && (jb + j) * KV_BS < wave_kv_end; };
-  auto qks = [&](int j) {                     // local block j = absolute block jb + j
-    const int ja = jb + j;
-    const uint4* kl = reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE);
-    const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    pp_qks<D, LSUM, VPRE>(kl, kl + TILE / 16, qf, vf, o, m, l, lacc, pf, causal, ja, ctx, qpos, scale_log2, lane, g,
-                          __builtin_amdgcn_readfirstlane((int)!full) != 0);
-  };
-
-  // One op per barrier, the same op sequence QKS(0), PV(0), QKS(1), ... on every wave; group B
-  // passes barrier 0 before its first op (one half behind) and group A one extra barrier at the
-  // end, so both execute barriers 0 .. 2*nblk.  b = the barrier this wave passes before op k.
-  const int boff = grpB ? 1 : 0;
-  if (grpB) lgkm0_bar();                     // barrier 0 (the prologue already waited vmcnt(0))
-  for (int k = 0; k < 2 * nblk; ++k) {
-    const int b = k + boff;
-    if ((b & 1) == 0) {                      // barrier b publishes block b/2
-      if ((b >> 1) + 1 < nblk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lgkm0_bar();
-    if ((b & 1) && (b >> 1) + 2 < nblk) stage((b >> 1) + 2);   // the buffer block b/2 - 1 used
-    const int j = k >> 1;
-    if (act(j)) {
-      if ((k & 1) == 0) qks(j);
-      else pp_pv<D, LSUM, VPRE>(reinterpret_cast<const uint4*>(smem + (j % NBUF) * 2 * TILE + TILE), vf, o, lacc, pf,
-                                lane);
-    }
-  }
-  if (!grpB) lgkm0_bar();                    // barrier 2*nblk
-
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    float lt;
-    if constexpr (LSUM) lt = lacc[ct][0];     // every output row of the ones-MFMA holds the full sum
-    else lt = rowgroup_sum(l[ct]);
+    const float lt = FOLD != 0 ? la[ct][0] : rowgroup_sum(l[ct]);
     if (slot >= 0) {                          // a chunk of a split walk: partial state for the merge
       const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
 #pragma unroll
@@ -1322,8 +1194,7 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
 static int prefill_variant();
 
 // Lean big-tile prefill: items [nitems, 6] (see PrefillLean; LPT order), merge [nmerge, 6];
-// part_o / part_ml sized for the slots the items use.  Runs the kernel of the selected big-tile
-// variant: prefill2 (0, 4) or the ping-pong prefill3 (1-3; D = 64 always prefill3).
+// part_o / part_ml sized for the slots the items use.  Runs prefill2 in the selected variant.
 PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const int* ctx_lens, const int* block_tables,
                                            const void* k_cache, const void* v_cache, void* out, int Hq, int Hkv,
                                            int D, int max_blocks, float scale, int causal, float* lse,
@@ -1335,48 +1206,43 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   const float sl2 = scale * LOG2E;
   const PrefillLean lean{items, part_o, part_ml};
   const int var = prefill_variant();
-  if (D == 128 && (var == 0 || var == 4)) {
-    if (var == 4)
-      hipLaunchKernelGGL((prefill2_kernel<128, 8, 3, true, true, true>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
-                         (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
-                         (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
-    else
-      hipLaunchKernelGGL((prefill2_kernel<128, 8, 3, true>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
-                         (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
-                         (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
-    if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv, 32), dim3(256), 0, stream, merge, cu_q, part_o,
-                         part_ml, (bf16*)out, lse, Hq, Hkv);
-  } else if (D == 128) {
-    hipLaunchKernelGGL((prefill3_kernel<128, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
-    if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<128>, dim3(nmerge, Hkv, 32), dim3(256), 0, stream, merge, cu_q, part_o,
-                         part_ml, (bf16*)out, lse, Hq, Hkv);
+  const dim3 grid(Hkv, nitems, 1);
+#define LEAN_LAUNCH(DD, PREF_, SB_, FOLD_)                                                                        \
+  hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, PREF_, SB_, FOLD_>), grid, dim3(512), 0, stream,             \
+                     (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
+                     (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
+#define LEAN_VARIANTS(DD)                                   \
+  if (var == 5) LEAN_LAUNCH(DD, true, true, 1);             \
+  else if (var == 6) LEAN_LAUNCH(DD, true, true, 2);        \
+  else if (var == 4) LEAN_LAUNCH(DD, true, true, 0);        \
+  else LEAN_LAUNCH(DD, true, false, 0);                     \
+  if (nmerge > 0)                                           \
+    hipLaunchKernelGGL(prefill_merge_kernel<DD>, dim3(nmerge, Hkv, 256 / (4 * (64 / (DD / 4)))), dim3(256), 0, stream, \
+                       merge, cu_q, part_o, part_ml, (bf16*)out, lse, Hq, Hkv);
+  if (D == 128) {
+    LEAN_VARIANTS(128)
   } else if (D == 64) {
-    hipLaunchKernelGGL((prefill3_kernel<64, true, true, false>), dim3(Hkv, nitems, 1), dim3(512), 0, stream,
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);
-    if (nmerge > 0)
-      hipLaunchKernelGGL(prefill_merge_kernel<64>, dim3(nmerge, Hkv, 16), dim3(256), 0, stream, merge, cu_q, part_o,
-                         part_ml, (bf16*)out, lse, Hq, Hkv);
+    LEAN_VARIANTS(64)
   } else {
     return (int)hipErrorInvalidValue;
   }
+#undef LEAN_VARIANTS
+#undef LEAN_LAUNCH
   PENNY_RETURN_LAUNCH();
 }
 
-// Big-tile prefill variant: 4 (default) prefill2 with its K/V fragment prefetch pinned ahead of the
-// MFMAs (+4-6 % over 0 on the workload's steps, profiles/r4_prefill_attn_pinned_prefetch_variant4.jsonl),
-// 0 prefill2, 1 ping-pong prefill3 with ones-MFMA row sums, 2 ping-pong with VALU row sums,
-// 3 = 1 + static priority for waves 4-7 (PENNY_PREFILL_PP, or penny_attention_prefill_variant for
-// in-process A/B runs)
+// Big-tile prefill variant (PENNY_PREFILL_PP, or penny_attention_prefill_variant for in-process A/B
+// runs): 5 (default) prefill2 with the VALU-lean softmax (ones-MFMA row sums, lean max / grow
+// logic, exact Q; attend_block_fold), 6 = 5 with Q prescaled by scale*log2(e) (no per-score FMA; one
+// extra bf16 rounding of q*c, opt-in), 4 prefill2 with its K/V fragment prefetch pinned ahead of the
+// MFMAs (the r4 default, kept as the fallback with its tests), 0 prefill2.  The ping-pong prefill3
+// (r4 variants 1-3: 15-20 % slower on every mixed step, profiles/r4_prefill_attn_pingpong_lean_rejected.jsonl)
+// was removed in r5.
 static int g_prefill_variant = -1;
 static int prefill_variant() {
   if (g_prefill_variant < 0) {
     const char* v = getenv("PENNY_PREFILL_PP");
-    g_prefill_variant = v ? atoi(v) : 4;
+    g_prefill_variant = v ? atoi(v) : 5;
   }
   return g_prefill_variant;
 }
@@ -1415,18 +1281,14 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
                         : (head_fast ? dim3(Hkv, ntiles, num_seqs) : grid);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && head_fast && pp_env == 1)                                                                                      \
-    hipLaunchKernelGGL((prefill3_kernel<DD, true, true, false>), grid2, dim3(512), 0, stream,                    \
+  if (big && head_fast && pp_env == 5)                                                                           \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 1>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
-  else if (big && head_fast && pp_env == 2)                                                                                 \
-    hipLaunchKernelGGL((prefill3_kernel<DD, true, false, false>), grid2, dim3(512), 0, stream,                   \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
+  else if (big && head_fast && pp_env == 6)                                                                      \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
-  else if (big && head_fast && pp_env == 3)                                                                                 \
-    hipLaunchKernelGGL((prefill3_kernel<DD, true, true, true>), grid2, dim3(512), 0, stream,                     \
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp, PrefillLean{});                      \
+                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big && head_fast && pp_env == 4)                                                                      \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true>), grid2, dim3(512), 0, stream,               \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \

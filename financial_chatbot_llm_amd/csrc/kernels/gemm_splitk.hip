@@ -319,200 +319,6 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Weight-in-VGPR variant (vw) for the decode batch sizes the workload runs (M <= 128).
-//
-// The LDS ring above holds W AND X stages, so a CU has only ~50 KB of W in flight: at B = 128 the
-// gate|up / down / QKV / O streams measured 2.4-4.4 TB/s -- per-CU Little's-law bound, not HBM.
-// Here each wave owns its own FW row groups of W (waves split W rows 4 ways, WB = 1), so W needs
-// no sharing and streams HBM -> VGPR directly (tile_weight's 1-KiB pieces: one coalesced 16-B-per-
-// lane load per fragment), P stages ahead in a register ring; only X (L2-resident, read by every
-// wave) goes through an LDS ring filled by glds.  A CU then keeps P * 16 * FW KiB of W in flight
-// (P = 7, FW = 2: 224 KiB) -- the 512 KiB VGPR file is the staging buffer, not the 160 KiB LDS.
-//   * per stage and wave: MT/2 X pieces (glds) then 2*FW W loads, in that order; one counted
-//     `s_waitcnt vmcnt` + s_barrier per stage covers both (W register uses also get hipcc's own
-//     wait, already satisfied); the next stage's loads are issued after the barrier, into the slot
-//     every wave finished reading one stage ago;
-//   * the K loop is unrolled by the ring depth so every W register slot is a compile-time index;
-//   * epilogues as splitk_gemm_kernel: f32 slabs (split-K S) or the fused SiLU(gate) * up.
-// ---------------------------------------------------------------------------------------------
-// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= N only (expcnt / lgkmcnt at their max)
-template <int N>
-__device__ constexpr int vmcnt_imm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  return (N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8);
-}
-
-// 16-B global load into VGPRs that hipcc's waitcnt pass does not see (inline asm): the caller's
-// counted s_waitcnt vmcnt covers it.  With the compiler-visible load, the pass saw it pending next
-// to the LDS-DMA of X (a different event type, so "out of order") and drained vmcnt(0) before
-// every MFMA that reads it.
-__device__ __forceinline__ void load16_untracked(uint4& dst, const char* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
-}
-
-// MFMAs of one vw stage: X fragments from the LDS slot, W fragments from the register slot.
-// `base` is a __restrict__ PARAMETER for the same reason as in stage_mma (alias scopes for the
-// ds_reads, so hipcc's waitcnt pass does not drain the younger stages' LDS-DMA before them).
-template <int FW, int MT>
-__device__ __forceinline__ void vw_stage_mma(const char* __restrict__ base, const Frag (&wr)[FW][2],
-                                             f32x4 (&acc)[FW][MT], int g, int col) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    Frag xf[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int r = t * 16 + col;
-      xf[t].u = *reinterpret_cast<const uint4*>(base + r * 128 + xswz(r, 4 * kk + g) * 16);
-    }
-#pragma unroll
-    for (int f = 0; f < FW; ++f)
-#pragma unroll
-      for (int t = 0; t < MT; ++t)
-        acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[f][kk].v, xf[t].v, acc[f][t], 0, 0, 0);
-  }
-}
-
-template <int FW, int MT, int P, bool SILU>
-__global__ void __launch_bounds__(256, 1) splitk_vw_kernel(const bf16* __restrict__ X, int ldx,
-                                                           const bf16* __restrict__ Wt, int K,
-                                                           float* __restrict__ Pout, int M, int N, int S,
-                                                           bf16* __restrict__ Y, int ldy) {
-  constexpr int NF = 4 * FW;                // W row groups per workgroup
-  constexpr int NB = P + 1;                 // ring slots (X in LDS, W in registers)
-  constexpr int XBYTES = MT * 2 * 1024;     // X image of one BK = 64 stage (16*MT rows x 128 B)
-  constexpr int XL = MT / 2;                // X glds pieces per wave per stage
-  constexpr int WL = 2 * FW;                // W fragment loads per wave per stage
-  constexpr int LPS = XL + WL;              // vector-memory instructions per wave per stage
-  static_assert(MT % 2 == 0 && (P - 1) * LPS < 64, "vmcnt range");
-  static_assert(!SILU || FW % 2 == 0, "SiLU epilogue needs (gate, up) row-group pairs per wave");
-  __shared__ __attribute__((aligned(1024))) char smem[NB * XBYTES];
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
-  const int s = blockIdx.x % S, tile = blockIdx.x / S;
-  PENNY_DASSERT(M <= 16 * MT && (tile + 1) * 16 * NF <= N && K % (64 * S) == 0);
-  const int n0 = tile * 16 * NF;
-  const int kc = K / S, k0 = s * kc;
-  const int nst = kc / 64;
-  const long ksteps = K / 32;
-
-  const char* xsrc[XL];
-#pragma unroll
-  for (int i = 0; i < XL; ++i) {
-    const int xp = w * XL + i;
-    const int r = xp * 8 + (lane >> 3);
-    const int c = xswz(r, lane & 7);
-    xsrc[i] = reinterpret_cast<const char*>(X + (long)min(r, M - 1) * ldx + k0 + 8 * c);
-  }
-  // W fragment (f, kk) of stage j: piece (row group, k-step 2j + kk) of the tiled copy
-  const char* wsrc[FW];
-#pragma unroll
-  for (int f = 0; f < FW; ++f)
-    wsrc[f] = reinterpret_cast<const char*>(Wt) + (((long)(n0 / 16 + w * FW + f) * ksteps + k0 / 32) * 64 + lane) * 16;
-
-  Frag wr[NB][FW][2];
-  f32x4 acc[FW][MT];
-#pragma unroll
-  for (int f = 0; f < FW; ++f)
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int j, auto slotc) {
-    constexpr int slot = decltype(slotc)::value;
-    char* base = smem + slot * XBYTES;
-#pragma unroll
-    for (int i = 0; i < XL; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(xsrc[i] + j * 128), (lds_void_t*)(base + (w * XL + i) * 1024),
-                                       16, 0, 0);
-#pragma unroll
-    for (int f = 0; f < FW; ++f)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        load16_untracked(wr[slot][f][kk].u, wsrc[f] + ((long)(2 * j + kk) << 10));
-  };
-  auto compute = [&](auto slotc) {
-    constexpr int slot = decltype(slotc)::value;
-    vw_stage_mma<FW, MT>(smem + slot * XBYTES, wr[slot], acc, g, col);
-  };
-
-  // prologue: stages 0 .. P-1 into slots 0 .. P-1
-  // Every stage issues exactly LPS loads, past the end too (clamped to the last stage: L2 hits into
-  // a slot nobody reads again), so the in-flight count is the same on every path -- a conditional
-  // issue made hipcc's waitcnt pass assume the worst path and drain vmcnt(0) before the MFMAs.
-  static_for<P>([&](auto uc) {
-    constexpr int U = decltype(uc)::value;
-    issue(min(U, nst - 1), uc);
-  });
-  __builtin_amdgcn_sched_barrier(0);
-
-  // Every ring slot turn waits, issues and (while j < nst) computes: the past-the-end turns of the
-  // last ring rotation still wait and issue (clamped L2 hits), so every path carries the same loads
-  // after each W slot -- a guarded issue is a path with fewer, on which hipcc's waitcnt pass drains
-  // vmcnt(0) before the MFMAs.
-  for (int j0 = 0; j0 < nst; j0 += NB) {
-    static_for<NB>([&](auto uc) {
-      constexpr int U = decltype(uc)::value;
-      const int j = j0 + U;
-      // stage j landed for every wave; P-1 younger in flight.  The compiler-visible s_waitcnt (not
-      // asm) lets the waitcnt pass count from it: with up to P * LPS loads pending in its model it
-      // otherwise overflows the 6-bit counter and drains vmcnt(0) before the MFMAs.
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm<(P - 1) * LPS>());
-      __builtin_amdgcn_s_barrier();
-      issue(min(j + P, nst - 1), std::integral_constant<int, (U + P) % NB>{});
-      __builtin_amdgcn_sched_barrier(0);
-      if (j < nst) compute(uc);
-    });
-  }
-  // Drain every load before the epilogue: no LDS-DMA may land after the workgroup ends, and the
-  // untracked W loads of the past-the-end turns must land before hipcc reuses their registers (it
-  // thinks they were written at issue).  sched_barriers keep the epilogue's code below the wait.
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // ... and keep every W slot register live up to here, so hipcc cannot hand one whose (never
-  // consumed) past-the-end load is still in flight to the epilogue before the wait
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int f = 0; f < FW; ++f)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const uint4 u = wr[b][f][kk].u;
-        asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
-      }
-  __builtin_amdgcn_sched_barrier(0);
-
-  if constexpr (SILU) {
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int m = t * 16 + col;
-      if (m >= M) continue;
-#pragma unroll
-      for (int f = 0; f < FW; f += 2) {
-        const int G = n0 / 16 + w * FW + f;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gt = (float)(bf16)acc[f][t][r], up = (float)(bf16)acc[f + 1][t][r];
-          o[r] = (bf16)((float)(bf16)(gt / (1.f + __expf(-gt))) * up);
-        }
-        *reinterpret_cast<bf16x4*>(Y + (long)m * ldy + (G >> 1) * 16 + 4 * g) = o;
-      }
-    }
-    return;
-  }
-  float* ps = Pout + (long)s * M * N;
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    const int m = t * 16 + col;
-    if (m >= M) continue;
-#pragma unroll
-    for (int f = 0; f < FW; ++f) {
-      const int n = n0 + (w * FW + f) * 16 + 4 * g;
-      *reinterpret_cast<f32x4*>(ps + (long)m * N + n) = acc[f][t];
-    }
-  }
-}
-
 // Y[m, n] = bf16(sum_s P[s, m, n]) (+ R[m, n], rounded like the unfused GEMM-then-add path)
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N,
                                                             bf16* __restrict__ Y, int ldy,
@@ -668,45 +474,6 @@ PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, v
   SK_CASE(16, 1, 1, 2)
 #undef SK_CASE
   return (int)hipErrorInvalidValue;
-}
-
-// Weight-in-VGPR decode projection (splitk_vw_kernel) for M <= 128 on the fragment-tiled W:
-// silu = 0: P [S, M, N] f32 slabs (ldy unused); silu = 1: Y [M, N/2] bf16 (row stride ldy), S = 1,
-// W the interleave16 gate|up.  nf = W row groups per workgroup (4, 8 or 12; silu: 8).  Contract
-// (checked): N % (16*nf) == 0, K % (64*S) == 0, ldx % 8 == 0, 1 <= M <= 128.
-PENNY_API int penny_splitk_vw_gemm(const void* X, int ldx, const void* Wt, int K, void* out, int ldy, int M, int N,
-                                   int S, int nf, int silu, hipStream_t stream) {
-  if (M <= 0) return 0;
-  if (M > 128 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 4 && nf != 8 && nf != 12) || N % (16 * nf) ||
-      (silu && (nf != 8 || S != 1 || ldy % 4)))
-    return (int)hipErrorInvalidValue;
-  const int mt = 2 * ((M + 31) / 32);        // token tiles, rounded up to even
-  const dim3 grid((N / (16 * nf)) * S), block(256);
-  const bf16* x = (const bf16*)X;
-  const bf16* w = (const bf16*)Wt;
-  // ring depth: 7 stages ahead; 5 at FW = 3 (its 8-slot W ring would not fit the arch VGPRs, and
-  // hipcc would copy in-flight W registers to AGPRs -- tests/test_vw_asm_hazards.py checks)
-#define VW_LAUNCH(FW_, MT_)                                                                                      \
-  {                                                                                                              \
-    constexpr int P_ = (FW_) == 3 ? 5 : 7;                                                                       \
-    if (silu)                                                                                                    \
-      hipLaunchKernelGGL((splitk_vw_kernel<2, MT_, 7, true>), grid, block, 0, stream, x, ldx, w, K, (float*)nullptr, \
-                         M, N, 1, (bf16*)out, ldy);                                                              \
-    else                                                                                                         \
-      hipLaunchKernelGGL((splitk_vw_kernel<FW_, MT_, P_, false>), grid, block, 0, stream, x, ldx, w, K,          \
-                         (float*)out, M, N, S, (bf16*)nullptr, 0);                                               \
-    return (int)hipGetLastError();                                                                               \
-  }
-#define VW_MT(FW_)                          \
-  if (mt <= 2) VW_LAUNCH(FW_, 2)            \
-  else if (mt <= 4) VW_LAUNCH(FW_, 4)       \
-  else if (mt <= 6) VW_LAUNCH(FW_, 6)       \
-  else VW_LAUNCH(FW_, 8)
-  if (nf == 4) VW_MT(1)
-  else if (nf == 8) VW_MT(2)
-  else VW_MT(3)
-#undef VW_MT
-#undef VW_LAUNCH
 }
 
 PENNY_API int penny_splitk_reduce(const void* P, int S, int M, int N, void* Y, int ldy, const void* R, int ldr,

@@ -598,6 +598,7 @@ class LLMEngine:
                                            / max(1, self.runner.stats["graph_steps"]), 3),
                 "gpu_eager_ms_mean": round(1e3 * self.runner.stats["gpu_eager_s"]
                                            / max(1, self.runner.stats["steps"] - self.runner.stats["graph_steps"]), 3),
+                "gpu_step_s": round(self.runner.stats["gpu_graph_s"] + self.runner.stats["gpu_eager_s"], 3),
                 "gpu_idle_between_steps_s": round(self.runner.stats["gpu_idle_s"], 3),
                 "gpu_idle_gaps": self.runner.stats["gpu_idle_gaps"], **self._memory_stats()}
 

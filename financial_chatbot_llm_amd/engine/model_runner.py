@@ -242,6 +242,7 @@ class ModelRunner:
         self._max_decode_ws = max(max_decode_batch, 1)
         self.decode_ws2 = None
         self.graphs: Dict[int, _DecodeGraph] = {}
+        self.graphs_filt: Dict[int, _DecodeGraph] = {}   # top-k / top-p twins of fused buckets (lazy)
         self._static = None
         self.graph_pool = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0,
@@ -251,7 +252,9 @@ class ModelRunner:
         # overlap the other half's compute (PENNY_TP_OVERLAP=0 disables)
         self.tp_overlap = os.environ.get("PENNY_TP_OVERLAP", "1") == "1"
         self.overlap_min_rows = int(os.environ.get("PENNY_TP_OVERLAP_MIN_ROWS", "1024"))
-        self._gpu_timing = self.on_gpu and os.environ.get("PENNY_STEP_GPU_TIMING", "0") == "1"
+        # device time of every step and the device idle between steps (two events per step: on by
+        # default so every bench run reports where the non-busy GPU time is; =0 turns it off)
+        self._gpu_timing = self.on_gpu and os.environ.get("PENNY_STEP_GPU_TIMING", "1") == "1"
         # sampled ids of the latest step stay on the device: the next step gathers its decode ids
         # from here when it was launched before this one's ids reached the host (overlap mode)
         # a speculative chunk samples draft + 1 rows (engine.speculative: drafts <= 16 tokens)
@@ -570,7 +573,7 @@ class ModelRunner:
                                                          self.device)
         return self._dual
 
-    def _run_static(self, B: int) -> torch.Tensor:
+    def _run_static(self, B: int, filtered: bool = False) -> torch.Tensor:
         s = self._static
         self._gather_pending(s["ids"], s["src"][:B], 0)
         if self.dual_decode and B >= self.dual_min_batch:
@@ -585,10 +588,12 @@ class ModelRunner:
                                      ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
                                      cascade=s["cascade"])
             h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
-        if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
-            return self.model.sample_vocab_parallel(h, s["temps"][:B], s["seeds"][:B])
-        if self._fused_sampling(h):
-            return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B], wt=self._lm_tiled())
+        if not filtered:
+            if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
+                return self.model.sample_vocab_parallel(h, s["temps"][:B], s["seeds"][:B])
+            if self._fused_sampling(h):
+                return ops.lm_head_sample(h, self.model.lm_weight(), s["temps"][:B], s["seeds"][:B],
+                                          wt=self._lm_tiled())
         logits = self.model.logits(h)
         # the top-k/top-p threshold kernel is always in the graph: unfiltered rows (k=0, p=1) exit
         # after reading their parameters
@@ -617,14 +622,41 @@ class ModelRunner:
         logger.info(f"captured decode hipGraphs for batch sizes {sorted(self.graphs)}")
 
     def _fused_graph_needs_eager(self, si: StepInputs) -> bool:
-        """A decode step with top-k / top-p rows whose bucket's graph samples inside the LM head runs
-        eagerly (logits -> filtered sampler) instead of replaying that graph."""
+        """A decode step with top-k / top-p rows whose bucket's graph samples inside the LM head: at
+        TP=1 it replays the bucket's FILTERED twin (logits -> threshold -> sampler), captured on the
+        first such step; under TP (vocab-parallel candidates) it runs eagerly."""
         if not self._has_filters(si):
             return False
         if not self.graphs:
             self.capture_graphs()
-        G = self.graphs.get(self._bucket(si.num_decode))
-        return G is not None and G.fused
+        B = self._bucket(si.num_decode)
+        G = self.graphs.get(B)
+        if G is None or not G.fused:
+            return False
+        if getattr(self.model, "tp_size", 1) > 1:
+            return True
+        if B not in self.graphs_filt:
+            self._capture_filtered(B)
+        return False
+
+    def _capture_filtered(self, B: int) -> None:
+        """Capture mid-serving: the static inputs still hold the step in flight, so the warm-up and
+        capture passes run with every KV slot masked (< 0: no cache write) and no pending-token
+        gather -- they must not rewrite live sequences' KV -- and the inputs are restored after."""
+        s = self._static
+        saved = (s["slots"][:B].clone(), s["src"][:B].clone())
+        s["slots"][:B].fill_(-1)
+        s["src"][:B].fill_(-1)
+        for _ in range(2):
+            self._run_static(B, filtered=True)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.graph_pool):
+            out = self._run_static(B, filtered=True)
+        self.graphs_filt[B] = _DecodeGraph(g, B, out, False)
+        s["slots"][:B].copy_(saved[0])
+        s["src"][:B].copy_(saved[1])
+        torch.cuda.synchronize()
 
     def _bucket(self, n: int) -> int:
         for b in self.graph_sizes:
@@ -638,6 +670,8 @@ class ModelRunner:
         n = si.num_decode
         B = self._bucket(n)
         G = self.graphs[B]
+        if G.fused and self._has_filters(si) and B in self.graphs_filt:
+            G = self.graphs_filt[B]
         S, W = self.max_decode_batch, self.max_blocks
         self._pinned_i32, self._pinned_f, self._pinned_l = self._pinned_sets[self._pin_flip]
         self._pin_flip ^= 1

@@ -32,7 +32,6 @@ _SIGS = {
     "penny_silu_mul": [P, P, c_int, c_int, c_int, P],
     "penny_skinny_gemm": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
-    "penny_splitk_vw_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "penny_splitk_reduce": [P, c_int, c_int, c_int, P, c_int, P, c_int, P],
     "penny_splitk_gemm_bf16": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_lm_head_stream_sample": [P, c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, c_int,

@@ -97,13 +97,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
     # or no copy was made) the row-major weight itself
     src = wt if wt is not None else (w if w.is_contiguous() else None)
     rowmajor = wt is None
-    vw = vw_config(M, N_, K, epilogue) if (not rowmajor and N.use_native(x) and x.stride(1) == 1
-                                           and x.stride(0) % 8 == 0 and residual is None) else None
-    if vw is not None and (epilogue == "silu" or slabs):
-        S, nf = vw
-        if epilogue == "silu":
-            return splitk_vw(x, wt, N_, 1, nf, silu=True)
-        return Slabs(splitk_vw(x, wt, N_, S, nf))
     if slabs and src is not None and epilogue is None and residual is None:
         cfg = splitk_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
         if cfg is not None:
@@ -290,6 +283,10 @@ def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
 # M >= 192 the 3-deep ring of the 256-token tile is MFMA/LDS-latency bound and the library wins.
 GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     (28672, 4096): [(1, 160, 8)],
+    # Llama-3-70B TP=8 gate|up shard (interleave16 of 2 x 3584 rows), fragment-tiled: 1.04-1.06x at
+    # M <= 16 (nf 4), 1.04-1.08x at M = 192-256 (nf 2, 224 workgroups); hipBLASLt + silu_mul ties or
+    # wins in between (profiles/r5_decode_v2.jsonl)
+    (7168, 8192): [(1, 16, 4), (176, 256, 2)],
 }
 
 
@@ -318,56 +315,6 @@ def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
     N.call("penny_gateup_silu_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), y.stride(0), M, N_, nf,
            int(rowmajor), N.stream())
     return y
-
-
-# Weight-in-VGPR decode kernel (gemm_splitk.hip splitk_vw_kernel, M <= 128, fragment-tiled W):
-# (N, K) -> (S, nf).  W streams HBM -> VGPR (a 7-stage register ring per wave), only X goes through
-# LDS, so a CU keeps 2-4x more W in flight than the LDS-ring kernel.  PENNY_SPLITK_VW=1 enables
-# (=force: any tiled shape the kernel takes, for tests); off until the A/B on the GPU settles it.
-VW: Dict[Tuple[int, int], Tuple[int, int]] = {
-    (6144, 4096): (4, 8),       # QKV: 48 tiles x S=4
-    (4096, 4096): (4, 4),       # O: 64 tiles x S=4
-    (4096, 14336): (4, 4),      # down: 64 tiles x S=4
-    (28672, 4096): (1, 8),      # gate|up + SiLU: 224 tiles
-}
-VW_MAX_M = 128
-
-
-def vw_config(M: int, N_: int, K: int, epilogue: Optional[str]) -> Optional[Tuple[int, int]]:
-    mode = os.environ.get("PENNY_SPLITK_VW", "0")
-    if mode == "0" or M > VW_MAX_M or epilogue not in (None, "silu"):
-        return None
-    if mode != "force" and epilogue is None and M <= SKINNY_MAX_M.get((N_, K), 0):
-        return None                  # the skinny kernel's range
-    cfg = VW.get((N_, K))
-    if cfg is None and mode == "force":
-        nf = 8 if N_ % 128 == 0 else (4 if N_ % 64 == 0 else None)
-        S = next((s for s in (4, 2, 1) if K % (64 * s) == 0), None)
-        cfg = (S, nf) if nf and S else None
-    if cfg is None or (epilogue == "silu" and cfg[1] != 8) or N_ % (16 * cfg[1]) or K % (64 * cfg[0]):
-        return None
-    return cfg
-
-
-def splitk_vw(x: torch.Tensor, wt: torch.Tensor, N_: int, S: int, nf: int, silu: bool = False) -> torch.Tensor:
-    """Decode projection on the weight-in-VGPR kernel: f32 slabs [S, M, N] of x @ w.T, or
-    (``silu``, S = 1, w = the interleave16 gate|up) silu(gate) * up as bf16 [M, N/2]."""
-    M, K = x.shape
-    if not N.use_native(x):
-        y = F.linear(x.float(), untile_weight(wt).float())
-        if silu:
-            return silu_mul(y.to(x.dtype), interleave16=True)
-        return torch.stack([x.float()[:, s * (K // S):(s + 1) * (K // S)] @
-                            untile_weight(wt).float()[:, s * (K // S):(s + 1) * (K // S)].t() for s in range(S)])
-    if silu:
-        out = torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
-        N.call("penny_splitk_vw_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(out), out.stride(0), M, N_, 1, nf,
-               1, N.stream())
-    else:
-        out = torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
-        N.call("penny_splitk_vw_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(out), 0, M, N_, S, nf, 0,
-               N.stream())
-    return out
 
 
 class ResidualSum:

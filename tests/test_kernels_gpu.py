@@ -130,7 +130,7 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 4, 5, 6])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
     # respond chunk behind a cached prefix + decide-like and spec-like chunks (dead waves: 17 x 4 rows)
     (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
@@ -139,8 +139,9 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     (12, 12, 64, False, [(200, 200), (33, 33)], 1.0),         # bidirectional, D = 64
 ])
 def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, qscale):
-    """The ping-pong kernel (prefill3, variants 1-3), prefill2 (0) and prefill2 with pinned fragment
-    prefetch (4) vs the fp32 reference, with the LPT work list and without (also the lse output)."""
+    """prefill2 (0), prefill2 with pinned fragment prefetch (4), its VALU-lean softmax (5: ones-MFMA
+    row sums, lean max / grow logic) and 5 with prescaled Q and -m accumulator starts (6) vs the fp32
+    reference, with the LPT work list and without (also the lse output)."""
     g = torch.Generator().manual_seed(40 + variant)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
@@ -154,18 +155,21 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
     ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, causal, lse=lse_ref)
     wl = ops.attention.prefill_work_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, causal)
     old = ops.attention.prefill_variant(variant)
+    # variant 6 rounds q*scale*log2(e) to bf16 once (opt-in): on the peaky rows (qscale 12, scores of
+    # std ~17 log2 units) that perturbation shows as up to ~0.08 in the output; typical rows hold 0.02
+    atol = 1e-1 if (variant == 6 and qscale > 1) else 2e-2
     try:
         for work in (None, torch.from_numpy(wl).to(DEV) if wl is not None else None):
             lse = torch.empty(q.shape[0], Hq, device=DEV)
             out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale,
                               causal, max_q_len=max(qlens), lse=lse, work=work)
-            close(out, ref, atol=2e-2)
-            close(lse, lse_ref, atol=2e-2, rtol=1e-3)
+            close(out, ref, atol=atol)
+            close(lse, lse_ref, atol=atol, rtol=1e-3)
     finally:
         ops.attention.prefill_variant(old)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4])
+@pytest.mark.parametrize("variant", [0, 4, 5, 6])
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
     (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
@@ -174,8 +178,8 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
 ])
 def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal, lens):
     """Lean prefill: the KV walks of long tiles cut into chunks on different workgroups, partial
-    (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse), on the prefill2
-    (0, 4) and ping-pong (1) kernels."""
+    (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse), on every prefill2
+    variant."""
     g = torch.Generator().manual_seed(50 + min_chunk)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
@@ -200,6 +204,40 @@ def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal,
         ops.attention.prefill_variant(old)
     close(out, ref, atol=2e-2)
     close(lse, lse_ref, atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("spike_block", [0, 3, 9])
+def test_prefill_attention_late_max_spike_forces_rescale(variant, spike_block):
+    """Rule 26: a rare rescale branch needs an input that FORCES it.  One query token's row is made to
+    match one key of block `spike_block` (score ~ 20 above every other in log2 units) so the running
+    max jumps past the defer threshold exactly there, after earlier blocks already summed into O and
+    l; the output must still equal the fp32 reference (every row, incl. the spiked one)."""
+    from financial_chatbot_llm_amd.ops.attention import gather_kv_ref
+    g = torch.Generator().manual_seed(70 + spike_block)
+    Hq, Hkv, D = 32, 8, 128
+    lens = [(96, 12 * 64), (40, 40)]
+    qlens = [a for a, _ in lens]
+    ctx = [b for _, b in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    q = rnd(int(cu[-1]), Hq, D, scale=0.3, gen=g)
+    # query token 90 of sequence 0 (position 762), head 5 (kv head 1) := 3.5 x key 64*spike_block + 7
+    kfull, _ = gather_kv_ref(kc, vc, tables[0], ctx[0])
+    key = 64 * spike_block + 7
+    q[90, 5] = (kfull[key, 1].float() * 3.5).to(torch.bfloat16)
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = ops.prefill(q, cu, ctx_t, tables, kc, vc, scale, True)
+    old = ops.attention.prefill_variant(variant)
+    try:
+        wl = ops.attention.prefill_work_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, True)
+        out = ops.prefill(q.to(DEV), cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, True,
+                          max_q_len=max(qlens), work=torch.from_numpy(wl).to(DEV) if wl is not None else None)
+    finally:
+        ops.attention.prefill_variant(old)
+    close(out, ref, atol=2e-2)
+    close(out[90, 5], ref[90, 5], atol=1e-2)
 
 
 @pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
@@ -351,43 +389,6 @@ def test_splitk_gemm(M, S, nf):
     xw[:, 32:32 + K] = x
     P2 = gemm.splitk_partials(xw.to(DEV)[:, 32:32 + K], wt, N_, S, nf)
     close(P2, ref_p, atol=1e-3)
-
-
-@pytest.mark.parametrize("M", [1, 17, 40, 64, 100, 128])
-@pytest.mark.parametrize("N_,K,S,nf", [(384, 2048, 1, 4), (768, 2048, 4, 8), (384, 1024, 2, 12), (6144, 4096, 4, 8),
-                                       (4096, 14336, 4, 4), (384, 832, 1, 4), (256, 192, 1, 8), (384, 576, 1, 12)])
-def test_splitk_vw_gemm(M, N_, K, S, nf):
-    """Weight-in-VGPR decode GEMM (untracked W register ring + X LDS ring): f32 slabs vs the fp32
-    reference at toy and production (QKV, down) shapes; stages per K slice 32, 8, 8, 16, 56 (whole
-    ring turns), 13 (a 5-stage past-the-end turn), 3 and 9 (fewer stages than the ring is deep)."""
-    from financial_chatbot_llm_amd.ops import gemm
-    if N_ % (16 * nf):
-        pytest.skip("shape")
-    g = torch.Generator().manual_seed(13)
-    x = rnd(M, K, gen=g)
-    w = rnd(N_, K, scale=0.05, gen=g)
-    P = gemm.splitk_vw(x.to(DEV), gemm.tile_weight(w.to(DEV)), N_, S, nf)
-    ref_p = (x.float().view(M, S, K // S).transpose(0, 1) @ w.float().view(N_, S, K // S).permute(1, 2, 0))
-    close(P, ref_p, atol=2e-3 * max(1.0, (K / S / 2048) ** 0.5))
-    # same MFMA order per slice as the LDS-ring kernel: identical slabs
-    if nf in (4, 8) and M > 1:
-        assert torch.equal(gemm.splitk_partials(x.to(DEV), gemm.tile_weight(w.to(DEV)), N_, S, nf), P)
-
-
-@pytest.mark.parametrize("M", [1, 33, 128])
-@pytest.mark.parametrize("Fr,K", [(512, 1024), (14336, 4096)])
-def test_splitk_vw_gateup_silu(M, Fr, K):
-    """vw kernel with the fused SiLU(gate) * up epilogue == the LDS-ring gate|up kernel (same
-    roundings, same MFMA order: bit-equal) and close to the fp32 reference."""
-    from financial_chatbot_llm_amd.ops import gemm
-    g = torch.Generator().manual_seed(6)
-    x = rnd(M, K, gen=g)
-    gate, up = rnd(Fr, K, scale=0.03, gen=g), rnd(Fr, K, scale=0.03, gen=g)
-    wt = gemm.tile_weight(gemm.interleave16(gate, up).to(DEV).contiguous())
-    y = gemm.splitk_vw(x.to(DEV), wt, 2 * Fr, 1, 8, silu=True)
-    assert torch.equal(y, gemm.gateup_silu(x.to(DEV), wt, 2 * Fr, 8))
-    gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
-    close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
 
 
 @pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])
