@@ -410,6 +410,18 @@ PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
     (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down
+    # Llama-3-70B (r5, profiles/r5_shard_shapes_v1_ring8.jsonl "shard_shapes_prefill" rows: each
+    # projection's kernels vs hipBLASLt at M = 384..4096, interleaved).  TP=1:
+    (10240, 8192): [(512, "lib"), (1 << 30, "fused")],                                   # QKV
+    (8192, 8192): [(384, "lib"), (512, "S4"), (1024, "S2"), (1 << 30, "lib")],           # O
+    (57344, 8192): [(768, "lib"), (1 << 30, "hip")],                                     # gate|up
+    (8192, 28672): [(512, "S4"), (768, "lib"), (1024, "S2"), (1536, "S4"), (1 << 30, "hip")],   # down
+    # TP=8 per-rank shards: the 256x256 tile underfills the CUs at these N up to ~1.5-2k rows (5 / 28
+    # / 32 column tiles), so the library keeps those; the tile kernel where it measured ahead
+    (1280, 8192): [(1536, "lib"), (3072, "S4"), (1 << 30, "S2")],                        # QKV shard
+    (8192, 1024): [(1536, "lib"), (2048, "hip"), (1 << 30, "lib")],                      # O shard
+    (7168, 8192): [(1024, "lib"), (3072, "hip"), (1 << 30, "lib")],                      # gate|up shard
+    (8192, 3584): [(1 << 30, "lib")],                                                    # down shard
 }
 
 
