@@ -81,6 +81,42 @@ def utilisation(trace_csv: str) -> str:
     return f"GPU busy {busy / 1e9:.2f} s of a {span / 1e9:.2f} s traced span ({100 * busy / span:.1f} %).\n"
 
 
+def gaps(trace_csv: str, top: int = 12) -> str:
+    """Where the idle time of the traced span sits: every gap of the kernel-interval union, binned by
+    length, and attributed to the (kernel class before -> kernel class after) transition.  Short gaps
+    (< 5 us) are kernel boundaries; long ones are the host not having launched the next kernel yet
+    (launch-bound stretches, step turnarounds)."""
+    iv = []
+    with open(trace_csv) as fh:
+        for r in csv.DictReader(fh):
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
+    iv.sort()
+    bins = [(2e3, "< 2 us"), (5e3, "2-5 us"), (20e3, "5-20 us"), (100e3, "20-100 us"), (1e6, "0.1-1 ms"),
+            (float("inf"), "> 1 ms")]
+    by_bin = defaultdict(lambda: [0, 0.0])
+    by_pair = defaultdict(lambda: [0, 0.0])
+    ce, cname = iv[0][1], iv[0][2]
+    for s_, e_, n in iv[1:]:
+        if s_ > ce:
+            g = s_ - ce
+            lab = next(lbl for lim, lbl in bins if g < lim)
+            by_bin[lab][0] += 1
+            by_bin[lab][1] += g
+            k = (classify(cname), classify(n))
+            by_pair[k][0] += 1
+            by_pair[k][1] += g
+        if e_ >= ce:
+            ce, cname = e_, n
+    out = ["| idle gap | count | total s |", "|---|---:|---:|"]
+    for _, lbl in bins:
+        c, t = by_bin.get(lbl, (0, 0.0))
+        out.append(f"| {lbl} | {c} | {t / 1e9:.3f} |")
+    out += ["", "| previous kernel -> next kernel | gaps | total s | mean us |", "|---|---:|---:|---:|"]
+    for (a, b), (c, t) in sorted(by_pair.items(), key=lambda kv: -kv[1][1])[:top]:
+        out.append(f"| {a} -> {b} | {c} | {t / 1e9:.3f} | {t / max(c, 1) / 1e3:.1f} |")
+    return "\n".join(out) + "\n"
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
@@ -91,7 +127,7 @@ def main(argv=None) -> int:
     text = summarise(a.csv, a.title, a.top)
     if a.trace:
         head, rest = text.split("\n\n", 1)
-        text = head + "\n\n" + utilisation(a.trace) + "\n" + rest
+        text = head + "\n\n" + utilisation(a.trace) + "\n" + gaps(a.trace) + "\n" + rest
     print(text, end="")
     return 0
 

@@ -116,6 +116,10 @@ def _worker(rank, world, port, q):
         torch.cuda.synchronize()
         results.append((float(y.float().mean().item()), float(world * (world + 1) / 2), 0.0))
         results.append((float(ar.counter.item()), 25.0, 0.0))   # 10 + 6 + 3 + 1 eager calls + 5 replays
+        # the engine's init-time first-contact check (one-shot, two-shot, all-gather vs the exact sum,
+        # consensus over the group) passes on a healthy group
+        ok, why = ar.self_test()
+        results.append((float(ok), 1.0, 0.0))
         ar.check()
         dist.barrier()
         ar.close()
@@ -153,11 +157,12 @@ def _run(target, world):
 def test_custom_all_reduce_processes(world):
     res = _run(_worker, world)
     for r, (status, payload) in res.items():
-        *sizes, graph, rounds = payload
+        *sizes, graph, rounds, selftest = payload
         for err, err_inplace, mag in sizes:
             assert err <= 0.02 * mag + 1e-2 and err_inplace <= 0.02 * mag + 1e-2, (err, err_inplace, mag)
         assert graph[0] == graph[1]
         assert rounds[0] == rounds[1]
+        assert selftest[0] == 1.0
 
 
 @pytest.mark.timeout(120)
