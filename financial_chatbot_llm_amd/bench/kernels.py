@@ -12,10 +12,8 @@ import argparse
 import json
 import math
 import statistics
-import time
 from typing import Callable, Dict, List
 
-import numpy as np
 import torch
 
 from .. import ops
@@ -70,16 +68,6 @@ def bench_decode(dev) -> List[Dict]:
         logical = B * ctx * Hkv * D * 2 * 2
         row = {"op": "decode_attn", "B": B, "ctx": ctx, "shared": shared, "us": round(us, 1),
                "GBps_unique": round(uniq / us / 1e3, 1), "GBps_logical": round(logical / us / 1e3, 1)}
-        if shared >= 2 * KV_BS:
-            lens_h, tables_h = lens.cpu().numpy(), tables.cpu().numpy()
-            t0 = time.perf_counter()
-            for _ in range(20):
-                plan = ops.plan_cascade(lens_h, tables_h, Hq // Hkv)
-            row["plan_host_us"] = round((time.perf_counter() - t0) / 20 * 1e6, 1)
-            ci = ops.CascadeInputs.from_plan(plan, dev)
-            usc = timeit(lambda: ops.decode(q, lens, tables, kc, vc, 0.088, workspace=ws, out=o, cascade=ci))
-            row["cascade_us"] = round(usc, 1)
-            row["cascade_GBps_unique"] = round(uniq / usc / 1e3, 1)
         out.append(row)
     return out
 
@@ -119,8 +107,7 @@ def bench_decode_mixed(dev) -> List[Dict]:
 
 def bench_decode_lean(dev) -> List[Dict]:
     """Work-balanced (lean) vs partitioned split-K decode on workload-shaped batches, interleaved
-    rounds; with and without the shared-prefix cascade.  GB/s counts unique KV bytes (the shared
-    prefix once) and logical bytes (every row's full context)."""
+    rounds.  GB/s counts unique KV bytes (the shared prefix once) and logical bytes (every row's full context)."""
     from ..ops import attention as A
     out = []
     g = torch.Generator(device=dev).manual_seed(3)
@@ -145,18 +132,13 @@ def bench_decode_lean(dev) -> List[Dict]:
         lens = torch.tensor(ctxs, dtype=torch.int32, device=dev)
         ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
         o = torch.empty_like(q)
-        plan = ops.plan_cascade(np.asarray(ctxs, np.int32), tables.numpy(), Hq // Hkv) if shared else None
-        ci = ops.CascadeInputs.from_plan(plan, dev) if plan is not None else None
 
-        def mk(lean, cas, chunks=0):
+        def mk(lean, chunks=0):
             def f():
                 A.DECODE_LEAN, A.LEAN_CHUNKS_PER_WAVE = lean, chunks
-                ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o, cascade=cas)
+                ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o)
             return f
-        fns = {"part": mk(False, None), "lean": mk(True, None, 0), "lean_dyn2": mk(True, None, 2),
-               "lean_dyn4": mk(True, None, 4)}
-        if ci is not None:
-            fns.update({"part_cascade": mk(False, ci), "lean_cascade": mk(True, ci)})
+        fns = {"part": mk(False), "lean": mk(True, 0), "lean_dyn2": mk(True, 2), "lean_dyn4": mk(True, 4)}
         ref = None
         errs = {}
         for k, f in fns.items():

@@ -116,14 +116,14 @@ class _FakeRetrieval:
 
 
 async def _replay(convs: int, turns: int, num_blocks: int, respond_tokens: int, hold: int, policy: str,
-                  warmup: int, hints: bool = True):
+                  warmup: int, hints: bool = True, tool_steps: int = 1):
     from ..engine.backend import EngineLLM
     from .workload import RagWorkload, decide_script
 
     eng = AuditEngine(num_blocks, hold=hold, policy=policy, hints=hints)
     llm = EngineLLM(eng, max_model_len=8192, decide_script=decide_script, respond_ignore_eos=True,
                     respond_tokens=respond_tokens)
-    wl = RagWorkload(llm, _FakeRetrieval(), convs, 10_000, respond_tokens)
+    wl = RagWorkload(llm, _FakeRetrieval(), convs, 10_000, respond_tokens, max_tool_steps=tool_steps)
     wl.kafka.setup_consumer()
     consumer = asyncio.create_task(wl.worker.consume_messages())
     per_turn: List[Dict] = []
@@ -159,13 +159,14 @@ def main(argv=None) -> int:
     ap.add_argument("--hold", type=int, default=0, help="requests in flight (blocks pinned)")
     ap.add_argument("--policy", default="lru")
     ap.add_argument("--no-hints", action="store_true", help="ignore the agent's ephemeral_kv hint (plain LRU)")
+    ap.add_argument("--tool-steps", type=int, default=1, help="agent tool-call rounds per turn (config 4: 3)")
     ap.add_argument("--per-turn", action="store_true")
     a = ap.parse_args(argv)
     pool = a.pool or 10_000_000
     summary, per_turn = asyncio.run(_replay(a.convs, a.turns, pool, a.respond_tokens, a.hold, a.policy, a.warmup,
-                                        not a.no_hints))
+                                        not a.no_hints, a.tool_steps))
     print(json.dumps({"convs": a.convs, "turns": a.turns, "warmup": a.warmup, "pool_blocks": a.pool or "inf",
-                      "policy": a.policy, "hold": a.hold, "hints": not a.no_hints,
+                      "policy": a.policy, "hold": a.hold, "hints": not a.no_hints, "tool_steps": a.tool_steps,
                       "per_turn_timed_mean": summary}))
     if a.per_turn:
         for p in per_turn:

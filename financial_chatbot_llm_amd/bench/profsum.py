@@ -16,7 +16,7 @@ from collections import defaultdict
 CLASSES = [
     ("gemm-prefill tile (HIP)", r"gemm_prefill_kernel"),
     ("attention-decode", r"decode_kernel|decode_reduce|decode_lean"),
-    ("attention-prefill", r"prefill_kernel|prefill2_kernel|cascade_kernel"),
+    ("attention-prefill", r"prefill_kernel|prefill2_kernel"),
     ("gemm-skinny (HIP)", r"skinny"),
     ("gemm-splitk (HIP)", r"splitk"),
     ("moe (HIP)", r"moe_|quant_rows"),

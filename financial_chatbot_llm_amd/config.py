@@ -151,10 +151,9 @@ class EngineConfig:
     # admission order: short-output (decide) prompts ahead of aged long-output ones (scheduler.py)
     sched_short_first: bool = False
     enable_prefix_caching: bool = True
-    # shared-prefix (cascade) decode attention over prefix-cached blocks.  Off by default: on
-    # MI355X the split-K decode grid already reads a shared prefix ~once from L2/MALL, so the
-    # extra launch + partials only pay at very high sharing (profiles/r1_decode_cascade.jsonl)
-    enable_cascade_attention: bool = False
+    # (a shared-prefix "cascade" decode attention was built in r1 and removed in r5: the lean
+    # split-K decode grid already reads a shared prefix ~once from L2/MALL, and the extra launch +
+    # partials only paid at very high sharing, profiles/r1_decode_cascade.jsonl)
     use_cuda_graph: bool = True             # hipGraph capture of decode steps
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256)
     seed: int = 0
@@ -186,7 +185,6 @@ class EngineConfig:
             sched_short_reserve_tokens=_env_int("PENNY_SHORT_RESERVE", cls.sched_short_reserve_tokens),
             sched_short_first=bool(_env_int("PENNY_SHORT_FIRST", int(cls.sched_short_first))),
             enable_prefix_caching=_env_bool("PENNY_PREFIX_CACHE", True),
-            enable_cascade_attention=_env_bool("PENNY_CASCADE_ATTENTION", False),
             moe_parallel=_env("PENNY_MOE_PARALLEL", cls.moe_parallel),
             sequence_parallel=_env_bool("PENNY_SEQUENCE_PARALLEL", False),
             async_scheduling=_env_bool("PENNY_ASYNC_SCHEDULING", True),

@@ -81,23 +81,6 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 // ------------------------------------------------------------------------------------------
 // Prefill
 // ------------------------------------------------------------------------------------------
-// Shared-prefix ("cascade") decode: the decode queries of every sequence in a prefix group are
-// the rows of one prefill-style tile against the group's shared KV blocks, so each shared block
-// is staged ONCE per 32 sequences instead of streamed once per sequence.  Output is flash-decoding
-// partial state (m, l, unnormalised O) in extra partition slots that decode_reduce merges with the
-// per-sequence suffix partitions.
-struct CascadeArgs {
-  const int* members;  // [*]  batch row of each group member (groups contiguous, bounds in cu_q)
-  const int* work;     // [nwork, 3] (group, member tile, kv chunk)
-  const int* nwork;    // device scalar
-  float* part_m;
-  float* part_l;
-  float* part_o;
-  int part_stride;     // partition slots per (row, head)
-  int slot0;           // first cascade slot (= number of suffix partitions)
-  int chunk_blocks;    // KV blocks per chunk (one work item)
-};
-
 // One 64-key block for a wave's 32 query rows (2 column tiles of 16): S^T = K.Q^T on MFMA,
 // base-2 online softmax in registers, O^T += V^T.P^T with P straight from the S^T registers.
 // kl / vl: the block's K and V tiles in LDS (fragment-native).  `full`: no key of the block needs
@@ -359,19 +342,20 @@ __device__ __forceinline__ void attend_block_fold(const uint4* __restrict__ kl, 
 template <int D>
 constexpr int prefill_smem_bytes() { return 4 * KV_BS * D * 2; }
 
-// One 128-row (token*G + head) tile of sequence/group `s`, kv head `h`, against KV blocks [jb, je).
-template <int D, bool CASCADE>
+// One 128-row (token*G + head) tile of sequence `s`, kv head `h` (4 waves x 32 rows): the short-chunk
+// prefill path (<= 128 rows per sequence and kv head).
+template <int D>
 __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__ q, const int* __restrict__ cu_q,
                                             const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
                                             const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
                                             bf16* __restrict__ out, float scale_log2, int Hq, int Hkv,
-                                            int max_blocks, int causal_arg, int s, int h, int tile, int chunk,
-                                            const CascadeArgs& ca, float* __restrict__ lse = nullptr) {
+                                            int max_blocks, int causal_arg, int s, int h, int tile,
+                                            float* __restrict__ lse = nullptr) {
   constexpr int KC = D / 32;                 // k-chunks of the QK^T product
   constexpr int DT = D / 16;                 // 16-row dim tiles of O^T
   constexpr int TILE = KV_BS * D * 2;        // bytes of one K (or V) block tile
   constexpr int PIECES = TILE / 1024 / 4;    // 1-KiB glds pieces per wave per tile
-  const bool causal = !CASCADE && causal_arg;
+  const bool causal = causal_arg;
 
   const int G = Hq / Hkv;
   const int TQ = 128 / G;
@@ -391,7 +375,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
     const bool valid = tok[ct] < qlen;
     qpos[ct] = valid ? ctx - qlen + tok[ct] : ctx - 1;
     const int qi = q0 + (valid ? tok[ct] : 0);
-    const bf16* qrow = q + ((long)(CASCADE ? ca.members[qi] : qi) * Hq + head[ct]) * D;
+    const bf16* qrow = q + ((long)qi * Hq + head[ct]) * D;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
       qf[ct][c].u = valid ? *reinterpret_cast<const uint4*>(qrow + c * 32 + g * 8) : make_uint4(0, 0, 0, 0);
@@ -400,9 +384,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
   const int last_tok = min(tok0 + TQ, qlen) - 1;
   const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
   const int nblk = (kv_end + KV_BS - 1) / KV_BS;
-  const int jb = CASCADE ? chunk * ca.chunk_blocks : 0;
-  const int je = CASCADE ? min(jb + ca.chunk_blocks, nblk) : nblk;
-  if (jb >= je && CASCADE) return;
+  const int jb = 0, je = nblk;
   const int* bt = block_tables + (long)s * max_blocks;
 
   f32x4 o[2][DT];
@@ -442,7 +424,7 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
     const uint4* kl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE);
     const uint4* vl = reinterpret_cast<const uint4*>(smem + buf * 2 * TILE + TILE);
 
-    const bool full = CASCADE || ((j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0));
+    const bool full = (j + 1) * KV_BS <= ctx && (!causal || (j + 1) * KV_BS - 1 <= ctx - qlen + tok0);
     attend_block<D, 2>(kl, vl, qf, o, m, l, causal, j, ctx, qpos, scale_log2, lane, g,
                        __builtin_amdgcn_readfirstlane((int)!full) != 0);
     __syncthreads();  // block j+1 landed (vmcnt drained) and everyone is done with buffer `buf`
@@ -454,17 +436,6 @@ __device__ __forceinline__ void attend_tile(char* smem, const bf16* __restrict__
     float lt = l[ct];
     lt = rowgroup_sum(lt);
     if (tok[ct] >= qlen) continue;
-    if constexpr (CASCADE) {
-      const long pi = ((long)ca.members[q0 + tok[ct]] * Hq + head[ct]) * ca.part_stride + ca.slot0 + chunk;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-        *reinterpret_cast<f32x4*>(ca.part_o + pi * D + 16 * dt + 4 * g) = o[ct][dt];
-      if (g == 0) {
-        ca.part_m[pi] = m[ct];
-        ca.part_l[pi] = lt;
-      }
-      continue;
-    }
     const float inv = lt > 0.f ? 1.f / lt : 0.f;
     bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
 #pragma unroll
@@ -486,23 +457,8 @@ __global__ void __launch_bounds__(256, 2) prefill_kernel(
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
     float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) char smem[prefill_smem_bytes<D>()];  // [buf][K|V]
-  attend_tile<D, false>(smem, q, cu_q, ctx_lens, block_tables, k_cache, v_cache, out, scale_log2, Hq, Hkv,
-                        max_blocks, causal, blockIdx.z, blockIdx.y, blockIdx.x, 0, CascadeArgs{}, lse);
-}
-
-// grid (W, Hkv): a fixed-size grid (hipGraph-capturable) strides over the device-side work list
-template <int D>
-__global__ void __launch_bounds__(256, 2) cascade_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ cu_g, const int* __restrict__ g_ctx,
-    const int* __restrict__ g_bt, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    float scale_log2, int Hq, int Hkv, int g_max_blocks, CascadeArgs ca) {
-  __shared__ __attribute__((aligned(16))) char smem[prefill_smem_bytes<D>()];
-  const int n = *ca.nwork;
-  for (int wi = blockIdx.x; wi < n; wi += gridDim.x) {
-    const int g = ca.work[3 * wi], tile = ca.work[3 * wi + 1], chunk = ca.work[3 * wi + 2];
-    attend_tile<D, true>(smem, q, cu_g, g_ctx, g_bt, k_cache, v_cache, nullptr, scale_log2, Hq, Hkv, g_max_blocks,
-                         0, g, blockIdx.y, tile, chunk, ca);
-  }
+  attend_tile<D>(smem, q, cu_q, ctx_lens, block_tables, k_cache, v_cache, out, scale_log2, Hq, Hkv, max_blocks,
+                 causal, blockIdx.z, blockIdx.y, blockIdx.x, lse);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -515,10 +471,10 @@ __global__ void __launch_bounds__(256, 2) cascade_kernel(
 // fastest: each XCD streams whole sequences, whose 8 heads of a KV block are contiguous.
 template <int D, bool HEAD_FAST>
 __global__ void __launch_bounds__(256) decode_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
-    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o,
-    float scale_log2, int Hq, int Hkv, int max_blocks, int pb, int nparts, int part_stride) {
+    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
+    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, float scale_log2, int Hq,
+    int Hkv, int max_blocks, int pb, int nparts, int part_stride) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ float s_m[4][16], s_l[4][16];
   __shared__ float s_o[4][16][D + 4];
@@ -528,7 +484,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
   const int h = HEAD_FAST ? blockIdx.x : blockIdx.z;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
-  const int blk0 = (kv_start ? kv_start[b] : 0) + p * pb;  // cascade: shared blocks are done elsewhere
+  const int blk0 = p * pb;
   if (blk0 >= nblk) return;
   const int blk1 = min(blk0 + pb, nblk);
   const int G = Hq / Hkv;
@@ -646,7 +602,7 @@ __global__ void __launch_bounds__(256) decode_kernel(
       O += s_o[ww][qc][d] * f;
     }
     const int hq = h * G + qc;
-    if (nparts == 1 && !kv_start) {
+    if (nparts == 1) {
       out[((long)b * Hq + hq) * D + d] = (bf16)(O / L);
     } else {
       const long pi = ((long)b * Hq + hq) * part_stride + p;
@@ -660,26 +616,17 @@ __global__ void __launch_bounds__(256) decode_kernel(
 }
 
 template <int D>
-__global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
-                                     const float* __restrict__ part_m, const float* __restrict__ part_l,
-                                     const float* __restrict__ part_o, bf16* __restrict__ out, int Hq, int pb,
-                                     int nparts, int part_stride, int chunk_blocks) {
+__global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const float* __restrict__ part_m,
+                                     const float* __restrict__ part_l, const float* __restrict__ part_o,
+                                     bf16* __restrict__ out, int Hq, int pb, int nparts, int part_stride) {
   const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
   const int nblk = (ctx_lens[b] + KV_BS - 1) / KV_BS;
-  const int s0 = kv_start ? kv_start[b] : 0;
-  const int np = min(nparts, (nblk - s0 + pb - 1) / pb);            // suffix partitions
-  const int nc = s0 > 0 ? (s0 + chunk_blocks - 1) / chunk_blocks : 0;  // shared-prefix chunks
+  const int np = min(nparts, (nblk + pb - 1) / pb);
   const long base = ((long)b * Hq + hq) * part_stride;
   float M = -INFINITY;
   for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
-  for (int i = 0; i < nc; ++i) M = fmaxf(M, part_m[base + nparts + i]);
   float L = 0.f, O = 0.f;
   for (int i = 0; i < np; ++i) {
-    const float f = exp2f(part_m[base + i] - M);
-    L += part_l[base + i] * f;
-    O += part_o[(base + i) * D + d] * f;
-  }
-  for (int i = nparts; i < nparts + nc; ++i) {
     const float f = exp2f(part_m[base + i] - M);
     L += part_l[base + i] * f;
     O += part_o[(base + i) * D + d] * f;
@@ -693,7 +640,7 @@ __global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int
 // The partitioned kernel above gives every (row, kv head, partition) its own workgroup, so a
 // batch whose contexts spread over 1.5-6.5k keys leaves long partitions running alone at the end
 // (and short rows waste whole workgroups).  Here each kv head's (row, block) units of the batch's
-// per-row SUFFIX (blocks from kv_start on -- cascade handles shared prefixes) are flattened
+// per-row KV blocks are flattened
 // row-major into one range that is cut into equal contiguous pieces, one per WAVE of the head's
 // share of a fixed grid sized to one round of the chip: every wave streams the same number of KV
 // blocks and the whole grid drains together.  Workgroup i serves kv head i % Hkv, so with the
@@ -702,25 +649,24 @@ __global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const int
 // writes one partial (m, l, unnormalised O) per row segment it touches, at slot (wave - first
 // wave of the segment); a segment one wave covers entirely is normalised and written straight to
 // `out` (no partial, no merge).  The plan (per-row prefix sums, units per wave) is recomputed by
-// every workgroup from ctx_lens/kv_start (device data: hipGraph-capturable), and workgroup 0
+// every workgroup from ctx_lens (device data: hipGraph-capturable), and workgroup 0
 // publishes it in `meta` for the merge kernel.
 constexpr int LEAN_MAX_B = 1024;
 
 struct LeanPlan {
-  int total;     // suffix blocks over all rows (per kv head)
+  int total;     // KV blocks over all rows (per kv head)
   int per_wave;  // units per wave
 };
 
-// s_pre[0..B]: exclusive prefix sums of the per-row suffix block counts
-__device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* __restrict__ ctx_lens,
-                                              const int* __restrict__ kv_start, int B, int nwaves, int nparts,
-                                              int min_per_wave) {
+// s_pre[0..B]: exclusive prefix sums of the per-row block counts
+__device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* __restrict__ ctx_lens, int B,
+                                              int nwaves, int nparts, int min_per_wave) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int c[4], sum = 0, mx = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int b = 4 * t + i;
-    c[i] = b < B ? (ctx_lens[b] + KV_BS - 1) / KV_BS - (kv_start ? kv_start[b] : 0) : 0;
+    c[i] = b < B ? (ctx_lens[b] + KV_BS - 1) / KV_BS : 0;
     sum += c[i];
     mx = max(mx, c[i]);
   }
@@ -767,15 +713,14 @@ constexpr int LEAN_META0 = 64;   // meta[0..64): per-head chunk counters; plan f
 
 template <int D>
 __global__ void __launch_bounds__(256) decode_lean_kernel(
-    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ kv_start,
-    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    bf16* __restrict__ out, float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o,
-    int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
+    const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
+    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
     int min_per_wave, int chunks_per_wave) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
-  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, kv_start, B, gridDim.x / Hkv * 4 * max(chunks_per_wave, 1),
+  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, B, gridDim.x / Hkv * 4 * max(chunks_per_wave, 1),
                                 nparts, min_per_wave);
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i <= B; i += 256) meta[LEAN_META0 + i] = s_pre[i];
@@ -807,8 +752,7 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
     const int seg0 = s_pre[b], n = s_pre[b + 1] - seg0;
     const int k0 = u - seg0, k1 = min(n, uend - seg0);
     const int ctx = ctx_lens[b];
-    const int kvs = kv_start ? kv_start[b] : 0;
-    const int* bt = block_tables + (long)b * max_blocks + kvs;
+    const int* bt = block_tables + (long)b * max_blocks;
 
     Frag qf[KC];
     {
@@ -842,7 +786,7 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int st = 0; st < 2; ++st) vf[dt][st].u = vb[(dt * 2 + st) * 64 + lane];
-      const int j = kvs + k;
+      const int j = k;
       f32x4 sc[4];
       float mt = -INFINITY;
 #pragma unroll
@@ -890,7 +834,7 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
     l = rowgroup_sum(l);
     if (col < G) {
       const int hq = h * G + col;
-      if (k0 == 0 && k1 == n && kvs == 0) {   // whole segment, no cascade part: final output
+      if (k0 == 0 && k1 == n) {   // whole segment: final output
         const float inv = 1.f / l;
         bf16* orow = out + ((long)b * Hq + hq) * D;
 #pragma unroll
@@ -920,36 +864,25 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
   }
 }
 
-// grid (Hq, B), D threads: merges a row's lean partials (slots 0..) and cascade chunks (slots
-// nparts..), skipping rows one wave already finished
+// grid (Hq, B), D threads: merges a row's lean partials, skipping rows one wave already finished
 template <int D>
-__global__ void decode_lean_reduce_kernel(int* __restrict__ meta, const int* __restrict__ ctx_lens,
-                                          const int* __restrict__ kv_start, const float* __restrict__ part_m,
+__global__ void decode_lean_reduce_kernel(int* __restrict__ meta, const float* __restrict__ part_m,
                                           const float* __restrict__ part_l, const float* __restrict__ part_o,
-                                          bf16* __restrict__ out, int B, int Hq, int Hkv, int nparts,
-                                          int part_stride, int chunk_blocks) {
+                                          bf16* __restrict__ out, int B, int Hq, int Hkv, int part_stride) {
   const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
   if (b == 0 && hq == 0 && d < Hkv) meta[d] = 0;   // chunk counters for the next launch
   const int pre = meta[LEAN_META0 + b], n = meta[LEAN_META0 + b + 1] - pre, pw = meta[LEAN_META0 + B + 1];
-  const int s0 = kv_start ? kv_start[b] : 0;
-  const int nc = s0 > 0 ? (s0 + chunk_blocks - 1) / chunk_blocks : 0;
   int np = 0;
   if (n > 0) {
     const int fw = pre / pw, lw = (pre + n - 1) / pw;
-    if (fw == lw && nc == 0) return;   // written by its one wave
+    if (fw == lw) return;   // written by its one wave
     np = lw - fw + 1;
   }
   const long base = ((long)b * Hq + hq) * part_stride;
   float M = -INFINITY;
   for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
-  for (int i = 0; i < nc; ++i) M = fmaxf(M, part_m[base + nparts + i]);
   float L = 0.f, O = 0.f;
   for (int i = 0; i < np; ++i) {
-    const float f = exp2f(part_m[base + i] - M);
-    L += part_l[base + i] * f;
-    O += part_o[(base + i) * D + d] * f;
-  }
-  for (int i = nparts; i < nparts + nc; ++i) {
     const float f = exp2f(part_m[base + i] - M);
     L += part_l[base + i] * f;
     O += part_o[(base + i) * D + d] * f;
@@ -1319,21 +1252,12 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
 PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const int* block_tables, const void* k_cache,
                                      const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
                                      int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts,
-                                     int part_stride, float scale, const int* kv_start, const int* members,
-                                     const int* cu_g, const int* g_ctx, const int* g_bt, const int* work,
-                                     const int* nwork, int grid_work, int g_max_blocks, int chunk_blocks,
-                                     int phases, int lean_grid, int* lean_meta, int lean_min_per_wave,
-                                     int lean_chunks_per_wave, hipStream_t stream) {
-  // phases: 1 cascade (shared-prefix tiles), 2 split-K decode, 4 merge -- the caller may run
-  // phase 1 on a side stream concurrently with phase 2 (ops/attention.py), joining before 4
+                                     int part_stride, float scale, int lean_grid, int* lean_meta,
+                                     int lean_min_per_wave, int lean_chunks_per_wave, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
-  const bool cascade = kv_start != nullptr;
-  if (cascade && (chunk_blocks <= 0 || grid_work <= 0 || 128 % (Hq / Hkv) ||
-                  part_stride < nparts + (g_max_blocks + chunk_blocks - 1) / chunk_blocks))
-    return (int)hipErrorInvalidValue;
-  // lean_grid > 0: the work-balanced suffix kernel (decode_lean_kernel) and its merge replace
-  // phases 2 and 4
+  // lean_grid > 0: the work-balanced kernel (decode_lean_kernel) and its merge; otherwise the
+  // per-(row, head, partition) kernel, kept as the fallback (PENNY_DECODE_LEAN=0)
   const bool lean = lean_grid > 0;
   if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv ||
                Hkv > LEAN_META0 || lean_chunks_per_wave < 0))
@@ -1348,31 +1272,27 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   const bool head_fast = head_fast_env >= 0 ? head_fast_env != 0 : B <= 16;
   const dim3 grid = head_fast ? dim3(Hkv, B, nparts) : dim3(B, nparts, Hkv);
   const float sl2 = scale * LOG2E;
-  const CascadeArgs ca{members, work, nwork, part_m, part_l, part_o, part_stride, nparts, chunk_blocks};
 #define DECODE_LAUNCH(DD)                                                                                         \
-  if (cascade && (phases & 1))                                                                                  \
-    hipLaunchKernelGGL(cascade_kernel<DD>, dim3(grid_work, Hkv), dim3(256), 0, stream, (const bf16*)q, cu_g, g_ctx,  \
-                       g_bt, (const bf16*)k_cache, (const bf16*)v_cache, sl2, Hq, Hkv, g_max_blocks, ca);         \
-  if ((phases & 2) && lean)                                                                                     \
+  if (lean) {                                                                                                   \
     hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
-                       kv_start, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,   \
-                       part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,              \
-                       lean_min_per_wave, lean_chunks_per_wave);                                                 \
-  if ((phases & 4) && lean)                                                                                     \
-    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, ctx_lens,       \
-                       kv_start, part_m, part_l, part_o, (bf16*)out, B, Hq, Hkv, nparts, part_stride,            \
-                       chunk_blocks);                                                                            \
-  if ((phases & 2) && !lean && head_fast)                                                                       \
-    hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start,  \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
-                       part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
-  if ((phases & 2) && !lean && !head_fast)                                                                      \
-    hipLaunchKernelGGL((decode_kernel<DD, false>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens, kv_start, \
-                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
-                       part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                                \
-  if ((phases & 4) && !lean && (nparts > 1 || cascade))                                                         \
-    hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, ctx_lens, kv_start, part_m,     \
-                       part_l, part_o, (bf16*)out, Hq, pb, nparts, part_stride, chunk_blocks);
+                       part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride, lean_min_per_wave,   \
+                       lean_chunks_per_wave);                                                                    \
+    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
+                       part_o, (bf16*)out, B, Hq, Hkv, part_stride);                                             \
+  } else {                                                                                                      \
+    if (head_fast)                                                                                              \
+      hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens,          \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,   \
+                         part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                              \
+    else                                                                                                        \
+      hipLaunchKernelGGL((decode_kernel<DD, false>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens,         \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,   \
+                         part_o, sl2, Hq, Hkv, max_blocks, pb, nparts, part_stride);                              \
+    if (nparts > 1)                                                                                             \
+      hipLaunchKernelGGL(decode_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, ctx_lens, part_m, part_l,     \
+                         part_o, (bf16*)out, Hq, pb, nparts, part_stride);                                        \
+  }
   if (D == 128) {
     DECODE_LAUNCH(128)
   } else if (D == 64) {

@@ -84,8 +84,7 @@ class LLMEngine:
                                    short_reserve_tokens=getattr(cfg, "sched_short_reserve_tokens", 0),
                                    short_first=getattr(cfg, "sched_short_first", False))
         self.runner = ModelRunner(self.model, self.kv, cfg.max_model_len, max_decode_batch=cfg.max_num_seqs,
-                                  use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes,
-                                  cascade=cfg.enable_cascade_attention)
+                                  use_graphs=cfg.use_cuda_graph, graph_sizes=cfg.graph_batch_sizes)
         self.requests: Dict[str, Sequence] = {}
         self.timing = {"prepare_s": 0.0, "execute_s": 0.0, "post_s": 0.0}   # host-side step anatomy
         self.spec_stats = {"proposed": 0, "accepted": 0}   # prompt-lookup draft tokens
@@ -587,8 +586,6 @@ class LLMEngine:
                 "steps": self.runner.stats["steps"], "graph_steps": self.runner.stats["graph_steps"],
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
                 "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),
-                "cascade_steps": self.runner.stats["cascade_steps"],
-                "cascade_rows": self.runner.stats["cascade_rows"],
                 "prefill_steps": self.runner.stats["prefill_steps"],
                 **(self.cp.stats if self.cp is not None else {}),
                 "prefill_step_tokens_mean": round(self.runner.stats["prefill_step_tokens"]

@@ -21,7 +21,7 @@ import torch
 
 from .. import ops
 from ..models.common import AttentionMetadata, KVCache
-from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace, plan_cascade, prefill_plan
+from ..ops.attention import KV_BS, DecodeWorkspace, prefill_plan
 from ..parallel import comm
 from ..utils.logging import get_logger
 from ..utils.profiling import marker
@@ -218,8 +218,7 @@ class _DecodeGraph:
 
 class ModelRunner:
     def __init__(self, model, kv: KVCache, max_model_len: int, max_decode_batch: int = 256,
-                 use_graphs: bool = True, graph_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 32, 64, 128, 256),
-                 cascade: bool = True):
+                 use_graphs: bool = True, graph_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 32, 64, 128, 256)):
         self.model = model
         self.kv = kv
         self.device = model.device
@@ -227,7 +226,6 @@ class ModelRunner:
         self.max_blocks = (max_model_len + KV_BS - 1) // KV_BS
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
-        self.cascade = cascade and self.on_gpu and ops._native.use_native(torch.empty(0, device=self.device))
         self.G = model.hq // model.hkv
         self.graph_sizes = tuple(sorted(s for s in graph_sizes if s <= max_decode_batch))
         self.max_decode_batch = max(self.graph_sizes) if self.graph_sizes else max_decode_batch
@@ -245,8 +243,7 @@ class ModelRunner:
         self.graphs_filt: Dict[int, _DecodeGraph] = {}   # top-k / top-p twins of fused buckets (lazy)
         self._static = None
         self.graph_pool = None
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "cascade_steps": 0, "cascade_rows": 0,
-                      "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
                       "gpu_idle_s": 0.0, "gpu_idle_gaps": 0, "_prev_end_ev": None, "overlap_steps": 0}
         # TP prefill steps of >= overlap_min_rows rows run as two micro-batches whose all-reduces
         # overlap the other half's compute (PENNY_TP_OVERLAP=0 disables)
@@ -338,19 +335,7 @@ class ModelRunner:
         if si.num_decode:
             m.ctx_lens_d = self._to_dev(si.ctx_d)
             m.block_tables_d = self._to_dev(si.bt_d)
-            plan = self._plan(si)
-            if plan is not None:
-                m.cascade = CascadeInputs.from_plan(plan, self.device)
         return m
-
-    def _plan(self, si: StepInputs):
-        if not self.cascade or si.num_decode < 2:
-            return None
-        plan = plan_cascade(si.ctx_d, si.bt_d, self.G)
-        if plan is not None:
-            self.stats["cascade_steps"] += 1
-            self.stats["cascade_rows"] += len(plan.members)
-        return plan
 
     def _gather_pending(self, ids: torch.Tensor, src: torch.Tensor, offset: int) -> None:
         """ids[offset + r] <- last_sampled[src[r]] where src[r] >= 0 (device-side, no host sync)."""
@@ -516,19 +501,16 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------
     def _alloc_static(self) -> None:
         B, W = self.max_decode_batch, self.max_blocks
-        # ids | pos | slots | ctx | block tables | cascade plan live in ONE device buffer fed by ONE
-        # pinned H2D copy
+        # ids | pos | slots | ctx | block tables | gather rows | top-k live in ONE device buffer fed
+        # by ONE pinned H2D copy
         self._src_off = 4 * B + B * W          # pending-token gather rows (-1: host id)
-        self._cas_off = self._src_off + B
-        n_cas = sum(n for _, n in CascadeInputs.section_sizes(B)) if self.cascade else 0
-        self._topk_off = self._cas_off + n_cas    # per-row top-k (0: off), in the same H2D copy
+        self._topk_off = self._src_off + B     # per-row top-k (0: off)
         self._dev_i32 = torch.zeros(self._topk_off + B, dtype=torch.int32, device=self.device)
         d = self._dev_i32
         self._static = {
             "ids": d[0:B], "pos": d[B:2 * B], "slots": d[2 * B:3 * B], "ctx": d[3 * B:4 * B],
             "bt": d[4 * B:self._src_off].view(B, W),
-            "src": d[self._src_off:self._cas_off],
-            "cascade": CascadeInputs.views(d[self._cas_off:self._topk_off], B) if self.cascade else None,
+            "src": d[self._src_off:self._topk_off],
             "top_k": d[self._topk_off:self._topk_off + B],
             "f32": torch.zeros(2 * B, dtype=torch.float32, device=self.device),     # temps | top_p
             "seeds": torch.zeros(B, dtype=torch.int64, device=self.device),
@@ -555,10 +537,6 @@ class ModelRunner:
                               and getattr(m.cfg, "arch", "") == "llama" and comm.custom_all_reduce() is not None
                               and getattr(comm, "_CUSTOM_AR_2", None) is not None
                               and os.environ.get("PENNY_TP_DUAL_DECODE", "1") != "0")
-            if self._dual and self.cascade:
-                # the two chains carry no cascade plan (forward_decode_dual): never drop it silently
-                logger.warning("TP dual decode disabled: cascade attention is on")
-                self._dual = False
             if self._dual:
                 # each chain's all-reduce must fit ITS custom instance: a half batch falling back to
                 # RCCL would put two streams' RCCL collectives on one communicator inside one graph
@@ -585,8 +563,7 @@ class ModelRunner:
             h = self.model.forward_decode_dual(s["ids"][:B], s["pos"][:B], metas, k, self.kv)
         else:
             meta = AttentionMetadata(slots=s["slots"][:B], num_prefill_tokens=0, num_decode=B,
-                                     ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws,
-                                     cascade=s["cascade"])
+                                     ctx_lens_d=s["ctx"][:B], block_tables_d=s["bt"][:B], decode_ws=self.decode_ws)
             h = self.model.forward(s["ids"][:B], s["pos"][:B], meta, self.kv)
         if not filtered:
             if self._shard_sampling():     # TP: top-k / top-p rows of this bucket replay eagerly
@@ -690,8 +667,6 @@ class ModelRunner:
         src[:B] = -1
         if si.src is not None:
             src[:n] = si.src
-        if self.cascade:
-            CascadeInputs.pack(self._plan(si), buf[self._cas_off:], S, n)
         tk = buf[self._topk_off:self._topk_off + S]
         tk[:B] = 0
         tk[:n] = si.top_k

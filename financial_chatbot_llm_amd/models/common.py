@@ -7,7 +7,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..ops.attention import KV_BS, CascadeInputs, DecodeWorkspace
+from ..ops.attention import KV_BS, DecodeWorkspace
 
 
 @dataclass
@@ -25,7 +25,6 @@ class AttentionMetadata:
     ctx_lens_d: Optional[torch.Tensor] = None  # [Bd]
     block_tables_d: Optional[torch.Tensor] = None
     decode_ws: Optional[DecodeWorkspace] = None
-    cascade: Optional[CascadeInputs] = None     # shared-prefix groups of the decode rows
     causal: bool = True
     prefill_work: Optional[torch.Tensor] = None  # [n, 2] int32 (ops.attention.prefill_work_list) or lean [., 6]
     prefill_lean: Optional[tuple] = None          # lean list counts (items, merges, slots), host ints

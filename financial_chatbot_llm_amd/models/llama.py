@@ -229,7 +229,7 @@ class DecoderModel:
         attn = torch.empty_like(q)
         tp = meta.num_prefill_tokens
         side = None
-        if tp > 0 and meta.num_decode > 0 and ATTN_OVERLAP and q.is_cuda and meta.cascade is None:
+        if tp > 0 and meta.num_decode > 0 and ATTN_OVERLAP and q.is_cuda:
             # mixed step: the decode rows' attention (HBM-bound: streams their whole contexts) runs on
             # a side stream CONCURRENTLY with the prefill rows' attention (MFMA-bound) -- the two read
             # disjoint sequences' KV and write disjoint rows of attn; joined before the O projection
@@ -246,7 +246,7 @@ class DecoderModel:
             torch.cuda.current_stream().wait_stream(side)
         elif meta.num_decode > 0:
             ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
-                       workspace=meta.decode_ws, out=attn[tp:], cascade=meta.cascade)
+                       workspace=meta.decode_ws, out=attn[tp:])
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"),
                      slabs=self.tp_size == 1, fuse_residual=fuse_residual)
         return comm.tp_all_reduce(out) if self.tp_size > 1 and reduce else out

@@ -5,8 +5,8 @@ loudly if the library is missing), CPU tensors run an fp32 PyTorch reference tha
 oracle in the numerics tests.
 """
 from .activation import gelu_, silu_mul
-from .attention import (KV_BS, CascadeInputs, DecodeWorkspace, decode, default_scale, plan_cascade, prefill,
-                        rope_cos_sin, rope_kv_write, write_kv_ref)
+from .attention import (KV_BS, DecodeWorkspace, decode, default_scale, prefill, rope_cos_sin, rope_kv_write,
+                        write_kv_ref)
 from .embedding import embedding
 from .norm import layer_norm, rms_norm
 from .retrieval import filtered_topk

@@ -356,7 +356,7 @@ class DecodeWorkspace:
     part_o: torch.Tensor
     pb: int
     nparts: int
-    part_stride: int = 0    # partition slots per (row, head): nparts suffix + cascade chunk slots
+    part_stride: int = 0    # partition slots per (row, head)
     lean_meta: Optional[torch.Tensor] = None   # [64 + max_batch + 2] int32: chunk counters + lean plan
 
     def partitioning(self, B: int):
@@ -379,152 +379,11 @@ class DecodeWorkspace:
     def create(cls, max_batch: int, Hq: int, D: int, max_ctx: int, device, pb: int = 8) -> "DecodeWorkspace":
         nblk = (max_ctx + KV_BS - 1) // KV_BS
         nparts = max(2, (nblk + pb - 1) // pb)
-        stride = nparts + CASCADE_MAX_CHUNKS
+        stride = max(nparts, 2)
         f = dict(dtype=torch.float32, device=device)
         return cls(torch.empty((max_batch, Hq, stride), **f), torch.empty((max_batch, Hq, stride), **f),
                    torch.empty((max_batch, Hq, stride, D), **f), pb, max(nparts, 2), stride,
                    torch.zeros(LEAN_META0 + max_batch + 2, dtype=torch.int32, device=device))
-
-
-# ----------------------------------------------------------------------------------------------
-# Shared-prefix (cascade) decode
-# ----------------------------------------------------------------------------------------------
-# Prefix caching makes every decode sequence of a turn type point at the SAME physical blocks for
-# its system/tool prompt (2k tokens for the decide prompt, ~0.8k for the respond prompt).  Those
-# blocks are attended by one prefill-style MFMA tile per 32 sequences (cascade_kernel), the
-# per-sequence suffix by the split-K decode kernel, and decode_reduce merges both.
-CASCADE_CHUNK = 4            # KV blocks per cascade work item (256 keys)
-CASCADE_MAX_BLOCKS = 64      # longest shared prefix handled (4096 tokens); longer -> capped
-CASCADE_MAX_CHUNKS = CASCADE_MAX_BLOCKS // CASCADE_CHUNK
-CASCADE_MAX_GROUPS = 8
-CASCADE_MIN_BLOCKS = 2
-CASCADE_GRID = 64            # fixed grid.x of the cascade kernel (strides over the work list)
-
-
-@dataclass
-class CascadePlan:
-    """Host plan of one decode batch's prefix groups (all int32 numpy)."""
-
-    kv_start: np.ndarray     # [B] shared blocks skipped by the suffix kernel (0 = no group)
-    members: np.ndarray      # [M] batch rows, grouped
-    cu_g: np.ndarray         # [ng+1]
-    g_ctx: np.ndarray        # [ng] shared tokens
-    g_bt: np.ndarray         # [ng, CASCADE_MAX_BLOCKS]
-    work: np.ndarray         # [nw, 3] (group, member tile, chunk)
-
-    @property
-    def num_groups(self) -> int:
-        return len(self.g_ctx)
-
-
-def plan_cascade(ctx_lens: np.ndarray, block_tables: np.ndarray, G: int,
-                 min_members: int = 2) -> Optional[CascadePlan]:
-    """Group decode rows by identical leading physical KV blocks.
-
-    A row's last block (holding the token being decoded) is never shared.  Rows are grouped by
-    their first block; a group's shared prefix is the longest common block prefix of its rows,
-    capped at CASCADE_MAX_BLOCKS.  Returns None when no group is worth it."""
-    B = len(ctx_lens)
-    if B < min_members or block_tables.shape[1] < CASCADE_MIN_BLOCKS:
-        return None
-    usable = (np.asarray(ctx_lens) + KV_BS - 1) // KV_BS - 1
-    first = block_tables[:, 0]
-    cand = np.nonzero(usable >= CASCADE_MIN_BLOCKS)[0]
-    if len(cand) < min_members:
-        return None
-    order = cand[np.argsort(first[cand], kind="stable")]
-    keys = first[order]
-    bounds = np.flatnonzero(np.diff(keys)) + 1
-    groups = []
-    for rows in np.split(order, bounds):
-        if len(rows) < min_members:
-            continue
-        lim = int(min(usable[rows].min(), CASCADE_MAX_BLOCKS))
-        sub = block_tables[rows, :lim]
-        same = (sub == sub[0]).all(axis=0)
-        lcp = lim if same.all() else int(np.argmin(same))
-        if lcp >= CASCADE_MIN_BLOCKS:
-            groups.append((len(rows) * lcp, rows, lcp))
-    if not groups:
-        return None
-    groups.sort(key=lambda t: -t[0])          # keep the groups that save the most KV reads
-    groups = groups[:CASCADE_MAX_GROUPS]
-    tq = 128 // G
-    kv_start = np.zeros(B, np.int32)
-    members, cu, g_ctx, work = [], [0], [], []
-    g_bt = np.zeros((len(groups), CASCADE_MAX_BLOCKS), np.int32)
-    for gi, (_, rows, lcp) in enumerate(groups):
-        kv_start[rows] = lcp
-        members.extend(rows.tolist())
-        cu.append(cu[-1] + len(rows))
-        g_ctx.append(lcp * KV_BS)
-        g_bt[gi, :lcp] = block_tables[rows[0], :lcp]
-        for t in range((len(rows) + tq - 1) // tq):
-            for c in range((lcp + CASCADE_CHUNK - 1) // CASCADE_CHUNK):
-                work.append((gi, t, c))
-    i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
-    return CascadePlan(kv_start, i32(members), i32(cu), i32(g_ctx), g_bt, i32(work).reshape(-1, 3))
-
-
-@dataclass
-class CascadeInputs:
-    """Device views of a CascadePlan (eager: exact sizes; hipGraph: capacity-sized sections of
-    the step's staging buffer, with ``nwork`` read by the kernel)."""
-
-    kv_start: torch.Tensor
-    members: torch.Tensor
-    cu_g: torch.Tensor
-    g_ctx: torch.Tensor
-    g_bt: torch.Tensor
-    work: torch.Tensor
-    nwork: torch.Tensor      # [1]
-    grid: int = CASCADE_GRID
-
-    @staticmethod
-    def section_sizes(B: int):
-        """int32 element counts of each section for a batch capacity B (fixed graph layout)."""
-        max_work = (B // 8 + 1 + CASCADE_MAX_GROUPS) * CASCADE_MAX_CHUNKS   # member tiles >= 8 rows (G <= 16)
-        return [("kv_start", B), ("members", B), ("cu_g", CASCADE_MAX_GROUPS + 1), ("g_ctx", CASCADE_MAX_GROUPS),
-                ("g_bt", CASCADE_MAX_GROUPS * CASCADE_MAX_BLOCKS), ("work", 3 * max_work), ("nwork", 1)]
-
-    @classmethod
-    def views(cls, buf: torch.Tensor, B: int) -> "CascadeInputs":
-        out, off = {}, 0
-        for name, n in cls.section_sizes(B):
-            out[name] = buf[off:off + n]
-            off += n
-        out["g_bt"] = out["g_bt"].view(CASCADE_MAX_GROUPS, CASCADE_MAX_BLOCKS)
-        return cls(**out)
-
-    @staticmethod
-    def pack(plan: Optional[CascadePlan], host: np.ndarray, B: int, n: int) -> None:
-        """Write ``plan`` for the first n rows of a capacity-B layout into int32 ``host``."""
-        off = 0
-        sec = dict()
-        for name, cnt in CascadeInputs.section_sizes(B):
-            sec[name] = host[off:off + cnt]
-            off += cnt
-        sec["kv_start"][:] = 0
-        sec["nwork"][0] = 0
-        if plan is None:
-            return
-        sec["kv_start"][:n] = plan.kv_start
-        sec["members"][:len(plan.members)] = plan.members
-        sec["cu_g"][:len(plan.cu_g)] = plan.cu_g
-        sec["g_ctx"][:len(plan.g_ctx)] = plan.g_ctx
-        sec["g_bt"][:plan.g_bt.size] = plan.g_bt.reshape(-1)
-        sec["work"][:plan.work.size] = plan.work.reshape(-1)
-        sec["nwork"][0] = len(plan.work)
-
-    @classmethod
-    def from_plan(cls, plan: CascadePlan, device) -> "CascadeInputs":
-        B = len(plan.kv_start)
-        host = np.zeros(sum(n for _, n in cls.section_sizes(B)), np.int32)
-        cls.pack(plan, host, B, B)
-        buf = torch.from_numpy(host)
-        if torch.device(device).type == "cuda":
-            buf = buf.pin_memory().to(device, non_blocking=True)
-        return cls.views(buf, B)
 
 
 _SIDE_STREAMS = {}
@@ -562,12 +421,10 @@ def _side_stream(device) -> "torch.cuda.Stream":
 
 def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, k_cache: torch.Tensor,
            v_cache: torch.Tensor, scale: float, workspace: Optional[DecodeWorkspace] = None,
-           max_ctx: Optional[int] = None, out: Optional[torch.Tensor] = None,
-           cascade: Optional[CascadeInputs] = None) -> torch.Tensor:
-    """One query token per sequence against its paged context (split-K over partitions).
-
-    With ``cascade`` the shared-prefix blocks of each group are attended once per 32 rows by the
-    cascade kernel and merged with the per-row suffix partitions (same result, far fewer bytes)."""
+           max_ctx: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One query token per sequence against its paged context: the work-balanced split-K kernel
+    (``decode_lean_kernel``) by default, the per-(row, head, partition) kernel with
+    ``PENNY_DECODE_LEAN=0``."""
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     if N.use_native(q):
@@ -577,31 +434,15 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
                 max_ctx = int(ctx_lens.max().item())
             workspace = DecodeWorkspace.create(B, Hq, D, max(max_ctx, 1), q.device)
         ws = workspace
-        c = cascade
-        cas = ((N.ptr(c.kv_start), N.ptr(c.members), N.ptr(c.cu_g), N.ptr(c.g_ctx), N.ptr(c.g_bt), N.ptr(c.work),
-                N.ptr(c.nwork), c.grid, CASCADE_MAX_BLOCKS, CASCADE_CHUNK) if c is not None
-               else (None, None, None, None, None, None, None, 0, 0, 0))
         lean = (DECODE_LEAN and B >= LEAN_MIN_B and ws.lean_meta is not None
                 and ws.lean_meta.numel() >= LEAN_META0 + B + 2)
-        pb, nparts = ws.partitioning(B) if (c is None and not lean) else (ws.pb, ws.nparts)
+        pb, nparts = ws.partitioning(B) if not lean else (ws.pb, ws.nparts)
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
-                nparts, ws.part_stride, float(scale), *cas]
+                nparts, ws.part_stride, float(scale)]
         lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE)
                      if lean else (0, None, 1, 0))
-        if c is None:
-            N.call("penny_attention_decode", *args, 7, *lean_args, N.stream())
-        else:
-            # shared-prefix tiles on a side stream, concurrent with the per-row suffix partitions;
-            # join before the merge (fork/join via events: hipGraph-capturable)
-            main = torch.cuda.current_stream()
-            side = _side_stream(q.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                N.call("penny_attention_decode", *args, 1, *lean_args, side.cuda_stream)
-            N.call("penny_attention_decode", *args, 2, *lean_args, main.cuda_stream)
-            main.wait_stream(side)
-            N.call("penny_attention_decode", *args, 4, *lean_args, main.cuda_stream)
+        N.call("penny_attention_decode", *args, *lean_args, N.stream())
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()

@@ -133,30 +133,6 @@ def test_bge_encoder_gpu_matches_cpu():
     assert torch.allclose(a, b, atol=3e-2), (a - b).abs().max()
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_cascade_attention_engine_matches_plain(graphs):
-    """Rows sharing a prefix-cached system prompt decode through the cascade path (eager and
-    hipGraph) and produce the same greedy tokens as plain split-K decode."""
-    base = dict(model="llama-tiny", device="cuda", num_kv_blocks=256, max_model_len=2048, max_num_seqs=16,
-                graph_batch_sizes=(1, 2, 4, 8, 16), use_cuda_graph=graphs)
-    system = list(range(300, 300 + 5 * KV_BS + 9))                  # 5 full shared blocks
-    prompts = [system + list(range(1000 + 13 * i, 1000 + 13 * i + 20 + 9 * i)) for i in range(6)]
-    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
-    e1 = LLMEngine(EngineConfig(enable_cascade_attention=False, **base))
-    e1.generate([system + [7]], SamplingParams(temperature=0.0, max_tokens=1))  # warm the prefix cache
-    plain = e1.generate(prompts, sp)
-    e2 = LLMEngine(EngineConfig(enable_cascade_attention=True, **base), model=e1.model)
-    e2.warmup()
-    e2.generate([system + [7]], SamplingParams(temperature=0.0, max_tokens=1))
-    casc = e2.generate(prompts, sp)
-    assert e2.runner.stats["cascade_steps"] >= 8 and e2.runner.stats["cascade_rows"] >= 40
-    # greedy decoding of a random model: one near-tied pick flips the rest of that sequence, so
-    # require the leading tokens everywhere and high overall agreement (kernel-level exactness is
-    # test_kernels_gpu.py::test_cascade_decode_matches_reference)
-    agree = sum(a == b for x, y in zip(plain, casc) for a, b in zip(x, y)) / 72
-    assert agree >= 0.85 and all(x[:4] == y[:4] for x, y in zip(plain, casc)), (plain, casc)
-
-
 def test_gemm_tuning_table_loads_and_matches_default():
     """The curated TunableOp table must pass the runtime's validators (else it is silently
     ignored) and its solutions must compute the same GEMM."""
