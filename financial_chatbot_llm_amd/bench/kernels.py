@@ -261,7 +261,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2": 0, "pf2_sb": 4, "pf2_fold": 5, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
+        variants = {"pf2_sb": 4, "pf2_fold": 5, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
                     "pf2_fold_lean": "lean_5", "pf2_foldq_lean": "lean_6"}
         old = ops.attention.prefill_variant()
         outs = {}
@@ -277,7 +277,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         for k in variants:
             row[f"{k}_us"] = round(ts[k], 1)
             row[f"{k}_TFLOPs"] = round(flops / ts[k] / 1e6, 1)
-            row[f"{k}_maxdiff_vs_pf2"] = round(float((outs[k].float() - outs["pf2"].float()).abs().max()), 5)
+            row[f"{k}_maxdiff_vs_pf2_sb"] = round(float((outs[k].float() - outs["pf2_sb"].float()).abs().max()), 5)
         print(json.dumps(row), flush=True)
         out.append(row)
     return out

@@ -9,6 +9,7 @@ retrieval / copies) so the per-step budget is visible at a glance.
 from __future__ import annotations
 
 import argparse
+import bisect
 import csv
 import re
 from collections import defaultdict
@@ -117,17 +118,92 @@ def gaps(trace_csv: str, top: int = 12) -> str:
     return "\n".join(out) + "\n"
 
 
+def _ranges(marker_csv: str):
+    """roctx ranges of a rocprofv3 --marker-trace CSV: {thread: sorted [(start, end, name)]}."""
+    by_t = defaultdict(list)
+    with open(marker_csv) as fh:
+        for r in csv.DictReader(fh):
+            s_, e_ = int(r.get("Start_Timestamp") or 0), int(r.get("End_Timestamp") or 0)
+            name = r.get("Function") or r.get("Operation") or r.get("Name") or "?"
+            if e_ > s_:
+                by_t[r.get("Thread_Id", "0")].append((s_, e_, name))
+    for v in by_t.values():
+        v.sort()
+    return by_t
+
+
+def _innermost(rs, starts, maxdur, t):
+    """Shortest range of one thread's sorted ranges containing time t (None: outside all)."""
+    i = bisect.bisect_right(starts, t) - 1
+    best = None
+    while i >= 0 and starts[i] >= t - maxdur:
+        s_, e_, n = rs[i]
+        if e_ >= t and (best is None or e_ - s_ < best[1] - best[0]):
+            best = (s_, e_, n)
+        i -= 1
+    return best
+
+
+def gaps_by_marker(trace_csv: str, marker_csv: str, min_us: float = 100.0, top: int = 16) -> str:
+    """Attribute every GPU idle gap >= min_us to what the host threads were doing at its midpoint:
+    the innermost roctx range (PENNY_MARKERS=1) of the engine thread (the one issuing
+    ``engine.step``) and of any other thread active then (serving loop, retrieval)."""
+    iv = []
+    with open(trace_csv) as fh:
+        for r in csv.DictReader(fh):
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    iv.sort()
+    gaps = []
+    ce = iv[0][1]
+    for s_, e_ in iv[1:]:
+        if s_ - ce >= min_us * 1e3:
+            gaps.append((ce, s_))
+        ce = max(ce, e_)
+    by_t = _ranges(marker_csv)
+    eng = next((t for t, rs in by_t.items() if any(n.startswith("engine.step") for _, _, n in rs)), None)
+    idx = {t: ([x[0] for x in rs], max(e_ - s_ for s_, e_, _ in rs)) for t, rs in by_t.items()}
+    norm = lambda n: re.sub(r"\[\d+\]", "[n]", n)  # noqa: E731
+    eng_tab = defaultdict(lambda: [0, 0.0])
+    oth_tab = defaultdict(lambda: [0, 0.0])
+    for gs, ge in gaps:
+        mid = (gs + ge) // 2
+        d = ge - gs
+        lab = "(engine thread outside every range)"
+        if eng is not None:
+            hit = _innermost(by_t[eng], idx[eng][0], idx[eng][1], mid)
+            if hit is not None:
+                lab = norm(hit[2])
+        eng_tab[lab][0] += 1
+        eng_tab[lab][1] += d
+        others = sorted({norm(h[2]) for t, rs in by_t.items() if t != eng
+                         for h in [_innermost(rs, idx[t][0], idx[t][1], mid)] if h is not None})
+        k = (lab, ", ".join(others) or "-")
+        oth_tab[k][0] += 1
+        oth_tab[k][1] += d
+    tot = sum(ge - gs for gs, ge in gaps)
+    out = [f"GPU idle gaps >= {min_us:.0f} us: {len(gaps)}, {tot / 1e9:.3f} s", "",
+           "| engine thread in | gaps | total s | mean us |", "|---|---:|---:|---:|"]
+    for k, (c, t) in sorted(eng_tab.items(), key=lambda kv: -kv[1][1])[:top]:
+        out.append(f"| {k} | {c} | {t / 1e9:.3f} | {t / max(c, 1) / 1e3:.1f} |")
+    out += ["", "| engine thread in | other threads in | gaps | total s |", "|---|---|---:|---:|"]
+    for (a, b), (c, t) in sorted(oth_tab.items(), key=lambda kv: -kv[1][1])[:top]:
+        out.append(f"| {a} | {b} | {c} | {t / 1e9:.3f} |")
+    return "\n".join(out) + "\n"
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--title", default="")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--trace", default="", help="kernel_trace.csv: also report GPU busy fraction")
+    ap.add_argument("--markers", default="", help="marker_api_trace.csv (with --trace): idle gaps by host range")
     a = ap.parse_args(argv)
     text = summarise(a.csv, a.title, a.top)
     if a.trace:
         head, rest = text.split("\n\n", 1)
-        text = head + "\n\n" + utilisation(a.trace) + "\n" + gaps(a.trace) + "\n" + rest
+        extra = gaps_by_marker(a.trace, a.markers) + "\n" if a.markers else ""
+        text = head + "\n\n" + utilisation(a.trace) + "\n" + gaps(a.trace) + "\n" + extra + rest
     print(text, end="")
     return 0
 

@@ -1145,10 +1145,9 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                      (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
                      (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
 #define LEAN_VARIANTS(DD)                                   \
-  if (var == 5) LEAN_LAUNCH(DD, true, true, 1);             \
-  else if (var == 6) LEAN_LAUNCH(DD, true, true, 2);        \
+  if (var == 6) LEAN_LAUNCH(DD, true, true, 2);             \
   else if (var == 4) LEAN_LAUNCH(DD, true, true, 0);        \
-  else LEAN_LAUNCH(DD, true, false, 0);                     \
+  else LEAN_LAUNCH(DD, true, true, 1);                      \
   if (nmerge > 0)                                           \
     hipLaunchKernelGGL(prefill_merge_kernel<DD>, dim3(nmerge, Hkv, 256 / (4 * (64 / (DD / 4)))), dim3(256), 0, stream, \
                        merge, cu_q, part_o, part_ml, (bf16*)out, lse, Hq, Hkv);
@@ -1168,9 +1167,10 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
 // runs): 5 (default) prefill2 with the VALU-lean softmax (ones-MFMA row sums, lean max / grow
 // logic, exact Q; attend_block_fold), 6 = 5 with Q prescaled by scale*log2(e) (no per-score FMA; one
 // extra bf16 rounding of q*c, opt-in), 4 prefill2 with its K/V fragment prefetch pinned ahead of the
-// MFMAs (the r4 default, kept as the fallback with its tests), 0 prefill2.  The ping-pong prefill3
-// (r4 variants 1-3: 15-20 % slower on every mixed step, profiles/r4_prefill_attn_pingpong_lean_rejected.jsonl)
-// was removed in r5.
+// MFMAs (the r4 default, kept as the fallback with its tests); any other value selects 5.  Removed
+// in r5: the ping-pong prefill3 (r4 variants 1-3: 15-20 % slower on every mixed step,
+// profiles/r4_prefill_attn_pingpong_lean_rejected.jsonl), the unpinned prefill2 (variant 0, 4-6 %
+// slower than 4) and the tile-fastest grid order (PENNY_PREFILL_HEAD_FAST=0, 5-47 % slower).
 static int g_prefill_variant = -1;
 static int prefill_variant() {
   if (g_prefill_variant < 0) {
@@ -1200,40 +1200,27 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   const int pp_env = prefill_variant();
   const int TQ = (big ? 256 : 128) / G;
   const int ntiles = (max_q_len + TQ - 1) / TQ;
-  // XCD-per-kv-head order measured +5-47 % TF/s (profiles/r1_prefill_head_fast.txt: 457 -> 672 at
-  // 4 x 2048 causal, 687 -> 905 at 1 x 8192); PENNY_PREFILL_HEAD_FAST=0 restores tile-fastest
-  static const int head_fast_env = [] {
-    const char* v = getenv("PENNY_PREFILL_HEAD_FAST");
-    return v ? atoi(v) : 1;
-  }();
-  const bool head_fast = head_fast_env != 0;
+  // grid (Hkv, tiles, seqs): the kv head is the fastest workgroup index, so with round-robin dispatch
+  // over the 8 XCDs each XCD owns one kv head (+5-47 % TF/s over tile-fastest,
+  // profiles/r1_prefill_head_fast.txt: 457 -> 672 at 4 x 2048 causal, 687 -> 905 at 1 x 8192)
   // work list (big tiles only): one workgroup per real (sequence, tile), LPT order
   const bool wl = big && work != nullptr && nwork > 0;
-  dim3 grid(ntiles, Hkv, num_seqs);
-  const dim3 grid2 = wl ? (head_fast ? dim3(Hkv, nwork, 1) : dim3(nwork, Hkv, 1))
-                        : (head_fast ? dim3(Hkv, ntiles, num_seqs) : grid);
+  const dim3 grid(ntiles, Hkv, num_seqs);
+  const dim3 grid2 = wl ? dim3(Hkv, nwork, 1) : dim3(Hkv, ntiles, num_seqs);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && head_fast && pp_env == 5)                                                                           \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 1>), grid2, dim3(512), 0, stream,            \
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big && head_fast && pp_env == 6)                                                                      \
+  if (big && pp_env == 6)                                                                                        \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big && head_fast && pp_env == 4)                                                                      \
+  else if (big && pp_env == 4)                                                                                   \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true>), grid2, dim3(512), 0, stream,               \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big && head_fast)                                                                                     \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true>), grid2, dim3(512), 0, stream,                           \
+  else if (big)                                                                                                  \
+    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 1>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big)                                                                                                  \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, false>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q,    \
-                       ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,    \
-                       Hkv, max_blocks, causal, lse, wp);                                                          \
   else                                                                                                           \
     hipLaunchKernelGGL(prefill_kernel<DD>, grid, dim3(256), 0, stream, (const bf16*)q, cu_q, ctx_lens,           \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,         \

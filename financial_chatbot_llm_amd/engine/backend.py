@@ -29,6 +29,7 @@ from ..agent.grammar import ToolCallGrammar, jump_mask
 from ..agent.llm import LLMBackend, LLMResult
 from ..agent.toolcall import parse_tool_calls
 from ..tools.base import Tool
+from ..utils.profiling import marker
 from ..wire import ChatMessage
 from .async_engine import AsyncEngine
 from .chat_template import ChatEncoder
@@ -83,8 +84,9 @@ class EngineLLM(LLMBackend):
         return self.encoder.count(text)
 
     def _encode(self, messages, tools, max_tokens) -> list:
-        ids = self.encoder.encode(messages, tools, max_prompt_tokens=self.max_model_len - max_tokens - 1,
-                                  history_token_budget=self.history_token_budget)
+        with marker("serve.encode"):
+            ids = self.encoder.encode(messages, tools, max_prompt_tokens=self.max_model_len - max_tokens - 1,
+                                      history_token_budget=self.history_token_budget)
         self.last_prompt_tokens = len(ids)
         return ids
 

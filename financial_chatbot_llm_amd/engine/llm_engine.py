@@ -434,12 +434,15 @@ class LLMEngine:
         t0 = time.perf_counter()
         prev = self._inflight
         if prev is not None:
-            self._advance(prev[0], prev[1])
-        batch = self.scheduler.schedule()
+            with marker("engine.advance"):
+                self._advance(prev[0], prev[1])
+        with marker("engine.schedule"):
+            batch = self.scheduler.schedule()
         launched = None
         t1 = t0
         if not batch.empty():
-            si = build_step_inputs(batch)
+            with marker("engine.inputs"):
+                si = build_step_inputs(batch)
             if self.ps.tp_size > 1:
                 tb = time.perf_counter()
                 comm.broadcast_step(si)
@@ -458,7 +461,10 @@ class LLMEngine:
         t2 = time.perf_counter()
         outs: List[StepOutput] = []
         if prev is not None:
-            outs = self._resolve(prev[1], prev[2].result())
+            with marker("engine.wait"):
+                res = prev[2].result()
+            with marker("engine.resolve"):
+                outs = self._resolve(prev[1], res)
         self._inflight = launched
         t3 = time.perf_counter()
         tm = self.timing

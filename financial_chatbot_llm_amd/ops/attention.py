@@ -261,7 +261,7 @@ def prefill_plan(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causa
                  cus: int = 256) -> Optional[np.ndarray]:
     """The step's prefill-attention work list: lean ([., 6], when some walk needs splitting; every
     prefill2 variant takes it) or whole tiles in LPT order ([n, 2])."""
-    if PREFILL_LEAN and prefill_variant() in (0, 4, 5, 6):
+    if PREFILL_LEAN:
         lean = prefill_lean_list(cu_q, ctx_lens, G, Hkv, causal, cus)
         if lean is not None:
             return lean
@@ -286,7 +286,7 @@ def _lean_workspace(dev: torch.device, slots: int, Hkv: int, D: int) -> Tuple[to
 def prefill_variant(v: int = -1) -> int:
     """Select the big-tile prefill kernel for this process (returns the previous choice; -1 only
     reads it): 5 = prefill2 with the VALU-lean softmax (default), 6 = 5 with prescaled Q (opt-in),
-    4 = prefill2 with pinned K/V fragment prefetch (r4 default, the fallback), 0 = prefill2
+    4 = prefill2 with pinned K/V fragment prefetch (r4 default, the fallback); other values select 5
     (``PENNY_PREFILL_PP`` sets the initial value).  In-process A/B runs and tests only."""
     return int(N.load().penny_attention_prefill_variant(int(v)))
 

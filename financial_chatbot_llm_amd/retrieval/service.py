@@ -13,6 +13,7 @@ from typing import List, Optional, Sequence, Tuple
 
 from ..utils.logging import get_logger
 from ..utils.metrics import METRICS, now
+from ..utils.profiling import marker
 from .store import Hit
 
 logger = get_logger(__name__)
@@ -30,7 +31,7 @@ class RetrievalService:
     # -- synchronous core --------------------------------------------------------------
     def run_batch(self, queries: Sequence[str], user_ids: Sequence[str],
                   date_gte: Sequence[Optional[int]], limits: Sequence[int]) -> List[List[Hit]]:
-        with self._lock:
+        with self._lock, marker("retrieval.batch"):
             t0 = now()
             ctx = self._stream_ctx()
             with ctx:

@@ -1,0 +1,23 @@
+#!/bin/bash
+# r5 session 7: prefill-attention GPU tests after the variant-0 removal, then the driver bench under
+# rocprofv3 --kernel-trace --marker-trace with the engine's roctx ranges (PENNY_MARKERS=1): every GPU
+# idle gap >= 100 us attributed to what the engine / serving / retrieval threads were doing.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+stop_if_bad() { case "$1" in 124|134|137|139) echo "stopping after rc=$1"; exit "$1";; esac; }
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 240 --timeout-method thread \
+    tests/test_kernels_gpu.py -k "prefill" > gpurun_out/r5_s7_gpu_tests.txt 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/r5_s7_gpu_tests.txt; stop_if_bad $rc
+[ $rc -eq 0 ] || exit $rc
+export PENNY_MARKERS=1
+timeout -k 10 480 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d /tmp/prof -o run -- \
+    python3 bench.py --steps 20 --warmup 5 > gpurun_out/r5_s7_prof_bench.json 2> gpurun_out/r5_s7_prof_bench.err
+rc=$?; stop_if_bad $rc
+unset PENNY_MARKERS
+st=$(find /tmp/prof -name '*kernel_stats.csv' | head -1); tr=$(find /tmp/prof -name '*kernel_trace.csv' | head -1)
+mk=$(find /tmp/prof -name '*marker_api_trace.csv' | head -1)
+ls -la /tmp/prof/* > gpurun_out/r5_s7_prof_files.txt 2>&1
+head -5 "$mk" > gpurun_out/r5_s7_marker_head.csv
+python3 -m financial_chatbot_llm_amd.bench.profsum "$st" --trace "$tr" --markers "$mk" --title "r5 driver bench 20x5: GPU idle gaps by host roctx range" > gpurun_out/r5_s7_prof_kernel_stats.md 2>&1
+rm -rf /tmp/prof

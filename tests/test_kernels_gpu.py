@@ -130,7 +130,7 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 4, 5, 6])
+@pytest.mark.parametrize("variant", [4, 5, 6])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
     # respond chunk behind a cached prefix + decide-like and spec-like chunks (dead waves: 17 x 4 rows)
     (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
@@ -139,7 +139,7 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     (12, 12, 64, False, [(200, 200), (33, 33)], 1.0),         # bidirectional, D = 64
 ])
 def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, qscale):
-    """prefill2 (0), prefill2 with pinned fragment prefetch (4), its VALU-lean softmax (5: ones-MFMA
+    """prefill2 with pinned fragment prefetch (4), its VALU-lean softmax (5: ones-MFMA
     row sums, lean max / grow logic) and 5 with prescaled Q and -m accumulator starts (6) vs the fp32
     reference, with the LPT work list and without (also the lse output)."""
     g = torch.Generator().manual_seed(40 + variant)
@@ -169,7 +169,7 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
         ops.attention.prefill_variant(old)
 
 
-@pytest.mark.parametrize("variant", [0, 4, 5, 6])
+@pytest.mark.parametrize("variant", [4, 5, 6])
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
     (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
