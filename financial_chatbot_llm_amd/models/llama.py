@@ -26,7 +26,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.dist import state as pstate
-from ..ops.attention import _side_stream
+from ..ops.attention import _side_stream, fork_join_events
 
 _DUAL_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
@@ -233,17 +233,22 @@ class DecoderModel:
             # mixed step: the decode rows' attention (HBM-bound: streams their whole contexts) runs on
             # a side stream CONCURRENTLY with the prefill rows' attention (MFMA-bound) -- the two read
             # disjoint sequences' KV and write disjoint rows of attn; joined before the O projection
+            # (reused fork / join events, the raw side stream passed to the launch: no per-layer event
+            # creation or current-stream switching on the host)
             side = _side_stream(q.device)
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
-                           workspace=meta.decode_ws, out=attn[tp:])
+            main = torch.cuda.current_stream()
+            ev_fork, ev_join = fork_join_events(q.device)
+            ev_fork.record(main)
+            side.wait_event(ev_fork)
+            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
+                       workspace=meta.decode_ws, out=attn[tp:], stream=side.cuda_stream)
         if tp > 0:
             ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, self.scale,
                         causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp], work=meta.prefill_work,
                         lean=meta.prefill_lean)
         if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
+            ev_join.record(side)
+            main.wait_event(ev_join)
         elif meta.num_decode > 0:
             ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
                        workspace=meta.decode_ws, out=attn[tp:])

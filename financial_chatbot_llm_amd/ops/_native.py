@@ -116,12 +116,17 @@ def available() -> bool:
         return False
 
 
+_FORCE_TORCH_OPS = os.environ.get("PENNY_FORCE_TORCH_OPS") == "1"   # read once: checked on every op
+
+
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
 def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """The current HIP stream of the current device, raw (two C calls: ``torch.cuda.current_stream``
+    costs ~7 us of Python per call, and every kernel launch asks)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def call(name: str, *args) -> None:
@@ -132,8 +137,4 @@ def call(name: str, *args) -> None:
 
 def use_native(t: torch.Tensor) -> bool:
     """True -> run the HIP kernel.  CPU tensors use the torch reference path."""
-    if t.device.type != "cuda":
-        return False
-    if os.environ.get("PENNY_FORCE_TORCH_OPS") == "1":
-        return False
-    return True
+    return t.device.type == "cuda" and not _FORCE_TORCH_OPS

@@ -419,12 +419,26 @@ def _side_stream(device) -> "torch.cuda.Stream":
     return _SIDE_STREAMS[key]
 
 
+_FORK_EVENTS: Dict[int, Tuple["torch.cuda.Event", "torch.cuda.Event"]] = {}
+
+
+def fork_join_events(device) -> Tuple["torch.cuda.Event", "torch.cuda.Event"]:
+    """Two reusable events per device for a main -> side -> main fork/join (``Stream.wait_stream``
+    creates a fresh event per call: ~30 us of HIP event creation + record, 64 times a mixed step).
+    Re-recording is safe: a wait enqueued earlier keeps the record it saw."""
+    key = torch.device(device).index
+    if key not in _FORK_EVENTS:
+        _FORK_EVENTS[key] = (torch.cuda.Event(disable_timing=True), torch.cuda.Event(disable_timing=True))
+    return _FORK_EVENTS[key]
+
+
 def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, k_cache: torch.Tensor,
            v_cache: torch.Tensor, scale: float, workspace: Optional[DecodeWorkspace] = None,
-           max_ctx: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           max_ctx: Optional[int] = None, out: Optional[torch.Tensor] = None,
+           stream: Optional[int] = None) -> torch.Tensor:
     """One query token per sequence against its paged context: the work-balanced split-K kernel
     (``decode_lean_kernel``) by default, the per-(row, head, partition) kernel with
-    ``PENNY_DECODE_LEAN=0``."""
+    ``PENNY_DECODE_LEAN=0``.  ``stream``: raw HIP stream to launch on (default: the current one)."""
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     if N.use_native(q):
@@ -442,7 +456,7 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
                 nparts, ws.part_stride, float(scale)]
         lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE)
                      if lean else (0, None, 1, 0))
-        N.call("penny_attention_decode", *args, *lean_args, N.stream())
+        N.call("penny_attention_decode", *args, *lean_args, N.stream() if stream is None else stream)
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()
