@@ -428,7 +428,7 @@ def fork_join_events(device) -> Tuple["torch.cuda.Event", "torch.cuda.Event"]:
     Re-recording is safe: a wait enqueued earlier keeps the record it saw."""
     key = torch.device(device).index
     if key not in _FORK_EVENTS:
-        _FORK_EVENTS[key] = (torch.cuda.Event(disable_timing=True), torch.cuda.Event(disable_timing=True))
+        _FORK_EVENTS[key] = (torch.cuda.Event(), torch.cuda.Event())   # enable_timing=False: no timestamps
     return _FORK_EVENTS[key]
 
 
