@@ -251,6 +251,7 @@ async def run(args, ps):
             "gpu_step_s": round(gpu_step, 2), "gpu_busy_frac": round(gpu_step / max(elapsed, 1e-9), 3),
             "gpu_idle_between_steps_s": round(stats.get("gpu_idle_between_steps_s", 0.0)
                                               - stats0.get("gpu_idle_between_steps_s", 0.0), 3),
+            "max_rss_gib": round(ru1.ru_maxrss / 2**20, 2),      # host memory high-water mark (ru_maxrss is KiB)
             "custom_all_reduce": dict(comm.AR_STATUS) if args.tp > 1 else None}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
             "host": host,
