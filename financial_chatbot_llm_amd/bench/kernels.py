@@ -831,9 +831,10 @@ def bench_gemm_hip(dev, Ms=None) -> List[Dict]:
     return out
 
 
-def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
-    """Each Llama-3-8B projection WITH its consumer, as the decoder layer runs it at a prefill
-    step of M rows, under every available choice (microseconds; same random operands):
+def bench_prefill_policy(dev, Ms=None, model: str = "8b") -> List[Dict]:
+    """Each Llama-3-8B (``model="70b"``: Llama-3-70B at TP=1) projection WITH its consumer, as the
+    decoder layer runs it at a prefill step of M rows, under every available choice (microseconds;
+    same random operands):
       qkv:     hipBLASLt + rope_kv_write | fused QKV+RoPE+KV-write tile kernel
       o, down: hipBLASLt + add&RMSNorm   | tile kernel bf16 + add&RMSNorm | split-K S slabs + slab RMSNorm
                | tile kernel adding the residual in place + RMSNorm (hipR)
@@ -843,9 +844,10 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
     from ..ops.activation import silu_mul
     from ..ops.attention import rope_cos_sin, rope_kv_write
     out = []
-    H, F_, Hq, Hkv = 4096, 14336, 32, 8
+    H, F_, Hq, Hkv = (8192, 28672, 64, 8) if model == "70b" else (4096, 14336, 32, 8)
+    NQ = (Hq + 2 * Hkv) * 128
     rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
-    w = {"qkv": rnd(6144, H), "o": rnd(H, H), "gate_up": rnd(2 * F_, H), "down": rnd(H, F_)}
+    w = {"qkv": rnd(NQ, H), "o": rnd(H, Hq * 128), "gate_up": rnd(2 * F_, H), "down": rnd(H, F_)}
     nw = torch.ones(H, dtype=torch.bfloat16, device=dev)
     cs = rope_cos_sin(128, 8192, 500000.0, device=dev)
     Ms = Ms or [256 * k for k in range(1, 17)]
@@ -853,7 +855,7 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
     kc = torch.zeros((nb, Hkv, 64 * 128), dtype=torch.bfloat16, device=dev)
     vc = torch.zeros_like(kc)
     for M in Ms:
-        row = {"op": "prefill_policy", "M": M}
+        row = {"op": "prefill_policy", "model": model, "M": M}
         x = rnd(M, H)
         xf = rnd(M, F_)
         res = rnd(M, H)
@@ -864,7 +866,7 @@ def bench_prefill_policy(dev, Ms=None) -> List[Dict]:
                                                Hq, Hkv, 128)
         fns["qkv_fused"] = lambda: gemm.prefill_qkv_rope(x, w["qkv"], pos, cs, slots, kc, vc, Hq, Hkv)
         for S in (2, 4):   # split-K slabs summed by the RoPE / KV-write pass
-            Pq = torch.empty((S, M, 6144), dtype=torch.float32, device=dev)
+            Pq = torch.empty((S, M, NQ), dtype=torch.float32, device=dev)
             fns[f"qkv_hipS{S}"] = (lambda S=S, Pq=Pq: rope_kv_write(gemm.Slabs(gemm.prefill_gemm(
                 x, w["qkv"], "slabs", S, out=Pq)), pos, cs, slots, kc, vc, Hq, Hkv, 128))
         for name, a in (("o", x), ("down", xf)):
@@ -1191,7 +1193,7 @@ def main(argv=None) -> int:
                 "topk": bench_topk, "gemm": bench_gemm, "gemm_prefill": bench_gemm_prefill, "lm_head": bench_lm_head, "lm_head_fused": bench_lm_head_fused, "bge_query": bench_bge_query, "gemm_tail": bench_gemm_tail,
                 "gemm_tune": bench_gemm_tune_sweep, "skinny": bench_skinny, "splitk": bench_splitk,
                 "splitk_qkv": lambda d: bench_splitk(d, ("qkv",)), "gateup": bench_gateup, "moe": bench_moe,
-                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]),
+                "moe_prefill": bench_moe_prefill, "gemm_hip": bench_gemm_hip, "gemm_hip_quick": lambda d: bench_gemm_hip(d, [512, 1024, 2048, 3072, 4096]), "gemm_hip_check": check_gemm_hip, "gemm_lds_probe": gemm_lds_probe, "prefill_policy": bench_prefill_policy, "prefill_policy_quick": lambda d: bench_prefill_policy(d, [512, 1024, 1536, 2048, 2560, 3072, 3584, 4096]), "prefill_policy_70b": lambda d: bench_prefill_policy(d, [384, 512, 768, 1024, 1536, 2048, 2560, 3072, 4096], model="70b"),
                 "prefill_policy_small": lambda d: bench_prefill_policy(d, [512, 768, 1024, 1280, 1536]), "gemm_ablate": bench_gemm_ablate,
                 "splitk70b": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B),
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
