@@ -651,12 +651,6 @@ __global__ void decode_reduce_kernel(const int* __restrict__ ctx_lens, const flo
 // `out` (no partial, no merge).  The plan (per-row prefix sums, units per wave) is recomputed by
 // every workgroup from ctx_lens (device data: hipGraph-capturable), and workgroup 0
 // publishes it in `meta` for the merge kernel.
-// FUSED merge (static chunks): a wave that wrote a partial of row b releases it (agent-scope fence)
-// and draws a ticket from the (row, kv head) counter; the wave drawing the last of the row's
-// ceil-spanned writer count acquires, merges the row's partials in slot order (bitwise the same
-// result whichever wave merges) straight into `out` and re-zeroes the counter -- no second launch
-// (the separate merge kernel cost 11 us per call plus its launch gap, 1.1 % of the driver config's
-// GPU time).  No wave ever waits on another.
 constexpr int LEAN_MAX_B = 1024;
 
 struct LeanPlan {
@@ -716,39 +710,13 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
 // in mixed steps -- simply take fewer chunks.  Either way a chunk's partial slots depend only on
 // its index, and the merge kernel re-zeroes the counters for the next launch.
 constexpr int LEAN_META0 = 64;   // meta[0..64): per-head chunk counters; plan from meta[64]
-// fused-merge tickets: meta[LEAN_TICKET0 + b * Hkv + h] (zero between launches)
-constexpr int LEAN_TICKET0 = LEAN_META0 + LEAN_MAX_B + 2;
-
-// merge row b's partial slots [0, np) of kv head h (G q-heads) into out: one wave, 64 lanes x D/64 dims
-template <int D>
-__device__ __forceinline__ void lean_merge_row(const float* __restrict__ part_m, const float* __restrict__ part_l,
-                                               const float* __restrict__ part_o, bf16* __restrict__ out, int b,
-                                               int h, int G, int Hq, int part_stride, int np, int lane) {
-  for (int c = 0; c < G; ++c) {
-    const int hq = h * G + c;
-    const long base = ((long)b * Hq + hq) * part_stride;
-    float M = -INFINITY;
-    for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
-    float L = 0.f, O[D / 64];
-#pragma unroll
-    for (int e = 0; e < D / 64; ++e) O[e] = 0.f;
-    for (int i = 0; i < np; ++i) {
-      const float f = exp2f(part_m[base + i] - M);
-      L += part_l[base + i] * f;
-#pragma unroll
-      for (int e = 0; e < D / 64; ++e) O[e] += part_o[(base + i) * D + e * 64 + lane] * f;
-    }
-#pragma unroll
-    for (int e = 0; e < D / 64; ++e) out[((long)b * Hq + hq) * D + e * 64 + lane] = (bf16)(L > 0.f ? O[e] / L : 0.f);
-  }
-}
 
 template <int D>
 __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
     float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
-    int min_per_wave, int chunks_per_wave, int fused) {
+    int min_per_wave, int chunks_per_wave) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
@@ -885,22 +853,6 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
           part_m[pi] = m;
           part_l[pi] = l;
         }
-      }
-    }
-    if (fused && !(k0 == 0 && k1 == n)) {
-      // publish this partial; the row's last writer merges (wave-uniform branch)
-      const int np = (seg0 + n - 1) / pl.per_wave - seg0 / pl.per_wave + 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      int old = 0;
-      if (lane == 0)
-        old = __hip_atomic_fetch_add(meta + LEAN_TICKET0 + b * Hkv + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (old == np - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (lane == 0)
-          __hip_atomic_store(meta + LEAN_TICKET0 + b * Hkv + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lean_merge_row<D>(part_m, part_l, part_o, out, b, h, G, Hq, part_stride, np, lane);
       }
     }
     u = seg0 + k1;
@@ -1288,8 +1240,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
                                      int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts,
                                      int part_stride, float scale, int lean_grid, int* lean_meta,
-                                     int lean_min_per_wave, int lean_chunks_per_wave, int lean_fused_merge,
-                                     hipStream_t stream) {
+                                     int lean_min_per_wave, int lean_chunks_per_wave, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
   // lean_grid > 0: the work-balanced kernel (decode_lean_kernel) and its merge; otherwise the
@@ -1298,9 +1249,6 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv ||
                Hkv > LEAN_META0 || lean_chunks_per_wave < 0))
     return (int)hipErrorInvalidValue;
-  // fused merge (static chunks only: the dynamic claim mode's counters are re-zeroed by the merge
-  // kernel); lean_meta then spans LEAN_TICKET0 + B * Hkv ints (ops/attention.py DecodeWorkspace)
-  const bool fused = lean && lean_fused_merge && lean_chunks_per_wave == 0;
   // measured (profiles/r1_decode_head_fast.txt): head-fastest wins at B <= 16 (18.5 vs 21.6 us at
   // ctx 2048 / 1024 shared), sequence-fastest at B >= 64 (a sequence's 8 heads of a KV block are
   // one contiguous 128 KB run, read by one XCD); PENNY_DECODE_HEAD_FAST=0/1 forces either
@@ -1316,10 +1264,9 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
     hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
                        part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride, lean_min_per_wave,   \
-                       lean_chunks_per_wave, (int)fused);                                                        \
-    if (!fused)                                                                                                 \
-      hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m,       \
-                         part_l, part_o, (bf16*)out, B, Hq, Hkv, part_stride);                                   \
+                       lean_chunks_per_wave);                                                                    \
+    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
+                       part_o, (bf16*)out, B, Hq, Hkv, part_stride);                                             \
   } else {                                                                                                      \
     if (head_fast)                                                                                              \
       hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens,          \

@@ -357,7 +357,7 @@ class DecodeWorkspace:
     pb: int
     nparts: int
     part_stride: int = 0    # partition slots per (row, head)
-    lean_meta: Optional[torch.Tensor] = None   # int32: chunk counters | lean plan | fused-merge tickets
+    lean_meta: Optional[torch.Tensor] = None   # [64 + max_batch + 2] int32: chunk counters + lean plan
 
     def partitioning(self, B: int):
         """(pb, nparts) for a decode batch of B rows.  Batches of 32+ rows already fill the chip
@@ -383,7 +383,7 @@ class DecodeWorkspace:
         f = dict(dtype=torch.float32, device=device)
         return cls(torch.empty((max_batch, Hq, stride), **f), torch.empty((max_batch, Hq, stride), **f),
                    torch.empty((max_batch, Hq, stride, D), **f), pb, max(nparts, 2), stride,
-                   torch.zeros(LEAN_TICKET0 + max_batch * Hq, dtype=torch.int32, device=device))
+                   torch.zeros(LEAN_META0 + max_batch + 2, dtype=torch.int32, device=device))
 
 
 _SIDE_STREAMS = {}
@@ -401,11 +401,6 @@ LEAN_MIN_PER_WAVE = 2
 # a prefill (profiles/r3_decode_lean_vs_partitioned.jsonl)
 LEAN_CHUNKS_PER_WAVE = int(os.environ.get("PENNY_DECODE_LEAN_CHUNKS", "0"))
 LEAN_META0 = 64             # lean_meta[0:64] per-head chunk counters (attention.hip LEAN_META0)
-LEAN_MAX_B = 1024
-LEAN_TICKET0 = LEAN_META0 + LEAN_MAX_B + 2   # fused-merge (row, kv head) tickets (attention.hip)
-# the lean kernel's last writer of a row merges its partials (no separate merge launch);
-# PENNY_DECODE_LEAN_FUSED=0 restores the merge kernel (A/B)
-LEAN_FUSED_MERGE = os.environ.get("PENNY_DECODE_LEAN_FUSED", "1") != "0"
 _CU_COUNT = {}
 
 
@@ -459,9 +454,8 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale)]
-        fused = int(LEAN_FUSED_MERGE and ws.lean_meta.numel() >= LEAN_TICKET0 + B * Hkv) if lean else 0
-        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE, fused)
-                     if lean else (0, None, 1, 0, 0))
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE)
+                     if lean else (0, None, 1, 0))
         N.call("penny_attention_decode", *args, *lean_args, N.stream() if stream is None else stream)
         return out
     out = torch.empty_like(q) if out is None else out

@@ -567,37 +567,6 @@ def test_shared_prefix_decode_matches_reference(D, Hq, Hkv, lean, monkeypatch):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv,B", [(128, 32, 8, 96), (128, 32, 8, 7), (64, 8, 4, 40)])
-def test_lean_decode_fused_merge_equals_merge_kernel(D, Hq, Hkv, B, monkeypatch):
-    """The lean kernel's in-kernel merge (the last writer of a row merges its partials, ticketed)
-    equals the separate merge kernel bit for bit, leaves its tickets at zero (a second launch is
-    identical), and matches the fp32 reference; rows split over 1..several waves and rows one wave
-    covers whole are both present (contexts 1..4k)."""
-    g = torch.Generator().manual_seed(31 + B)
-    W = 64
-    ctx = torch.randint(1, W * KV_BS, (B,), generator=g, dtype=torch.int32)
-    ctx[0] = W * KV_BS
-    nb = B * W + 1
-    tables = torch.randperm(nb - 1, generator=g)[:B * W].view(B, W).to(torch.int32)
-    kc, vc = rnd(nb, Hkv, KV_BS * D, gen=g), rnd(nb, Hkv, KV_BS * D, gen=g)
-    q = rnd(B, Hq, D, gen=g)
-    scale = 1 / math.sqrt(D)
-    ws = ops.DecodeWorkspace.create(B, Hq, D, W * KV_BS, DEV)
-    args = (q.to(DEV), ctx.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale)
-    monkeypatch.setattr(ops.attention, "DECODE_LEAN", True)
-    monkeypatch.setattr(ops.attention, "LEAN_FUSED_MERGE", False)
-    sep = ops.decode(*args, workspace=ws).clone()
-    monkeypatch.setattr(ops.attention, "LEAN_FUSED_MERGE", True)
-    fused = ops.decode(*args, workspace=ws).clone()
-    again = ops.decode(*args, workspace=ws).clone()
-    torch.cuda.synchronize()
-    assert torch.equal(fused, sep)
-    assert torch.equal(again, fused)
-    t0 = ops.attention.LEAN_TICKET0
-    assert int(ws.lean_meta[t0:t0 + B * Hkv].abs().sum()) == 0
-    close(fused, ops.decode(q, ctx, tables, kc, vc, scale), atol=2e-2)
-
-
 def _kept_ref(lg, k, p, t):
     m = ops.apply_top_k_top_p(lg[None].float(), torch.tensor([k]), torch.tensor([p]), torch.tensor([t]))[0]
     return torch.isfinite(m)
