@@ -410,12 +410,17 @@ PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
     (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
     (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down
-    # Llama-3-70B (r5, profiles/r5_shard_shapes_v1_ring8.jsonl "shard_shapes_prefill" rows: each
-    # projection's kernels vs hipBLASLt at M = 384..4096, interleaved).  TP=1:
-    (10240, 8192): [(512, "lib"), (1 << 30, "fused")],                                   # QKV
-    (8192, 8192): [(384, "lib"), (512, "S4"), (1024, "S2"), (1 << 30, "lib")],           # O
+    # Llama-3-70B TP=1 (r5): each projection WITH its consumer (RoPE/KV write, add&RMSNorm, SiLU),
+    # interleaved, M = 384..4096 (bench/kernels.py --only prefill_policy_70b,
+    # profiles/r5_prefill_policy_70b_tp1_with_consumers.jsonl).  The hand-written choice is taken
+    # wherever it is within ~8 % of hipBLASLt (O with the residual epilogue: 2-5 % behind at
+    # 1.5-4k rows; down S2 / S4: 7 % behind at 768 / 1536 rows); the library keeps QKV at <= 384
+    # and 1024 rows (13-18 % ahead) and gate|up to 768 rows (7-16 % ahead: 2 row tiles x 224
+    # columns leave the 256x256 tile's tail round mostly idle)
+    (10240, 8192): [(384, "lib"), (768, "S2"), (1024, "lib"), (1 << 30, "fused")],       # QKV
+    (8192, 8192): [(512, "S4"), (1024, "S2"), (1 << 30, "R")],                           # O
     (57344, 8192): [(768, "lib"), (1 << 30, "hip")],                                     # gate|up
-    (8192, 28672): [(512, "S4"), (768, "lib"), (1024, "S2"), (1536, "S4"), (1 << 30, "hip")],   # down
+    (8192, 28672): [(512, "S4"), (768, "S2"), (1024, "hip"), (1536, "S4"), (1 << 30, "R")],   # down
     # TP=8 per-rank shards: the 256x256 tile underfills the CUs at these N up to ~1.5-2k rows (5 / 28
     # / 32 column tiles), so the library keeps those; the tile kernel where it measured ahead
     (1280, 8192): [(1536, "lib"), (3072, "S4"), (1 << 30, "S2")],                        # QKV shard
