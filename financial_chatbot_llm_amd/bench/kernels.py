@@ -1028,6 +1028,7 @@ SHARD_SHAPES = {
     "70b_tp8_gate_up": (7168, 8192, "gateup"), "70b_tp8_down": (8192, 3584, "row"),
     "70b_tp1_qkv": (10240, 8192, "col"), "70b_tp1_gate_up": (57344, 8192, "gateup"),
     "70b_tp1_o": (8192, 8192, "col"), "70b_tp1_down": (8192, 28672, "col"),
+    "8b_gate_up": (28672, 4096, "gateup"),     # the 8B shape above the fused kernel's 160 rows
 }
 
 
@@ -1065,6 +1066,17 @@ def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)
                     if N % (16 * nf) == 0:
                         fns[f"gu_nf{nf}_tiled"] = lambda nf=nf: gemm.gateup_silu(x, wts[nxt()], N, nf)
                         fns[f"gu_nf{nf}_rm"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=True)
+                # split-K slabs + the reduce-SiLU pass (gemm.gateup_splitk)
+                for S in (2, 4, 8):
+                    for nf in (2, 4, 8):
+                        if K % (64 * S) or N % (32 * nf):
+                            continue
+                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                        y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
+                        fns[f"guS{S}nf{nf}_rm"] = (lambda S=S, nf=nf, P=P, y=y: gemm.gateup_splitk(
+                            x, ws[nxt()], N, S, nf, rowmajor=True, slabs=P, out=y))
+                        fns[f"guS{S}nf{nf}_tiled"] = (lambda S=S, nf=nf, P=P, y=y: gemm.gateup_splitk(
+                            x, wts[nxt()], N, S, nf, slabs=P, out=y))
             else:
                 fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
                 if kind == "row":
@@ -1202,7 +1214,7 @@ def main(argv=None) -> int:
                 "shard_shapes": bench_shard_shapes,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
-                "lm_head_stream": bench_lm_head_stream,
+                "lm_head_stream": bench_lm_head_stream, "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
                 "lm_head_stream_shard": lambda d: bench_lm_head_stream(d, V=16128, Ms=(1, 8, 32, 64, 127))}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)

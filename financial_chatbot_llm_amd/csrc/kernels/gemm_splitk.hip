@@ -476,6 +476,48 @@ PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, v
   return (int)hipErrorInvalidValue;
 }
 
+// Split-K gate|up: P [S, M, N] f32 slabs of the interleave16 gate|up projection (row group 2j = gate
+// features 16j..16j+15, 2j+1 = their up rows) -> Y [M, N/2] bf16 = silu(gate) * up with the SK_SILU
+// epilogue's roundings.  For gate|up shapes whose column tiles alone underfill the chip (Llama-3-70B
+// TP=8 shard: 7168 rows = 112 tiles at nf = 4) or whose weights stream row-major (70B TP=1: no tiled
+// copy), the K split fills the CUs and this pass adds S*8 B per output.  One thread per 8 outputs.
+__global__ void __launch_bounds__(256) splitk_reduce_silu_kernel(const float* __restrict__ P, int S, int M, int N,
+                                                                 bf16* __restrict__ Y, int ldy) {
+  const int F = N / 2;
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;  // index of 8 outputs
+  const long total8 = (long)M * F / 8;
+  if (i8 >= total8) return;
+  const int m = (int)(i8 / (F / 8));
+  const int f = (int)(i8 % (F / 8)) * 8;                 // 8 features of one 16-feature group
+  const int ng = (f >> 4) * 32 + (f & 15);               // gate column; up = ng + 16
+  float gt[8], up[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gt[j] = up[j] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const f32x4* pg = reinterpret_cast<const f32x4*>(P + ((long)s * M + m) * N + ng);
+    const f32x4* pu = reinterpret_cast<const f32x4*>(P + ((long)s * M + m) * N + ng + 16);
+    const f32x4 g0 = pg[0], g1 = pg[1], u0 = pu[0], u1 = pu[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gt[j] += g0[j], gt[4 + j] += g1[j], up[j] += u0[j], up[4 + j] += u1[j];
+  }
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float gb = (float)(bf16)gt[j], ub = (float)(bf16)up[j];
+    o[j] = (float)(bf16)(gb / (1.f + __expf(-gb))) * ub;
+  }
+  *reinterpret_cast<uint4*>(Y + (long)m * ldy + f) = pack8(o);
+}
+
+PENNY_API int penny_splitk_reduce_silu(const void* P, int S, int M, int N, void* Y, int ldy, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % 32 || ldy % 8 || S < 1) return (int)hipErrorInvalidValue;
+  const long total8 = (long)M * (N / 2) / 8;
+  hipLaunchKernelGGL(splitk_reduce_silu_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, stream,
+                     (const float*)P, S, M, N, (bf16*)Y, ldy);
+  return (int)hipGetLastError();
+}
+
 PENNY_API int penny_splitk_reduce(const void* P, int S, int M, int N, void* Y, int ldy, const void* R, int ldr,
                                   hipStream_t stream) {
   if (M <= 0) return 0;

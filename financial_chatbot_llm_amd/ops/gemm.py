@@ -114,9 +114,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
                 return splitk_bf16(x, ww, N_, nf, rowmajor=rm)
             return splitk_reduce(splitk_partials(x, ww, N_, S, nf, rowmajor=rm))
     if epilogue == "silu" and src is not None and residual is None:
-        nf = gateup_config(M, N_, K) if N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0 else None
+        ok = N.use_native(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0
+        nf = gateup_config(M, N_, K) if ok else None
         if nf is not None:
             return gateup_silu(x, src, N_, nf, rowmajor=rowmajor)
+        cfg = gateup_splitk_config(M, N_, K) if ok else None
+        if cfg is not None and (cfg[2] or not rowmajor):
+            S, nf, rm = cfg
+            return gateup_splitk(x, w if rm else src, N_, S, nf, rowmajor=rm)
     if skinny_ok(x, w, epilogue, wt):
         ntf, nw = _config(N_, K, epilogue)
         out_n = N_ // 2 if epilogue == "silu" else N_
@@ -256,7 +261,7 @@ def uses_tiled_weight(N_: int, K: int) -> bool:
         return False
     if os.environ.get("PENNY_SPLITK", "1") == "force":
         return True
-    return (N_, K) in SPLITK or (N_, K) in GATEUP
+    return (N_, K) in SPLITK or (N_, K) in GATEUP or any(not e[4] for e in GATEUP_SPLITK.get((N_, K), ()))
 
 
 def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
@@ -314,6 +319,38 @@ def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
     y = out if out is not None else torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
     N.call("penny_gateup_silu_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), y.stride(0), M, N_, nf,
            int(rowmajor), N.stream())
+    return y
+
+
+# (N, K) of the interleave16 gate|up weight -> [(min M, max M, S, nf, rowmajor), ...]: split-K slabs +
+# the reduce-SiLU pass (penny_splitk_reduce_silu) where the fused kernel's column tiles alone underfill
+# the chip or its weights stream row-major (Llama-3-70B: TP=8 shard, TP=1 without a tiled copy).
+# Filled from bench/kernels.py --only shard_shapes (guS* rows).
+GATEUP_SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int, int, bool]]] = {}
+
+
+def gateup_splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int, bool]]:
+    """(S, nf, rowmajor) for the split-K gate|up path at this shape, or None."""
+    if os.environ.get("PENNY_GATEUP", "1") == "0" or M > 256:
+        return None
+    for lo, hi, S, nf, rm in GATEUP_SPLITK.get((N_, K), ()):
+        if lo <= M <= hi and K % (64 * S) == 0 and N_ % (32 * nf) == 0:
+            return S, nf, rm
+    return None
+
+
+def gateup_splitk(x: torch.Tensor, w: torch.Tensor, N_: int, S: int, nf: int, rowmajor: bool = False,
+                  slabs: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) as split-K f32 slabs of the interleave16 gate|up weight (``w`` its
+    fragment-tiled copy, or the [N, K] weight with ``rowmajor``) + one reduce-SiLU pass -- the same
+    roundings as the fused kernel (gate / up rounded to bf16, SiLU in bf16, product rounded)."""
+    M, K = x.shape
+    P = splitk_partials(x, w, N_, S, nf, out=slabs, rowmajor=rowmajor)
+    if not N.use_native(x):
+        g = P.sum(0).to(torch.bfloat16)
+        return silu_mul(g, interleave16=True)
+    y = out if out is not None else torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
+    N.call("penny_splitk_reduce_silu", N.ptr(P), S, M, N_, N.ptr(y), y.stride(0), N.stream())
     return y
 
 

@@ -1295,6 +1295,26 @@ def test_gateup_silu_nf2_tp8_shard(M):
     close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
 
 
+@pytest.mark.parametrize("M,S,nf", [(1, 8, 4), (64, 4, 2), (160, 2, 8)])
+def test_gateup_splitk_reduce_silu_tp8_shard(M, S, nf):
+    """Split-K gate|up (slabs + the reduce-SiLU pass) on the Llama-3-70B TP=8 gate|up shard vs the
+    fp32 reference; row-major == tiled bitwise; the reduce pass equals silu_mul over the summed slabs."""
+    from financial_chatbot_llm_amd.ops import gemm
+    from financial_chatbot_llm_amd.ops.activation import silu_mul
+    g = torch.Generator().manual_seed(M + 7)
+    Fr, K = 3584, 8192
+    x = rnd(M, K, gen=g)
+    gate, up = rnd(Fr, K, scale=0.02, gen=g), rnd(Fr, K, scale=0.02, gen=g)
+    wi = gemm.interleave16(gate, up).to(DEV).contiguous()
+    y = gemm.gateup_splitk(x.to(DEV), wi, 2 * Fr, S, nf, rowmajor=True)
+    assert torch.equal(gemm.gateup_splitk(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, S, nf), y)
+    P = gemm.splitk_partials(x.to(DEV), wi, 2 * Fr, S, nf, rowmajor=True)
+    assert torch.equal(silu_mul(P.sum(0).to(torch.bfloat16), interleave16=True), y)
+    xd = x.to(DEV).float()
+    gf, uf = xd @ gate.to(DEV).float().t(), xd @ up.to(DEV).float().t()
+    close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
+
+
 @pytest.mark.parametrize("Vs", [16033, 1001])
 def test_sample_shard_any_width(Vs):
     """a vocab shard whose width is not a multiple of 8 (row stride V/tp) samples on the

@@ -117,6 +117,20 @@ def test_splitk_slabs_cpu_reference_and_consumers():
     assert torch.equal(r1, r2)
 
 
+def test_gateup_splitk_cpu_reference():
+    """CPU path of the split-K gate|up op: the SiLU*up of the summed slabs (interleave16 layout)."""
+    from financial_chatbot_llm_amd.ops import gemm
+    from financial_chatbot_llm_amd.ops.activation import silu_mul
+    g = torch.Generator().manual_seed(1)
+    gate, up = torch.randn(64, 256, generator=g).to(torch.bfloat16), torch.randn(64, 256, generator=g).to(torch.bfloat16)
+    wi = gemm.interleave16(gate, up)
+    x = torch.randn(5, 256, generator=g).to(torch.bfloat16)
+    y = gemm.gateup_splitk(x, wi, 128, 4, 2, rowmajor=True)
+    ref = silu_mul((x.float() @ wi.float().t()).to(torch.bfloat16), interleave16=True)
+    assert y.shape == (5, 64)
+    assert torch.allclose(y.float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_decode_gemm_dispatch_tables(monkeypatch):
     """Which decode kernel a projection shape gets, and whether it keeps a tiled weight copy."""
     from financial_chatbot_llm_amd.ops import gemm
