@@ -287,11 +287,9 @@ def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
 # profiles/r1_gateup_v1.jsonl): 1.4x at M <= 16, 1.22-1.35x at M = 32..96, 1.14x at M = 128; at
 # M >= 192 the 3-deep ring of the 256-token tile is MFMA/LDS-latency bound and the library wins.
 GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
-    (28672, 4096): [(1, 160, 8)],
-    # Llama-3-70B TP=8 gate|up shard (interleave16 of 2 x 3584 rows), fragment-tiled: 1.04-1.06x at
-    # M <= 16 (nf 4), 1.04-1.08x at M = 192-256 (nf 2, 224 workgroups); hipBLASLt + silu_mul ties or
-    # wins in between (profiles/r5_decode_v2.jsonl)
-    (7168, 8192): [(1, 16, 4), (176, 256, 2)],
+    # r5 re-measure (profiles/r5_gateup_shapes.jsonl): 1.5x at M <= 16, 1.2-1.3x at 32-128, and also
+    # ahead above 160 rows (1.15x at 192, 1.02x at 256)
+    (28672, 4096): [(1, 256, 8)],
 }
 
 
@@ -326,7 +324,14 @@ def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
 # the reduce-SiLU pass (penny_splitk_reduce_silu) where the fused kernel's column tiles alone underfill
 # the chip or its weights stream row-major (Llama-3-70B: TP=8 shard, TP=1 without a tiled copy).
 # Filled from bench/kernels.py --only shard_shapes (guS* rows).
-GATEUP_SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int, int, bool]]] = {}
+GATEUP_SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int, int, bool]]] = {
+    # Llama-3-70B TP=8 gate|up shard (interleave16 of 2 x 3584 rows), fragment-tiled: 1.26-1.48x
+    # hipBLASLt + silu_mul at every M = 1..256 (the fused kernel: 112 column tiles, 0.96-1.10x)
+    (7168, 8192): [(1, 64, 2, 4, False), (65, 256, 4, 8, False)],
+    # Llama-3-70B TP=1, row-major (no tiled copy: 75 GB): 1.23x at M = 1, 1.08x at 8, 1.04x at 16;
+    # hipBLASLt from 32 rows
+    (57344, 8192): [(1, 1, 8, 2, True), (2, 16, 4, 2, True)],
+}
 
 
 def gateup_splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int, bool]]:

@@ -137,7 +137,14 @@ def test_decode_gemm_dispatch_tables(monkeypatch):
     # Llama-3-8B: measured split-K / fused gate|up configs, tiled copies
     assert gemm.splitk_config(128, 6144, 4096) == (4, 6)
     assert gemm.splitk_config(300, 6144, 4096) is None              # prefill size: hipBLASLt
-    assert gemm.gateup_config(128, 28672, 4096) == 8 and gemm.gateup_config(200, 28672, 4096) is None
+    assert gemm.gateup_config(128, 28672, 4096) == 8 and gemm.gateup_config(200, 28672, 4096) == 8
+    assert gemm.gateup_config(300, 28672, 4096) is None
+    # 70B gate|up: split-K + reduce-SiLU (TP=8 shard tiled, TP=1 row-major at M <= 16 only)
+    assert gemm.gateup_splitk_config(64, 7168, 8192) == (2, 4, False)
+    assert gemm.gateup_splitk_config(200, 7168, 8192) == (4, 8, False)
+    assert gemm.gateup_splitk_config(1, 57344, 8192) == (8, 2, True)
+    assert gemm.gateup_splitk_config(32, 57344, 8192) is None
+    assert gemm.uses_tiled_weight(7168, 8192) and not gemm.uses_tiled_weight(57344, 8192)
     assert gemm.uses_tiled_weight(6144, 4096) and gemm.uses_tiled_weight(28672, 4096)
     # Llama-3-70B TP=1 (r5 re-measure): split-K on the row-major stream at every decode M, no copies
     assert gemm.splitk_config(32, 8192, 8192) == (8, 2) and gemm.splitk_config(128, 8192, 8192) == (8, 8)
