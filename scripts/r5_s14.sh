@@ -5,6 +5,11 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 stop_if_bad() { case "$1" in 124|134|137|139) echo "stopping after rc=$1"; exit "$1";; esac; }
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_world8_gpu.py tests/test_tp_gpu.py tests/test_kernels_gpu.py -k "world8 or tp or gateup or splitk" \
+    > gpurun_out/r5_s14_gpu_tests.txt 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/r5_s14_gpu_tests.txt; stop_if_bad $rc
+[ $rc -eq 0 ] || exit $rc
 export PENNY_MARKERS=1
 timeout -k 10 480 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d /tmp/prof -o run -- \
     python3 bench.py --steps 20 --warmup 5 > gpurun_out/r5_s14_prof_bench.json 2> gpurun_out/r5_s14_prof_bench.err
