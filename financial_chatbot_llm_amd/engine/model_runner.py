@@ -11,6 +11,7 @@ layers of a decode step become one launch, removing ~1.5 us x 300+ launch gaps p
 """
 from __future__ import annotations
 
+import itertools
 import math
 import os
 from dataclasses import dataclass
@@ -113,19 +114,38 @@ def sample_rows(seq, n: int) -> int:
     return max(1, min(seq.spec_rows, n))
 
 
+def _table(rows: List[List[int]]) -> np.ndarray:
+    """Ragged block tables -> zero-padded [len(rows), max len] int32, in one vectorised scatter."""
+    lens = np.fromiter((len(r) for r in rows), np.int64, len(rows))
+    w = max(int(lens.max()) if len(rows) else 1, 1)
+    out = np.zeros((len(rows), w), np.int32)
+    if len(rows):
+        flat = np.fromiter(itertools.chain.from_iterable(rows), np.int32, int(lens.sum()))
+        mask = np.arange(w)[None, :] < lens[:, None]
+        out[mask] = flat
+    return out
+
+
 def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
-    ids: List[int] = []
-    pos: List[int] = []
-    slots: List[int] = []
+    """The host arrays of one step.  Per-token work is numpy (a prefill step carries ~2-4k tokens:
+    a per-token Python list build cost ~1 ms of the host's critical path between GPU steps)."""
+    ids_parts: List[np.ndarray] = []
+    pos_parts: List[np.ndarray] = []
+    slot_parts: List[np.ndarray] = []
     cu = [0]
     ctx_p, tables_p = [], []
     logits_idx, temps, seeds, tk, tp = [], [], [], [], []
     max_q = 0
     for seq, start, n in batch.prefill:
-        all_ids = seq.all_ids
-        ids.extend(all_ids[start:start + n])
-        pos.extend(range(start, start + n))
-        slots.extend(_slots(seq, start, n))
+        np_ = len(seq.prompt_ids)
+        if start + n <= np_:
+            ids_parts.append(np.asarray(seq.prompt_ids[start:start + n], np.int32))
+        else:
+            ids_parts.append(np.asarray(seq.all_ids[start:start + n], np.int32))
+        p = np.arange(start, start + n, dtype=np.int32)
+        pos_parts.append(p)
+        bt = np.asarray(seq.block_table, np.int32)
+        slot_parts.append(bt[p // KV_BS] * KV_BS + p % KV_BS)
         cu.append(cu[-1] + n)
         ctx_p.append(start + n)
         tables_p.append(seq.block_table)
@@ -141,18 +161,19 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
                 tk.append(seq.params.top_k)
                 tp.append(seq.params.top_p)
     Tp = cu[-1]
+    ids_d, pos_d, slots_d = [], [], []
     ctx_d, tables_d, src = [], [], []
     for j, seq in enumerate(batch.decode):
         p = seq.num_tokens - 1
         if seq.pending_src >= 0:      # token sampled by the step still in flight: device gather
-            ids.append(0)
+            ids_d.append(0)
             src.append(seq.pending_src)
         else:
-            ids.append(seq.output_ids[-1] if seq.output_ids else seq.prompt_ids[-1])
+            ids_d.append(seq.output_ids[-1] if seq.output_ids else seq.prompt_ids[-1])
             src.append(-1)
-        pos.append(p)
-        slots.extend(_slots(seq, p, 1))
-        ctx_d.append(seq.num_tokens)
+        pos_d.append(p)
+        slots_d.append(seq.block_table[p // KV_BS] * KV_BS + p % KV_BS)
+        ctx_d.append(p + 1)
         tables_d.append(seq.block_table)
         logits_idx.append(Tp + j)
         temps.append(seq.params.temperature)
@@ -160,18 +181,13 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
         tk.append(seq.params.top_k)
         tp.append(seq.params.top_p)
 
-    def table(rows):
-        w = max((len(r) for r in rows), default=1) or 1
-        out = np.zeros((len(rows), w), np.int32)
-        for i, r in enumerate(rows):
-            out[i, :len(r)] = r
-        return out
-
     i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
+    cat = lambda parts, tail: np.concatenate(parts + [i32(tail)]) if parts else i32(tail)  # noqa: E731
     src_a = i32(src) if any(x >= 0 for x in src) else None
-    return StepInputs(i32(ids), i32(pos), i32(slots), i32(cu), i32(ctx_p), table(tables_p), max_q, i32(ctx_d),
-                      table(tables_d), np.asarray(logits_idx, np.int64), np.asarray(temps, np.float32),
-                      np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32), src_a)
+    return StepInputs(cat(ids_parts, ids_d), cat(pos_parts, pos_d), cat(slot_parts, slots_d), i32(cu), i32(ctx_p),
+                      _table(tables_p), max_q, i32(ctx_d), _table(tables_d), np.asarray(logits_idx, np.int64),
+                      np.asarray(temps, np.float32), np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32),
+                      src_a)
 
 
 class CollectiveTimeout(RuntimeError):
