@@ -1140,15 +1140,14 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   const PrefillLean lean{items, part_o, part_ml};
   const int var = prefill_variant();
   const dim3 grid(Hkv, nitems, 1);
-#define LEAN_LAUNCH(DD, PREF_, SB_, FOLD_, NB_)                                                                   \
-  hipLaunchKernelGGL((prefill2_kernel<DD, 8, NB_, true, PREF_, SB_, FOLD_>), grid, dim3(512), 0, stream,           \
+#define LEAN_LAUNCH(DD, PREF_, SB_, FOLD_)                                                                        \
+  hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, PREF_, SB_, FOLD_>), grid, dim3(512), 0, stream,             \
                      (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
                      (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
 #define LEAN_VARIANTS(DD)                                   \
-  if (var == 6) LEAN_LAUNCH(DD, true, true, 2, 3);          \
-  else if (var == 4) LEAN_LAUNCH(DD, true, true, 0, 3);     \
-  else if (var == 7) LEAN_LAUNCH(DD, true, true, 1, 4);     \
-  else LEAN_LAUNCH(DD, true, true, 1, 3);                   \
+  if (var == 6) LEAN_LAUNCH(DD, true, true, 2);             \
+  else if (var == 4) LEAN_LAUNCH(DD, true, true, 0);        \
+  else LEAN_LAUNCH(DD, true, true, 1);                      \
   if (nmerge > 0)                                           \
     hipLaunchKernelGGL(prefill_merge_kernel<DD>, dim3(nmerge, Hkv, 256 / (4 * (64 / (DD / 4)))), dim3(256), 0, stream, \
                        merge, cu_q, part_o, part_ml, (bf16*)out, lse, Hq, Hkv);
@@ -1216,10 +1215,6 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big && pp_env == 4)                                                                                   \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true>), grid2, dim3(512), 0, stream,               \
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big && pp_env == 7)                                                                                   \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 4, true, true, true, 1>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big)                                                                                                  \
