@@ -283,53 +283,6 @@ def bench_prefill_mixed(dev) -> List[Dict]:
     return out
 
 
-def bench_prefill_nw4(dev) -> List[Dict]:
-    """A/B on the workload's mixed-step shapes: prefill2 variant 5 as 8 waves x 256 rows (one
-    workgroup per CU, every SIMD's two waves behind one barrier) vs the same block code as 4 waves x
-    128 rows with two workgroups per CU (variant 8: a SIMD's two waves belong to different
-    workgroups, so their softmax / MFMA phases drift apart).  No work lists on either side (the
-    host lists are built for 256-row tiles); the production variant 5 with its LPT list as reference."""
-    out = []
-    g = torch.Generator(device=dev).manual_seed(2)
-    Hq, Hkv, D = 32, 8, 128
-    for name, shape in MIXED_STEPS.items():
-        tables, kc, vc = _paged_varlen(shape, Hkv, D, dev, g)
-        qlens = [q for q, _ in shape]
-        T = sum(qlens)
-        if max(qlens) * (Hq // Hkv) <= 128:
-            continue
-        q = torch.randn((T, Hq, D), generator=g, device=dev).to(torch.bfloat16)
-        cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=dev)
-        lens = torch.tensor([c for _, c in shape], dtype=torch.int32, device=dev)
-        o = torch.empty_like(q)
-        wl = ops.attention.prefill_work_list(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv)
-        wd = torch.from_numpy(wl).to(dev) if wl is not None else None
-
-        def run(v, work):
-            def f():
-                ops.attention.prefill_variant(v)
-                ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=work)
-            return f
-        fns = {"v5_lpt": run(5, wd), "v5_grid": run(5, None), "v8_nw4_grid": run(8, None)}
-        old = ops.attention.prefill_variant()
-        outs = {}
-        for k, f in fns.items():
-            f()
-            outs[k] = o.clone()
-        ts = interleaved(fns, rounds=7, iters=5)
-        ops.attention.prefill_variant(old)
-        keys = sum(ql * (c - ql) + ql * (ql + 1) / 2 for ql, c in shape)
-        flops = 4 * keys * Hq * D
-        row = {"op": "prefill_attn_nw4_ab", "step": name, "T": T}
-        for k in fns:
-            row[f"{k}_us"] = round(ts[k], 1)
-            row[f"{k}_TFLOPs"] = round(flops / ts[k] / 1e6, 1)
-            row[f"{k}_maxdiff_vs_v5"] = round(float((outs[k].float() - outs["v5_lpt"].float()).abs().max()), 5)
-        print(json.dumps(row), flush=True)
-        out.append(row)
-    return out
-
-
 def bench_prefill_spec_split(dev) -> List[Dict]:
     """Mixed steps with speculative chunks (9 query tokens behind 5k-token contexts): one launch of
     the 8-wave kernel over every sequence (LPT work list; a spec chunk's 36 rows fill one 256-row
@@ -1261,7 +1214,7 @@ def main(argv=None) -> int:
                 "shard_shapes": bench_shard_shapes,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
-                "lm_head_stream": bench_lm_head_stream, "prefill_nw4": bench_prefill_nw4, "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
+                "lm_head_stream": bench_lm_head_stream, "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
                 "lm_head_stream_shard": lambda d: bench_lm_head_stream(d, V=16128, Ms=(1, 8, 32, 64, 127))}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)

@@ -916,7 +916,7 @@ struct PrefillLean {
 };
 
 template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false, int FOLD = 0>
-__global__ void __launch_bounds__(NW * 64, 8 / NW) prefill2_kernel(
+__global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
@@ -1198,26 +1198,19 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   // 4-wave tile (a 256-row tile would be mostly padding)
   const bool big = (long)max_q_len * G > 128;
   const int pp_env = prefill_variant();
-  // variant 8 (A/B): 4-wave 128-row tiles of the same kernel, two workgroups per CU whose waves
-  // share each SIMD without sharing a barrier (K/V staged once per 128 rows, 2-deep ring)
-  const bool nw4 = big && pp_env == 8;
-  const int TQ = (big && !nw4 ? 256 : 128) / G;
+  const int TQ = (big ? 256 : 128) / G;
   const int ntiles = (max_q_len + TQ - 1) / TQ;
   // grid (Hkv, tiles, seqs): the kv head is the fastest workgroup index, so with round-robin dispatch
   // over the 8 XCDs each XCD owns one kv head (+5-47 % TF/s over tile-fastest,
   // profiles/r1_prefill_head_fast.txt: 457 -> 672 at 4 x 2048 causal, 687 -> 905 at 1 x 8192)
   // work list (big tiles only): one workgroup per real (sequence, tile), LPT order
-  const bool wl = big && !nw4 && work != nullptr && nwork > 0;
+  const bool wl = big && work != nullptr && nwork > 0;
   const dim3 grid(ntiles, Hkv, num_seqs);
   const dim3 grid2 = wl ? dim3(Hkv, nwork, 1) : dim3(Hkv, ntiles, num_seqs);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
   if (big && pp_env == 6)                                                                                        \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (nw4)                                                                                                  \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 4, 2, true, true, true, 1>), grid2, dim3(256), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big && pp_env == 4)                                                                                   \
