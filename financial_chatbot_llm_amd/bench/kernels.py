@@ -261,7 +261,7 @@ def bench_prefill_mixed(dev) -> List[Dict]:
                 ops.attention.prefill_variant(v)
                 ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
             return f
-        variants = {"pf2_sb": 4, "pf2_fold": 5, "pf2_fold_oldtail": 9, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
+        variants = {"pf2_sb": 4, "pf2_fold": 5, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
                     "pf2_fold_lean": "lean_5", "pf2_foldq_lean": "lean_6"}
         old = ops.attention.prefill_variant()
         outs = {}

@@ -78,21 +78,6 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// Two 4-dim groups of a lane's output row, lo = dims 16t + 4g .. +3 and hi = 16(t+1) + 4g .. +3 in
-// lane row g (= lane >> 4) -> the 8 CONSECUTIVE dims 16t + 8*(g>>1) + 16*(g&1) .. +7 of this lane
-// (v_permlane16_swap: odd lane rows of vdst <-> even lane rows of vsrc), as gemm_prefill.hip's pair16.
-__device__ __forceinline__ uint4 pair16(bf16x4 lo, bf16x4 hi) {
-  union {
-    bf16x4 v;
-    uint2 u;
-  } a, b;
-  a.v = lo;
-  b.v = hi;
-  const auto x = __builtin_amdgcn_permlane16_swap(a.u.x, b.u.x, false, false);
-  const auto y = __builtin_amdgcn_permlane16_swap(a.u.y, b.u.y, false, false);
-  return make_uint4(x[0], y[0], x[1], y[1]);
-}
-
 // ------------------------------------------------------------------------------------------
 // Prefill
 // ------------------------------------------------------------------------------------------
@@ -930,9 +915,7 @@ struct PrefillLean {
   float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
 };
 
-// TAIL (A/B of the two out-of-loop tweaks): bit 0 widened 16-B output stores, bit 1 static priority
-// of the younger wave half
-template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false, int FOLD = 0, int TAIL = 3>
+template <int D, int NW, int NBUF, bool HEAD_FAST, bool PREF = true, bool SB = false, int FOLD = 0>
 __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -1045,10 +1028,6 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
   const bool wave_live = wave_tok0 < qlen;
   const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
   const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
-  // the younger half of an 8-wave workgroup (waves 4-7, one per SIMD beside an older wave) loses VALU
-  // arbitration on every segment by age; one static priority raise evens it (guide T5, static form;
-  // readfirstlane keeps the condition scalar so only those waves execute the s_setprio)
-  if ((TAIL & 2) && NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int j = 0; j < nblk; ++j) {           // local block j = absolute block jb + j
     // my pieces of block j landed (younger blocks j+1.. may stay in flight), then publish
     if (j + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
@@ -1080,39 +1059,16 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
       }
       continue;
     }
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    if constexpr (!(TAIL & 1)) {
-      if (tok[ct] >= qlen) continue;
-      bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        bf16x4 v4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
-      }
-      if (lse != nullptr && g == 0)
-        lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
-      continue;
-    }
-    // 16-B stores: lane rows g, g^1 hold the same output row, so one permlane16 swap per dword turns
-    // two 4-dim groups (dt, dt+1) into 8 consecutive dims (pair16; computed with every lane active,
-    // stored under the row mask -- the store tail is issue-bound, cdna_hip_programming.md T21)
-    uint4 w16[DT / 2];
-#pragma unroll
-    for (int dt = 0; dt < DT; dt += 2) {
-      bf16x4 lo, hi;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        lo[r] = (bf16)(o[ct][dt][r] * inv);
-        hi[r] = (bf16)(o[ct][dt + 1][r] * inv);
-      }
-      w16[dt / 2] = pair16(lo, hi);
-    }
     if (tok[ct] >= qlen) continue;
-    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D + 8 * (g >> 1) + 16 * (g & 1);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    bf16* orow = out + ((long)(q0 + tok[ct]) * Hq + head[ct]) * D;
 #pragma unroll
-    for (int dt = 0; dt < DT; dt += 2) *reinterpret_cast<uint4*>(orow + 16 * dt) = w16[dt / 2];
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x4 v4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = v4;
+    }
     if (lse != nullptr && g == 0)
       lse[(long)(q0 + tok[ct]) * Hq + head[ct]] = lt > 0.f ? (m[ct] + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
   }
@@ -1255,10 +1211,6 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
 #define PREFILL_LAUNCH(DD)                                                                                       \
   if (big && pp_env == 6)                                                                                        \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
-                       (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
-                       (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
-  else if (big && pp_env == 9)                                                                                   \
-    hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 1, 0>), grid2, dim3(512), 0, stream,         \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \
   else if (big && pp_env == 4)                                                                                   \
