@@ -1029,6 +1029,8 @@ SHARD_SHAPES = {
     "70b_tp1_qkv": (10240, 8192, "col"), "70b_tp1_gate_up": (57344, 8192, "gateup"),
     "70b_tp1_o": (8192, 8192, "col"), "70b_tp1_down": (8192, 28672, "col"),
     "8b_gate_up": (28672, 4096, "gateup"),     # the 8B shape above the fused kernel's 160 rows
+    # the 8B decode projections (TP=1: slabs read by the consumer), re-swept at HEAD
+    "8b_qkv": (6144, 4096, "col"), "8b_o": (4096, 4096, "col"), "8b_down": (4096, 14336, "col"),
 }
 
 
@@ -1214,7 +1216,7 @@ def main(argv=None) -> int:
                 "shard_shapes": bench_shard_shapes,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
-                "lm_head_stream": bench_lm_head_stream, "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
+                "lm_head_stream": bench_lm_head_stream, "decode_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down"), Ms=(32, 64, 96, 128, 160, 192, 256), prefill_Ms=()), "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
                 "lm_head_stream_shard": lambda d: bench_lm_head_stream(d, V=16128, Ms=(1, 8, 32, 64, 127))}[name](dev)
     for r in res:
         print(json.dumps(r), flush=True)
