@@ -120,11 +120,37 @@ def _worker(rank, world, port, q, kind):
             os.environ.pop("PENNY_FUSED_LM_HEAD")
             out = (out, tok_fused, tok_shard, h.cpu())
         torch.cuda.synchronize()
-        q.put((rank, "OK", (logits.cpu() if rank == 0 else None, out, shard)))
+        # tensors go as bytes (_pack): a torch tensor in a multiprocessing queue is shared by file
+        # descriptor, which the parent can no longer open once this rank has exited
+        q.put((rank, "OK", _pack((logits.cpu() if rank == 0 else None, out, shard))))
         shutdown()
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, "ERR", traceback.format_exc()))
+
+
+def _pack(obj):
+    """Tensors -> ("__tensor__", dtype, shape, bytes), recursively through tuples / lists / dicts."""
+    if isinstance(obj, torch.Tensor):
+        t = obj.detach().cpu().contiguous()
+        return ("__tensor__", str(t.dtype), tuple(t.shape), t.view(torch.uint8).numpy().tobytes())
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_pack(x) for x in obj)
+    if isinstance(obj, dict):
+        return {k: _pack(v) for k, v in obj.items()}
+    return obj
+
+
+def _unpack(obj):
+    if isinstance(obj, tuple) and len(obj) == 4 and obj[0] == "__tensor__":
+        _, dt, shape, raw = obj
+        buf = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        return buf.view(getattr(torch, dt.split(".")[-1])).reshape(shape).clone()
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_unpack(x) for x in obj)
+    if isinstance(obj, dict):
+        return {k: _unpack(v) for k, v in obj.items()}
+    return obj
 
 
 def _spawn(kind):
@@ -146,7 +172,7 @@ def _spawn(kind):
                 p.kill()
     for r, (status, payload) in res.items():
         assert status == "OK", f"rank {r}: {payload}"
-    return {r: p for r, (s, p) in res.items()}
+    return {r: _unpack(p) for r, (s, p) in res.items()}
 
 
 def _assert_logits_close(got, ref):
