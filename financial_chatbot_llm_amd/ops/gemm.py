@@ -186,7 +186,7 @@ def load_gemm_tuning(model: str, tp: int = 1) -> Optional[str]:
 # (profiles/r1_splitk_v4_qkv.jsonl: the 96-row QKV tile beats 128 rows x 192 workgroups by 10 %).
 SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     (6144, 4096): [(256, 4, 6)],                             # QKV: 96-row tiles -> 256 workgroups
-    (4096, 4096): [(192, 4, 4)],                             # O (M=256: hipBLASLt is faster)
+    (4096, 4096): [(256, 4, 4)],                             # O (r5: S4 nf4 also ahead at M = 256, 23.4 vs 24.4 us)
     (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
     # Llama-3-70B (TP=1), streamed row-major (profiles/r1_splitk_70b.jsonl): down 1.2-1.9x hipBLASLt
     # at M = 32..256; O 1.1-1.5x from M = 96 (S = 0: the library is as fast below that)
