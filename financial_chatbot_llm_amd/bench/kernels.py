@@ -133,12 +133,12 @@ def bench_decode_lean(dev) -> List[Dict]:
         ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
         o = torch.empty_like(q)
 
-        def mk(lean, chunks=0):
+        def mk(lean):
             def f():
-                A.DECODE_LEAN, A.LEAN_CHUNKS_PER_WAVE = lean, chunks
+                A.DECODE_LEAN = lean
                 ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o)
             return f
-        fns = {"part": mk(False), "lean": mk(True, 0), "lean_dyn2": mk(True, 2), "lean_dyn4": mk(True, 4)}
+        fns = {"part": mk(False), "lean": mk(True)}
         ref = None
         errs = {}
         for k, f in fns.items():
@@ -165,9 +165,9 @@ def bench_decode_lean(dev) -> List[Dict]:
                 torch.cuda.current_stream().wait_stream(side)
             return g2
         tp = interleaved({"prefill_only": lambda: ops.prefill(pq, pcu, plens, ptab, pkc, pvc, 0.088, True, 512, out=po),
-                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean", "lean_dyn2", "lean_dyn4")}},
+                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean")}},
                          rounds=7, iters=20)
-        A.DECODE_LEAN, A.LEAN_CHUNKS_PER_WAVE = True, 0
+        A.DECODE_LEAN = True
         uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2
         logical = sum(ctxs) * Hkv * D * 2 * 2
         row = {"op": "decode_lean_ab", "B": B, "ctx_range": [lo, hi], "ctx_mean": round(sum(ctxs) / B),

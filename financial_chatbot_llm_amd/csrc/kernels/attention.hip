@@ -703,25 +703,22 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
 }
 
 // grid (nwg), nwg % Hkv == 0: workgroup i serves kv head i % Hkv with 4 waves.  A head's units
-// are cut into chunks of per_wave blocks.  Static (chunks_per_wave == 0): wave hw of the head owns
-// chunk hw.  Dynamic (chunks_per_wave = k > 0): chunks are k times smaller and each wave claims
-// the next one from the head's counter (meta[h], one vector atomic per chunk) until none is left,
-// so workgroups that start late -- the grid shares the chip with a concurrent prefill attention
-// in mixed steps -- simply take fewer chunks.  Either way a chunk's partial slots depend only on
-// its index, and the merge kernel re-zeroes the counters for the next launch.
-constexpr int LEAN_META0 = 64;   // meta[0..64): per-head chunk counters; plan from meta[64]
+// are cut into chunks of per_wave blocks and wave hw of the head owns chunk hw.  (A dynamic form --
+// smaller chunks claimed from a per-head atomic counter, for workgroups that start late beside a
+// concurrent prefill attention -- measured slower, the claim round trip costing more than it
+// balanced: 185 vs 140 us at B = 64, profiles/r3_decode_lean_vs_partitioned.jsonl; removed in r5.)
+constexpr int LEAN_META0 = 64;   // meta[LEAN_META0..]: the plan, published for the merge kernel
 
 template <int D>
 __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
-    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta, float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride,
-    int min_per_wave, int chunks_per_wave) {
+    float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta,
+    float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride, int min_per_wave) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
-  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, B, gridDim.x / Hkv * 4 * max(chunks_per_wave, 1),
-                                nparts, min_per_wave);
+  const LeanPlan pl = lean_plan(s_pre, s_w, ctx_lens, B, gridDim.x / Hkv * 4, nparts, min_per_wave);
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i <= B; i += 256) meta[LEAN_META0 + i] = s_pre[i];
     if (threadIdx.x == 0) meta[LEAN_META0 + B + 1] = pl.per_wave;
@@ -730,13 +727,8 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
   const int h = blockIdx.x % Hkv;
   const int G = Hq / Hkv;
   const int nch = (pl.total + pl.per_wave - 1) / pl.per_wave;
-  auto claim = [&]() {
-    int v = 0;
-    if (lane == 0) v = atomicAdd(meta + h, 1);
-    return __builtin_amdgcn_readfirstlane(v);
-  };
-  int chunk = chunks_per_wave > 0 ? claim() : (blockIdx.x / Hkv) * 4 + (threadIdx.x >> 6);
-  while (chunk < nch) {   // no barrier below this point
+  const int chunk = (blockIdx.x / Hkv) * 4 + (threadIdx.x >> 6);
+  if (chunk < nch) {   // no barrier below this point
   int u = chunk * pl.per_wave;
   const int uend = min(pl.total, u + pl.per_wave);
   // row of unit u: the last b with s_pre[b] <= u (skips empty rows)
@@ -860,17 +852,15 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
       ++b;
     } while (b < B - 1 && s_pre[b + 1] == s_pre[b]);
   }
-  chunk = chunks_per_wave > 0 ? claim() : nch;
   }
 }
 
 // grid (Hq, B), D threads: merges a row's lean partials, skipping rows one wave already finished
 template <int D>
-__global__ void decode_lean_reduce_kernel(int* __restrict__ meta, const float* __restrict__ part_m,
+__global__ void decode_lean_reduce_kernel(const int* __restrict__ meta, const float* __restrict__ part_m,
                                           const float* __restrict__ part_l, const float* __restrict__ part_o,
-                                          bf16* __restrict__ out, int B, int Hq, int Hkv, int part_stride) {
+                                          bf16* __restrict__ out, int B, int Hq, int part_stride) {
   const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
-  if (b == 0 && hq == 0 && d < Hkv) meta[d] = 0;   // chunk counters for the next launch
   const int pre = meta[LEAN_META0 + b], n = meta[LEAN_META0 + b + 1] - pre, pw = meta[LEAN_META0 + B + 1];
   int np = 0;
   if (n > 0) {
@@ -1240,14 +1230,14 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
                                      int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts,
                                      int part_stride, float scale, int lean_grid, int* lean_meta,
-                                     int lean_min_per_wave, int lean_chunks_per_wave, hipStream_t stream) {
+                                     int lean_min_per_wave, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
   // lean_grid > 0: the work-balanced kernel (decode_lean_kernel) and its merge; otherwise the
   // per-(row, head, partition) kernel, kept as the fallback (PENNY_DECODE_LEAN=0)
   const bool lean = lean_grid > 0;
   if (lean && (B > LEAN_MAX_B || nparts < 2 || !lean_meta || lean_min_per_wave < 1 || lean_grid % Hkv ||
-               Hkv > LEAN_META0 || lean_chunks_per_wave < 0))
+               Hkv > LEAN_META0))
     return (int)hipErrorInvalidValue;
   // measured (profiles/r1_decode_head_fast.txt): head-fastest wins at B <= 16 (18.5 vs 21.6 us at
   // ctx 2048 / 1024 shared), sequence-fastest at B >= 64 (a sequence's 8 heads of a KV block are
@@ -1263,10 +1253,9 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   if (lean) {                                                                                                   \
     hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
                        block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
-                       part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride, lean_min_per_wave,   \
-                       lean_chunks_per_wave);                                                                    \
+                       part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride, lean_min_per_wave); \
     hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
-                       part_o, (bf16*)out, B, Hq, Hkv, part_stride);                                             \
+                       part_o, (bf16*)out, B, Hq, part_stride);                                                  \
   } else {                                                                                                      \
     if (head_fast)                                                                                              \
       hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens,          \

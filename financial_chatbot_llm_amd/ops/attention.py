@@ -395,12 +395,7 @@ DECODE_LEAN = os.environ.get("PENNY_DECODE_LEAN", "1") != "0"
 LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
-# 0 (default): one static chunk per wave.  k > 0: chunks k times smaller claimed from a per-head
-# atomic counter -- meant to absorb a concurrent prefill attention holding CUs, but the claim
-# round trip costs more than it saves: 185 vs 140 us at B=64 alone, 279 vs 249 us concurrent with
-# a prefill (profiles/r3_decode_lean_vs_partitioned.jsonl)
-LEAN_CHUNKS_PER_WAVE = int(os.environ.get("PENNY_DECODE_LEAN_CHUNKS", "0"))
-LEAN_META0 = 64             # lean_meta[0:64] per-head chunk counters (attention.hip LEAN_META0)
+LEAN_META0 = 64             # lean_meta[64:]: the plan published for the merge (attention.hip LEAN_META0)
 _CU_COUNT = {}
 
 
@@ -454,8 +449,8 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale)]
-        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_CHUNKS_PER_WAVE)
-                     if lean else (0, None, 1, 0))
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE)
+                     if lean else (0, None, 1))
         N.call("penny_attention_decode", *args, *lean_args, N.stream() if stream is None else stream)
         return out
     out = torch.empty_like(q) if out is None else out

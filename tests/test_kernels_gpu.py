@@ -247,10 +247,9 @@ def test_prefill_attention_late_max_spike_forces_rescale(variant, spike_block):
                                          # lean split: one long row among short ones, many rows
                                          (32, 8, [8000] + [70] * 40 + [3000, 1]),
                                          (32, 8, [(97 * i) % 500 + 1 for i in range(700)])])
-@pytest.mark.parametrize("lean,chunks", [(True, 0), (True, 2), (True, 5), (False, 0)])
-def test_decode_attention(Hq, Hkv, ctxs, lean, chunks, monkeypatch):
+@pytest.mark.parametrize("lean", [True, False])
+def test_decode_attention(Hq, Hkv, ctxs, lean, monkeypatch):
     monkeypatch.setattr(ops.attention, "DECODE_LEAN", lean)
-    monkeypatch.setattr(ops.attention, "LEAN_CHUNKS_PER_WAVE", chunks)
     g = torch.Generator().manual_seed(5)
     D = 128
     tables, kc, vc = _paged_setup(ctxs, Hkv, D, gen=g)
