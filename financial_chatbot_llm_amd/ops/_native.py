@@ -124,10 +124,17 @@ def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream() -> int:
     """The current HIP stream of the current device, raw (two C calls: ``torch.cuda.current_stream``
-    costs ~7 us of Python per call, and every kernel launch asks)."""
-    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+    costs ~7 us of Python per call, and every kernel launch asks); the public API where this torch
+    build lacks the private entry points."""
+    if _RAW_STREAM is not None and _CUR_DEVICE is not None:
+        return _RAW_STREAM(_CUR_DEVICE())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def call(name: str, *args) -> None:
