@@ -1034,6 +1034,81 @@ SHARD_SHAPES = {
 }
 
 
+def bench_rm_pair(dev, names=("70b_tp1_gate_up", "70b_tp1_qkv", "70b_tp1_o", "70b_tp1_down", "70b_tp8_o",
+                                "70b_tp8_down"), Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)) -> List[Dict]:
+    """Row-major decode streams with BK=64 stages issued singly vs in pairs (gemm.RM_PAIR: each W row's
+    two 128-B chunks back to back), per (S, nf) config, with the fragment-tiled stream and hipBLASLt
+    as references; interleaved per M, weights rotated over >= 768 MB.  The paired stream must be
+    bit-identical to the single one (same k order): checked per config."""
+    from ..ops import gemm
+    from ..ops.activation import silu_mul
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+
+    def paired(f):
+        def g():
+            gemm.RM_PAIR = True
+            try:
+                return f()
+            finally:
+                gemm.RM_PAIR = False
+        return g
+    for name in names:
+        N, K, kind = SHARD_SHAPES[name]
+        copies = max(2, min(16, (768 << 20) // (N * K * 2)))
+        ws = [rnd(N, K) for _ in range(copies)]
+        it = [0]
+
+        def nxt():
+            it[0] = (it[0] + 1) % copies
+            return it[0]
+        for M in Ms:
+            x = rnd(M, K)
+            fns = {}
+            if kind == "gateup":
+                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, ws[nxt()]), interleave16=True)
+                for nf in (4, 8):
+                    fns[f"gu_nf{nf}"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=True)
+                for S, nf in ((2, 2), (4, 2), (8, 2), (2, 8), (4, 8)):
+                    P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                    y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
+                    fns[f"guS{S}nf{nf}"] = (lambda S=S, nf=nf, P=P, y=y: gemm.gateup_splitk(
+                        x, ws[nxt()], N, S, nf, rowmajor=True, slabs=P, out=y))
+            elif kind == "row":
+                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
+                for nf in (2, 4, 8):
+                    fns[f"bf16_nf{nf}"] = lambda nf=nf: gemm.splitk_bf16(x, ws[nxt()], N, nf)
+            else:
+                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
+                for S in (1, 2, 4, 8):
+                    for nf in (2, 4, 8):
+                        if K % (128 * S) or N % (16 * nf) or (N // (16 * nf)) * S < 128:
+                            continue
+                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                        fns[f"S{S}nf{nf}"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
+                            x, ws[nxt()], N, S, nf, out=P, rowmajor=True))
+            same = {}
+            for k in [k for k in fns if k != "lib"]:
+                it[0] = copies - 1
+                a = fns[k]()
+                it[0] = copies - 1
+                b = paired(fns[k])()
+                same[k] = bool(torch.equal(a, b))
+                fns[k + "_p"] = paired(fns[k])
+            t = interleaved(fns, rounds=5, iters=copies)
+            single = min((k for k in t if k != "lib" and not k.endswith("_p")), key=lambda k: t[k])
+            pair = min((k for k in t if k.endswith("_p")), key=lambda k: t[k])
+            row = {"op": "rm_pair", "name": name, "N": N, "K": K, "kind": kind, "M": M,
+                   **{k: round(v, 1) for k, v in t.items()}, "best_single": single, "best_pair": pair,
+                   "pair_gain": round(t[single] / t[pair], 3), "pair_vs_lib": round(t["lib"] / t[pair], 3),
+                   "pair_GBps": round(N * K * 2 / t[pair] / 1e3, 1), "bit_identical": all(same.values())}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del ws
+        torch.cuda.empty_cache()
+    return out
+
+
 def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
                        prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
     """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
@@ -1213,7 +1288,7 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
                 "lm_head_stream": bench_lm_head_stream, "decode_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down"), Ms=(32, 64, 96, 128, 160, 192, 256), prefill_Ms=()), "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),

@@ -63,13 +63,17 @@ __device__ __forceinline__ int xswz(int r, int c) { return c ^ (r & 7) ^ ((r >> 
 // MAXB: ring depth cap -- 8 by default; 16 for the narrow configs (NF = 2-4 rows groups: 4-8 KiB of
 // W per stage) whose 8-stage ring keeps only 28-56 KiB in flight per CU.  Also capped so the counted
 // vmcnt ((NBUF - 2) * loads per stage) fits the 6-bit counter.
-template <int NF, int MT, int KB = 150, int MAXB = 8>
+// BKM: BK=64 stages issued (and waited for) in pairs -- a ring slot then holds BKM stages, so each
+// W row's consecutive 128-B chunks leave the CU back to back (row-major W: 256 contiguous bytes per
+// row per issue instead of 128 B one stage period apart)
+template <int NF, int MT, int KB = 150, int MAXB = 8, int BKM = 1>
 struct Ring {
-  static constexpr int SBYTES = (NF + MT) * 2 * 1024;
-  static constexpr int LOADS = (2 * NF + 2 * MT) / 4;
+  static constexpr int SBYTES = (NF + MT) * 2 * 1024 * BKM;
+  static constexpr int LOADS = (2 * NF + 2 * MT) / 4 * BKM;
   static constexpr int BY_LDS = KB * 1024 / SBYTES;
   static constexpr int BY_VM = 63 / LOADS + 2;
-  static constexpr int NBUF = BY_LDS < MAXB ? (BY_LDS < BY_VM ? BY_LDS : BY_VM) : (MAXB < BY_VM ? MAXB : BY_VM);
+  static constexpr int CAP = MAXB / BKM > 3 ? MAXB / BKM : 3;
+  static constexpr int NBUF = BY_LDS < CAP ? (BY_LDS < BY_VM ? BY_LDS : BY_VM) : (CAP < BY_VM ? CAP : BY_VM);
 };
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>)
@@ -143,7 +147,7 @@ __device__ __forceinline__ void stage_mma(const char* __restrict__ base, f32x4 (
 // whole 128-B lines and the fragment reads stay conflict-free.
 // RKB: LDS ring budget in KiB (150: one workgroup per CU; ~72: two co-resident workgroups, so one's
 // pipeline ramp overlaps the other's stream when a CU runs several tiles in sequence).
-template <int NF, int MT, int WA, int EPI = SK_SLAB, bool WROW = false, int RKB = 150, int MAXB = 8>
+template <int NF, int MT, int WA, int EPI = SK_SLAB, bool WROW = false, int RKB = 150, int MAXB = 8, int BKM = 1>
 __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restrict__ X, int ldx,
                                                              const bf16* __restrict__ Wt, int K,
                                                              float* __restrict__ P, int M, int N, int S,
@@ -155,7 +159,7 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
   constexpr int TW = MT / WB;   // token tiles per wave
   static_assert(NF % WA == 0 && MT % WB == 0, "wave split");
   static_assert(!SILU || FW % 2 == 0, "SiLU epilogue needs (gate, up) row-group pairs per wave");
-  constexpr int NBUF = Ring<NF, MT, RKB, MAXB>::NBUF;
+  constexpr int NBUF = Ring<NF, MT, RKB, MAXB, BKM>::NBUF;   // ring slots of BKM stages each
   static_assert(NBUF >= 3, "ring too shallow");
   constexpr int WBYTES = NF * 2 * 1024;        // W pieces of one BK=64 stage
   constexpr int XBYTES = MT * 2 * 1024;        // X pieces (16*MT rows x 128 B)
@@ -163,14 +167,15 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
   constexpr int PIECES = (2 * NF + 2 * MT);     // 1-KiB pieces per stage
   static_assert(PIECES % 4 == 0, "pieces must split evenly over 4 waves");
   constexpr int LOADS = PIECES / 4;             // glds per wave per stage
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * SBYTES];
+  constexpr int SLOT = BKM * SBYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * SLOT];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
   const int s = blockIdx.x % S, tile = blockIdx.x / S;
-  PENNY_DASSERT(M <= 16 * MT && (tile + 1) * 16 * NF <= N && K % (64 * S) == 0);
+  PENNY_DASSERT(M <= 16 * MT && (tile + 1) * 16 * NF <= N && K % (64 * BKM * S) == 0);
   const int n0 = tile * 16 * NF;
   const int kc = K / S, k0 = s * kc;
-  const int nst = kc / 64;
+  const int nst = kc / (64 * BKM);              // ring slots to stream
   const int ksteps = K / 32;
   const int wa = w / WB, wb = w % WB;
 
@@ -205,12 +210,15 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
     }
   }
   auto stage = [&](int j) {
-    char* base = smem + (j % NBUF) * SBYTES;
+    char* base = smem + (j % NBUF) * SLOT;
     // default cache policy on W too: the nt hint measured 4-7 % slower at M >= 48 (2-3 % faster
     // only at M <= 32; profiles/r1_splitk_v5_qkv_nont.jsonl vs r1_splitk_v4_qkv.jsonl)
 #pragma unroll
     for (int i = 0; i < LOADS; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + j * step[i]), (lds_void_t*)(base + dst[i]), 16, 0, 0);
+#pragma unroll
+      for (int u = 0; u < BKM; ++u)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[i] + (j * BKM + u) * step[i]),
+                                         (lds_void_t*)(base + u * SBYTES + dst[i]), 16, 0, 0);
   };
 
   f32x4 acc[FW][TW];
@@ -225,9 +233,11 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
 
   for (int j = 0; j < nst; ++j) {
     // stages j+1 .. min(j+NBUF-2, nst-1) may stay in flight
-    wait_stage<LOADS, NBUF - 2>(min(NBUF - 2, nst - 1 - j));
+    wait_stage<LOADS * BKM, NBUF - 2>(min(NBUF - 2, nst - 1 - j));
     if (j + NBUF - 1 < nst) stage(j + NBUF - 1);
-    stage_mma<FW, TW, WBYTES, WROW>(smem + (j % NBUF) * SBYTES, acc, wa, wb, lane, g, col);
+#pragma unroll
+    for (int u = 0; u < BKM; ++u)
+      stage_mma<FW, TW, WBYTES, WROW>(smem + (j % NBUF) * SLOT + u * SBYTES, acc, wa, wb, lane, g, col);
   }
 
   if constexpr (SILU) {
@@ -350,8 +360,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<uint4*>(Y + (long)m * ldy + n) = pack8(o);
 }
 
+// wrow: 0 = fragment-tiled W, 1 = row-major W, 2 = row-major W with paired stages (BKM = 2) where
+// the ring still holds >= 3 slots and the K slice is a multiple of 128 (else as 1)
+template <int NF, int MT, int RKB, int MAXB>
+constexpr bool pair_fits() {
+  return Ring<NF, MT, RKB, MAXB, 2>::NBUF >= 3;
+}
+
 template <int NF, int MT, int WA>
 int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
+  if constexpr (pair_fits<NF, MT, 150, 8>()) {
+    if (wrow == 2 && (K / S) % 128 == 0) {
+      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SLAB, true, 150, 8, 2>), dim3((N / (16 * NF)) * S), dim3(256),
+                         0, st, (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
+      return (int)hipGetLastError();
+    }
+  }
   if (wrow)
     hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SLAB, true>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
@@ -364,6 +388,14 @@ int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N
 template <int NF, int MT, int WA>
 int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
+  if constexpr (pair_fits<NF, MT, 150, NF == 2 ? 16 : 8>()) {
+    if (wrow == 2 && K % 128 == 0) {
+      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, true, 150, NF == 2 ? 16 : 8, 2>), dim3(N / (16 * NF)),
+                         dim3(256), 0, st, (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y,
+                         ldy);
+      return (int)hipGetLastError();
+    }
+  }
   if (wrow)
     hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, true, 150, NF == 2 ? 16 : 8>), dim3(N / (16 * NF)), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
@@ -376,6 +408,14 @@ int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy,
 template <int NF, int MT, int WA>
 int launch_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
+  if constexpr (pair_fits<NF, MT, 150, 16>()) {
+    if (wrow == 2 && K % 128 == 0) {
+      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, true, 150, 16, 2>), dim3(N / (16 * NF)), dim3(256), 0,
+                         st, (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy,
+                         SkSample{});
+      return (int)hipGetLastError();
+    }
+  }
   if (wrow)
     hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, true, 150, 16>), dim3(N / (16 * NF)), dim3(256), 0, st,
                        (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});

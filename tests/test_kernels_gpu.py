@@ -365,6 +365,16 @@ def test_skinny_gemm(M, cfg):
         gemm.TUNING.pop((N_, K), None)
 
 
+def _paired(fn):
+    """fn() with the row-major decode streams issuing their stages in pairs (gemm.RM_PAIR)."""
+    from financial_chatbot_llm_amd.ops import gemm
+    gemm.RM_PAIR = True
+    try:
+        return fn()
+    finally:
+        gemm.RM_PAIR = False
+
+
 @pytest.mark.parametrize("M", [5, 33, 64, 90, 128, 200, 256])
 @pytest.mark.parametrize("S,nf", [(1, 4), (2, 8), (4, 4), (8, 8), (2, 2), (4, 6)])
 def test_splitk_gemm(M, S, nf):
@@ -381,6 +391,8 @@ def test_splitk_gemm(M, S, nf):
     close(P, ref_p, atol=1e-3)
     # the row-major weight (no tiled copy) runs the identical MFMA sequence: bit-equal slabs
     assert torch.equal(gemm.splitk_partials(x.to(DEV), w.to(DEV), N_, S, nf, rowmajor=True), P)
+    # ... and so does the paired-stage row-major stream (same k order)
+    assert torch.equal(_paired(lambda: gemm.splitk_partials(x.to(DEV), w.to(DEV), N_, S, nf, rowmajor=True)), P)
     close(gemm.splitk_reduce(P), x.float() @ w.float().t(), atol=2e-2)
     close(gemm.splitk_reduce(P, residual=res.to(DEV)), x.float() @ w.float().t() + res.float(), atol=3e-2)
     # strided X (a view into a wider activation buffer) is a supported input
@@ -399,6 +411,11 @@ def test_splitk_rowmajor_tp_and_70b_shapes(N_, K, S, nf):
     w = rnd(N_, K, scale=0.02, gen=g).to(DEV)
     y = gemm.splitk_reduce(gemm.splitk_partials(x, w, N_, S, nf, rowmajor=True))
     close(y, x.float() @ w.float().t(), atol=3e-2)
+    assert torch.equal(_paired(lambda: gemm.splitk_reduce(gemm.splitk_partials(x, w, N_, S, nf, rowmajor=True))), y)
+    for nf2 in (2, 4, 8):          # the bf16-output (row-parallel TP shard) form
+        yb = gemm.splitk_bf16(x, w, N_, nf2)
+        close(yb, x.float() @ w.float().t(), atol=3e-2)
+        assert torch.equal(_paired(lambda: gemm.splitk_bf16(x, w, N_, nf2)), yb)
 
 
 @pytest.mark.parametrize("M,F", [(1, 384), (37, 14336), (300, 2048)])
@@ -441,6 +458,7 @@ def test_gateup_silu_gemm(M, nf):
     wi = gemm.interleave16(gate, up).to(DEV).contiguous()
     y = gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, nf)
     assert torch.equal(gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, nf, rowmajor=True), y)
+    assert torch.equal(_paired(lambda: gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, nf, rowmajor=True)), y)
     gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
     close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
     unfused = ops.silu_mul(torch.nn.functional.linear(x.to(DEV), wi), interleave16=True)
