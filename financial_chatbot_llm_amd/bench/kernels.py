@@ -1034,29 +1034,35 @@ SHARD_SHAPES = {
 }
 
 
-def bench_rm_pair(dev, names=("70b_tp1_gate_up", "70b_tp1_qkv", "70b_tp1_o", "70b_tp1_down", "70b_tp8_o",
-                                "70b_tp8_down"), Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)) -> List[Dict]:
-    """Row-major decode streams with BK=64 stages issued singly vs in pairs (gemm.RM_PAIR: each W row's
-    two 128-B chunks back to back), per (S, nf) config, with the fragment-tiled stream and hipBLASLt
-    as references; interleaved per M, weights rotated over >= 768 MB.  The paired stream must be
-    bit-identical to the single one (same k order): checked per config."""
+def bench_rm_pair(dev, names=("70b_tp8_o", "70b_tp8_down", "70b_tp8_qkv", "70b_tp8_gate_up", "70b_tp1_qkv", "70b_tp1_o",
+                                "70b_tp1_down", "70b_tp1_gate_up", "8b_qkv", "8b_o", "8b_down", "8b_gate_up"),
+                  Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)) -> List[Dict]:
+    """Decode GEMM streams with BK=64 stages issued singly vs in pairs (gemm.PAIR_MODE / BKM = 2),
+    per (S, nf) config, in the W layout the model streams at that shape (fragment-tiled where
+    ``uses_tiled_weight``, else row-major), hipBLASLt as the reference; interleaved per M, weights
+    rotated over >= 768 MB.  The paired stream must be bit-identical to the single one (same k order):
+    checked per config."""
     from ..ops import gemm
     from ..ops.activation import silu_mul
     out = []
     rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
 
-    def paired(f):
+    def mode(f, m):
         def g():
-            gemm.RM_PAIR = True
+            gemm.PAIR_MODE = m
             try:
                 return f()
             finally:
-                gemm.RM_PAIR = False
+                gemm.PAIR_MODE = "table"
         return g
     for name in names:
         N, K, kind = SHARD_SHAPES[name]
+        rm = not gemm.uses_tiled_weight(N, K)
         copies = max(2, min(16, (768 << 20) // (N * K * 2)))
         ws = [rnd(N, K) for _ in range(copies)]
+        w_lib = ws                      # hipBLASLt reads the row-major weights
+        if not rm:
+            ws = [gemm.tile_weight(w) for w in ws]
         it = [0]
 
         def nxt():
@@ -1066,45 +1072,53 @@ def bench_rm_pair(dev, names=("70b_tp1_gate_up", "70b_tp1_qkv", "70b_tp1_o", "70
             x = rnd(M, K)
             fns = {}
             if kind == "gateup":
-                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, ws[nxt()]), interleave16=True)
+                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, w_lib[nxt()]), interleave16=True)
                 for nf in (4, 8):
-                    fns[f"gu_nf{nf}"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=True)
-                for S, nf in ((2, 2), (4, 2), (8, 2), (2, 8), (4, 8)):
+                    fns[f"gu_nf{nf}"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=rm)
+                for S, nf in ((2, 2), (4, 2), (8, 2), (2, 4), (4, 4), (2, 8), (4, 8)):
+                    if K % (128 * S) or N % (32 * nf):
+                        continue
                     P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
                     y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
                     fns[f"guS{S}nf{nf}"] = (lambda S=S, nf=nf, P=P, y=y: gemm.gateup_splitk(
-                        x, ws[nxt()], N, S, nf, rowmajor=True, slabs=P, out=y))
-            elif kind == "row":
-                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
-                for nf in (2, 4, 8):
-                    fns[f"bf16_nf{nf}"] = lambda nf=nf: gemm.splitk_bf16(x, ws[nxt()], N, nf)
+                        x, ws[nxt()], N, S, nf, rowmajor=rm, slabs=P, out=y))
             else:
-                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
-                for S in (1, 2, 4, 8):
+                fns["lib"] = lambda: torch.nn.functional.linear(x, w_lib[nxt()])
+                if kind == "row":
                     for nf in (2, 4, 8):
+                        fns[f"bf16_nf{nf}"] = lambda nf=nf: gemm.splitk_bf16(x, ws[nxt()], N, nf, rowmajor=rm)
+                for S in (1, 2, 4, 8):
+                    for nf in (2, 4, 6, 8):
                         if K % (128 * S) or N % (16 * nf) or (N // (16 * nf)) * S < 128:
                             continue
                         P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
-                        fns[f"S{S}nf{nf}"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
-                            x, ws[nxt()], N, S, nf, out=P, rowmajor=True))
+                        if kind == "row":
+                            y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+                            fns[f"S{S}nf{nf}+red"] = (lambda S=S, nf=nf, P=P, y=y: gemm.splitk_reduce(
+                                gemm.splitk_partials(x, ws[nxt()], N, S, nf, out=P, rowmajor=rm), out=y))
+                        else:
+                            fns[f"S{S}nf{nf}"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
+                                x, ws[nxt()], N, S, nf, out=P, rowmajor=rm))
             same = {}
             for k in [k for k in fns if k != "lib"]:
+                f = fns[k]
                 it[0] = copies - 1
-                a = fns[k]()
+                a = mode(f, "0")()
                 it[0] = copies - 1
-                b = paired(fns[k])()
+                b = mode(f, "1")()
                 same[k] = bool(torch.equal(a, b))
-                fns[k + "_p"] = paired(fns[k])
+                fns[k] = mode(f, "0")
+                fns[k + "_p"] = mode(f, "1")
             t = interleaved(fns, rounds=5, iters=copies)
             single = min((k for k in t if k != "lib" and not k.endswith("_p")), key=lambda k: t[k])
             pair = min((k for k in t if k.endswith("_p")), key=lambda k: t[k])
-            row = {"op": "rm_pair", "name": name, "N": N, "K": K, "kind": kind, "M": M,
+            row = {"op": "rm_pair", "name": name, "N": N, "K": K, "kind": kind, "rowmajor": rm, "M": M,
                    **{k: round(v, 1) for k, v in t.items()}, "best_single": single, "best_pair": pair,
                    "pair_gain": round(t[single] / t[pair], 3), "pair_vs_lib": round(t["lib"] / t[pair], 3),
                    "pair_GBps": round(N * K * 2 / t[pair] / 1e3, 1), "bit_identical": all(same.values())}
             print(json.dumps(row), flush=True)
             out.append(row)
-        del ws
+        del ws, w_lib
         torch.cuda.empty_cache()
     return out
 

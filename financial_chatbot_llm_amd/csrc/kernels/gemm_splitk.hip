@@ -360,69 +360,50 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<uint4*>(Y + (long)m * ldy + n) = pack8(o);
 }
 
-// wrow: 0 = fragment-tiled W, 1 = row-major W, 2 = row-major W with paired stages (BKM = 2) where
-// the ring still holds >= 3 slots and the K slice is a multiple of 128 (else as 1)
+// wrow bit 0: W is the row-major [N, K] weight (else tile_weight's fragment-tiled copy); bit 1: BK=64
+// stages issued in pairs (BKM = 2) -- taken where the ring still holds >= 3 slots and each K slice
+// is a multiple of 128, else single stages
 template <int NF, int MT, int RKB, int MAXB>
 constexpr bool pair_fits() {
   return Ring<NF, MT, RKB, MAXB, 2>::NBUF >= 3;
 }
 
-template <int NF, int MT, int WA>
-int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
-  if constexpr (pair_fits<NF, MT, 150, 8>()) {
-    if (wrow == 2 && (K / S) % 128 == 0) {
-      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SLAB, true, 150, 8, 2>), dim3((N / (16 * NF)) * S), dim3(256),
-                         0, st, (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
+// one launch of splitk_gemm_kernel<NF, MT, WA, EPI, *, 150, MAXB, *> with the W layout / stage pairing
+// of wrow (runtime) mapped onto the template arguments
+template <int NF, int MT, int WA, int EPI, int MAXB, class... A>
+int launch_any(int wrow, bool pair_ok, dim3 grid, hipStream_t st, A... args) {
+  const bool rm = wrow & 1;
+  if constexpr (pair_fits<NF, MT, 150, MAXB>()) {
+    if ((wrow & 2) && pair_ok) {
+      if (rm) hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, EPI, true, 150, MAXB, 2>), grid, dim3(256), 0, st, args...);
+      else hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, EPI, false, 150, MAXB, 2>), grid, dim3(256), 0, st, args...);
       return (int)hipGetLastError();
     }
   }
-  if (wrow)
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SLAB, true>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
-  else
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA>), dim3((N / (16 * NF)) * S), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0);
+  if (rm) hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, EPI, true, 150, MAXB>), grid, dim3(256), 0, st, args...);
+  else hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, EPI, false, 150, MAXB>), grid, dim3(256), 0, st, args...);
   return (int)hipGetLastError();
+}
+
+template <int NF, int MT, int WA>
+int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
+  return launch_any<NF, MT, WA, SK_SLAB, 8>(wrow, (K / S) % 128 == 0, dim3((N / (16 * NF)) * S), st, (const bf16*)X,
+                                            ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0, SkSample{});
 }
 
 template <int NF, int MT, int WA>
 int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
-  if constexpr (pair_fits<NF, MT, 150, NF == 2 ? 16 : 8>()) {
-    if (wrow == 2 && K % 128 == 0) {
-      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, true, 150, NF == 2 ? 16 : 8, 2>), dim3(N / (16 * NF)),
-                         dim3(256), 0, st, (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y,
-                         ldy);
-      return (int)hipGetLastError();
-    }
-  }
-  if (wrow)
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, true, 150, NF == 2 ? 16 : 8>), dim3(N / (16 * NF)), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
-  else
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_SILU, false, 150, NF == 2 ? 16 : 8>), dim3(N / (16 * NF)), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy);
-  return (int)hipGetLastError();
+  return launch_any<NF, MT, WA, SK_SILU, NF == 2 ? 16 : 8>(wrow, K % 128 == 0, dim3(N / (16 * NF)), st, (const bf16*)X,
+                                                          ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y,
+                                                          ldy, SkSample{});
 }
 
 template <int NF, int MT, int WA>
 int launch_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
-  if constexpr (pair_fits<NF, MT, 150, 16>()) {
-    if (wrow == 2 && K % 128 == 0) {
-      hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, true, 150, 16, 2>), dim3(N / (16 * NF)), dim3(256), 0,
-                         st, (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy,
-                         SkSample{});
-      return (int)hipGetLastError();
-    }
-  }
-  if (wrow)
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, true, 150, 16>), dim3(N / (16 * NF)), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
-  else
-    hipLaunchKernelGGL((splitk_gemm_kernel<NF, MT, WA, SK_BF16, false, 150, 16>), dim3(N / (16 * NF)), dim3(256), 0, st,
-                       (const bf16*)X, ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
-  return (int)hipGetLastError();
+  return launch_any<NF, MT, WA, SK_BF16, 16>(wrow, K % 128 == 0, dim3(N / (16 * NF)), st, (const bf16*)X, ldx,
+                                             (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
 }
 
 // the streaming LM head: row-major W (wrow) or its fragment-tiled copy; ring budget 150 KiB (one
@@ -438,12 +419,12 @@ int launch_sample(const void* X, int ldx, const void* Wt, int K, int M, int N, i
   constexpr bool R2 = Ring<NF, MT, 72, 16>::NBUF >= 3;
   if constexpr (R2) {
     if (ring2) {
-      if (wrow) SK_SAMPLE_LAUNCH(true, 72);
+      if (wrow & 1) SK_SAMPLE_LAUNCH(true, 72);
       else SK_SAMPLE_LAUNCH(false, 72);
       return (int)hipGetLastError();
     }
   }
-  if (wrow) SK_SAMPLE_LAUNCH(true, 150);
+  if (wrow & 1) SK_SAMPLE_LAUNCH(true, 150);
   else SK_SAMPLE_LAUNCH(false, 150);
 #undef SK_SAMPLE_LAUNCH
   return (int)hipGetLastError();
@@ -489,7 +470,7 @@ PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int
 }
 
 // Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
-// aligned (ldx % 8 == 0).  wrow: Wt is the row-major [N, K] weight instead of tile_weight's copy.  nf: W row groups per workgroup (2, 4, 6 or 8;
+// aligned (ldx % 8 == 0).  wrow: bit 0 row-major W instead of tile_weight's copy, bit 1 paired stages.  nf: W row groups per workgroup (2, 4, 6 or 8;
 // 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4).  P is [S, M, N] f32.
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
                                 int wrow, hipStream_t stream) {

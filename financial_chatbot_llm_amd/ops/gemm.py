@@ -241,7 +241,7 @@ def splitk_bf16(x: torch.Tensor, w: torch.Tensor, N_: int, nf: int, rowmajor: bo
         return F.linear(x.float(), (w if rowmajor else untile_weight(w)).float()).to(x.dtype)
     y = out if out is not None else torch.empty((M, N_), dtype=x.dtype, device=x.device)
     N.call("penny_splitk_gemm_bf16", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), y.stride(0), M, N_, nf,
-           _wrow(rowmajor), N.stream())
+           _wrow(rowmajor, M, N_, K), N.stream())
     return y
 
 
@@ -249,14 +249,17 @@ def splitk_bf16(x: torch.Tensor, w: torch.Tensor, N_: int, nf: int, rowmajor: bo
 # at load, ``tile_weight``; 3-10 % faster for gate|up); "rowmajor": they always stream the
 # row-major weights directly (no extra HBM).  Shapes without a tiled copy use row-major anyway.
 DECODE_WEIGHTS = os.environ.get("PENNY_DECODE_WEIGHTS", "tiled")
-# Row-major decode streams issue their BK=64 stages in pairs (gemm_splitk.hip BKM = 2: each W row's
-# two 128-B chunks back to back) -- PENNY_RM_PAIR=1; A/B in bench/kernels.py rm_pair
-RM_PAIR = os.environ.get("PENNY_RM_PAIR", "0") == "1"
+# Decode streams whose BK=64 stages are issued (and waited for) in pairs (gemm_splitk.hip BKM = 2:
+# half the ring iterations and barriers per K slice) -- (N, K) -> up to how many rows.  Short K
+# slices gain most (bench/kernels.py rm_pair).  PENNY_PAIR_STAGES=0 / 1: never / always (A/B).
+PAIRED: Dict[Tuple[int, int], int] = {}
+PAIR_MODE = os.environ.get("PENNY_PAIR_STAGES", "table")
 
 
-def _wrow(rowmajor: bool) -> int:
-    """The kernels' W-layout argument: 0 fragment-tiled, 1 row-major, 2 row-major with paired stages."""
-    return (2 if RM_PAIR else 1) if rowmajor else 0
+def _wrow(rowmajor: bool, M: int = 0, N_: int = 0, K: int = 0) -> int:
+    """The kernels' W-layout argument: bit 0 row-major (else fragment-tiled), bit 1 paired stages."""
+    pair = PAIR_MODE == "1" or (PAIR_MODE == "table" and M <= PAIRED.get((N_, K), 0))
+    return int(bool(rowmajor)) | (2 if pair else 0)
 
 
 def uses_tiled_weight(N_: int, K: int) -> bool:
@@ -324,7 +327,7 @@ def gateup_silu(x: torch.Tensor, wt: torch.Tensor, N_: int, nf: int,
         return silu_mul(F.linear(x, wt if rowmajor else untile_weight(wt)), interleave16=True)
     y = out if out is not None else torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
     N.call("penny_gateup_silu_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), y.stride(0), M, N_, nf,
-           _wrow(rowmajor), N.stream())
+           _wrow(rowmajor, M, N_, K), N.stream())
     return y
 
 
@@ -411,8 +414,8 @@ def splitk_partials(x: torch.Tensor, wt: torch.Tensor, N_: int, S: int, nf: int,
         xs = x.float().view(M, S, K // S).transpose(0, 1)
         return torch.einsum("smk,snk->smn", xs, w.view(N_, S, K // S).transpose(0, 1))
     P = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
-    N.call("penny_splitk_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(P), M, N_, S, nf, _wrow(rowmajor),
-           N.stream())
+    N.call("penny_splitk_gemm", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(P), M, N_, S, nf,
+           _wrow(rowmajor, M, N_, K), N.stream())
     return P
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# r5 session 24: row-major decode streams with paired BK=64 stages -- bit-identity GPU tests, then the
-# single vs paired A/B at the 70B TP=1 / TP=8 row-major shapes.
+# r5 session 24: decode GEMM streams with paired BK=64 stages -- bit-identity GPU tests, then the
+# single vs paired A/B at the 70B TP=1 / TP=8 and 8B decode shapes.
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1

@@ -366,13 +366,13 @@ def test_skinny_gemm(M, cfg):
 
 
 def _paired(fn):
-    """fn() with the row-major decode streams issuing their stages in pairs (gemm.RM_PAIR)."""
+    """fn() with the decode GEMM streams issuing their BK=64 stages in pairs (gemm.PAIR_MODE)."""
     from financial_chatbot_llm_amd.ops import gemm
-    gemm.RM_PAIR = True
+    gemm.PAIR_MODE = "1"
     try:
         return fn()
     finally:
-        gemm.RM_PAIR = False
+        gemm.PAIR_MODE = "table"
 
 
 @pytest.mark.parametrize("M", [5, 33, 64, 90, 128, 200, 256])
@@ -393,6 +393,7 @@ def test_splitk_gemm(M, S, nf):
     assert torch.equal(gemm.splitk_partials(x.to(DEV), w.to(DEV), N_, S, nf, rowmajor=True), P)
     # ... and so does the paired-stage row-major stream (same k order)
     assert torch.equal(_paired(lambda: gemm.splitk_partials(x.to(DEV), w.to(DEV), N_, S, nf, rowmajor=True)), P)
+    assert torch.equal(_paired(lambda: gemm.splitk_partials(x.to(DEV), wt, N_, S, nf)), P)
     close(gemm.splitk_reduce(P), x.float() @ w.float().t(), atol=2e-2)
     close(gemm.splitk_reduce(P, residual=res.to(DEV)), x.float() @ w.float().t() + res.float(), atol=3e-2)
     # strided X (a view into a wider activation buffer) is a supported input
@@ -459,6 +460,7 @@ def test_gateup_silu_gemm(M, nf):
     y = gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, nf)
     assert torch.equal(gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, nf, rowmajor=True), y)
     assert torch.equal(_paired(lambda: gemm.gateup_silu(x.to(DEV), wi, 2 * Fr, nf, rowmajor=True)), y)
+    assert torch.equal(_paired(lambda: gemm.gateup_silu(x.to(DEV), gemm.tile_weight(wi), 2 * Fr, nf)), y)
     gf, uf = x.float() @ gate.float().t(), x.float() @ up.float().t()
     close(y, torch.nn.functional.silu(gf) * uf, atol=3e-2)
     unfused = ops.silu_mul(torch.nn.functional.linear(x.to(DEV), wi), interleave16=True)
