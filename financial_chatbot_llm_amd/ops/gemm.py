@@ -186,7 +186,9 @@ def load_gemm_tuning(model: str, tp: int = 1) -> Optional[str]:
 # (profiles/r1_splitk_v4_qkv.jsonl: the 96-row QKV tile beats 128 rows x 192 workgroups by 10 %).
 SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     (6144, 4096): [(256, 4, 6)],                             # QKV: 96-row tiles -> 256 workgroups
-    (4096, 4096): [(256, 4, 4)],                             # O (r5: S4 nf4 also ahead at M = 256, 23.4 vs 24.4 us)
+    # O (r5: S4 nf4 also ahead at M = 256, 23.4 vs 24.4 us; with paired stages S4 nf2 is 2-8 % ahead of
+    # S4 nf4 to 32 rows, profiles/r5_decode_gemm_paired_stages_ab.jsonl)
+    (4096, 4096): [(32, 4, 2), (256, 4, 4)],
     (4096, 14336): [(16, 8, 8), (32, 4, 4), (256, 8, 8)],    # down
     # Llama-3-70B (TP=1), streamed row-major (profiles/r1_splitk_70b.jsonl): down 1.2-1.9x hipBLASLt
     # at M = 32..256; O 1.1-1.5x from M = 96 (S = 0: the library is as fast below that)
@@ -250,9 +252,17 @@ def splitk_bf16(x: torch.Tensor, w: torch.Tensor, N_: int, nf: int, rowmajor: bo
 # row-major weights directly (no extra HBM).  Shapes without a tiled copy use row-major anyway.
 DECODE_WEIGHTS = os.environ.get("PENNY_DECODE_WEIGHTS", "tiled")
 # Decode streams whose BK=64 stages are issued (and waited for) in pairs (gemm_splitk.hip BKM = 2:
-# half the ring iterations and barriers per K slice) -- (N, K) -> up to how many rows.  Short K
-# slices gain most (bench/kernels.py rm_pair).  PENNY_PAIR_STAGES=0 / 1: never / always (A/B).
-PAIRED: Dict[Tuple[int, int], int] = {}
+# half the ring iterations and barriers per K slice) -- (N, K) -> up to how many rows.  Measured per
+# table config, paired vs single, interleaved (bench/kernels.py rm_pair,
+# profiles/r5_decode_gemm_paired_stages_ab.jsonl; bit-identical outputs): at M <= 128 Llama-3-8B QKV
+# +4-6 %, O +5-12 %, down +2-4 %, gate|up +3-6 %; Llama-3-70B TP=8 shards QKV +5-13 %, O +3-17 %,
+# down +10-25 %, gate|up +2-5 %; 70B TP=1 +1-6 %.  From 192 rows the MFMA work per stage hides the
+# barrier and the two forms tie.  PENNY_PAIR_STAGES=0 / 1: never / always (A/B).
+PAIRED: Dict[Tuple[int, int], int] = {
+    (6144, 4096): 128, (4096, 4096): 128, (4096, 14336): 128, (28672, 4096): 128,        # Llama-3-8B
+    (1280, 8192): 128, (8192, 1024): 128, (8192, 3584): 128, (7168, 8192): 128,          # 70B TP=8 shards
+    (10240, 8192): 128, (8192, 8192): 128, (8192, 28672): 128, (57344, 8192): 16,        # 70B TP=1
+}
 PAIR_MODE = os.environ.get("PENNY_PAIR_STAGES", "table")
 
 
@@ -300,7 +310,8 @@ def splitk_config(M: int, N_: int, K: int) -> Optional[Tuple[int, int]]:
 GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
     # r5 re-measure (profiles/r5_gateup_shapes.jsonl): 1.5x at M <= 16, 1.2-1.3x at 32-128, and also
     # ahead above 160 rows (1.15x at 192, 1.02x at 256)
-    (28672, 4096): [(1, 256, 8)],
+    # (r5 paired stages: one row is the split-K form's, GATEUP_SPLITK)
+    (28672, 4096): [(2, 256, 8)],
 }
 
 
@@ -342,6 +353,9 @@ GATEUP_SPLITK: Dict[Tuple[int, int], List[Tuple[int, int, int, int, bool]]] = {
     # Llama-3-70B TP=1, row-major (no tiled copy: 75 GB): 1.23x at M = 1, 1.08x at 8, 1.04x at 16;
     # hipBLASLt from 32 rows
     (57344, 8192): [(1, 1, 8, 2, True), (2, 16, 4, 2, True)],
+    # Llama-3-8B at one row: S4 nf2 + reduce-SiLU with paired stages 44.4 us vs the fused kernel's 50.3
+    # (r5_decode_gemm_paired_stages_ab.jsonl)
+    (28672, 4096): [(1, 1, 4, 2, False)],
 }
 
 
