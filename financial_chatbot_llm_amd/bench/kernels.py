@@ -1123,6 +1123,87 @@ def bench_rm_pair(dev, names=("70b_tp8_o", "70b_tp8_down", "70b_tp8_qkv", "70b_t
     return out
 
 
+def bench_chunked_prefill(dev, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_up", "70b_tp8_down", "70b_tp1_qkv",
+                                       "8b_qkv", "8b_o"),
+                          Ms=(384, 512, 768, 1024, 1536, 2048)) -> List[Dict]:
+    """Small prefill steps (M > 256) on the decode split-K kernels with 256-row token chunks side by
+    side (grid y), vs the production path (``gemm.linear``: PREFILL_POLICY's library / tile-kernel
+    choice), hipBLASLt and the tile kernel, interleaved per M.  W in the layout the model keeps at that
+    shape.  "col" rows also report ``adj``: the time plus the consumer's extra slab read
+    ((4S - 2) * M * N bytes at 5 TB/s) against a bf16 output."""
+    from ..ops import gemm
+    from ..ops.activation import silu_mul
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    for name in names:
+        N, K, kind = SHARD_SHAPES[name]
+        rm = not gemm.uses_tiled_weight(N, K)
+        copies = max(2, min(16, (768 << 20) // (N * K * 2)))
+        ws = [rnd(N, K) for _ in range(copies)]
+        wts = [gemm.tile_weight(w) for w in ws] if not rm else ws
+        it = [0]
+
+        def nxt():
+            it[0] = (it[0] + 1) % copies
+            return it[0]
+        for M in Ms:
+            x = rnd(M, K)
+            fns, extra = {}, {}
+            if kind == "gateup":
+                fns["lib"] = lambda: silu_mul(torch.nn.functional.linear(x, ws[nxt()]), interleave16=True)
+                fns["prod"] = lambda: gemm.linear(x, ws[nxt()], epilogue="silu", wt=None if rm else wts[it[0]])
+                fns["tile"] = lambda: gemm.prefill_gemm(x, ws[nxt()], "silu")
+                for nf in (2, 4, 8):
+                    fns[f"ch_gu_nf{nf}"] = lambda nf=nf: gemm.gateup_silu(x, wts[nxt()], N, nf, rowmajor=rm)
+                for S, nf in ((2, 2), (2, 4), (4, 4), (2, 8)):
+                    if K % (64 * S) or N % (32 * nf):
+                        continue
+                    P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                    y = torch.empty((M, N // 2), dtype=torch.bfloat16, device=dev)
+                    fns[f"ch_guS{S}nf{nf}"] = (lambda S=S, nf=nf, P=P, y=y: gemm.gateup_splitk(
+                        x, wts[nxt()], N, S, nf, rowmajor=rm, slabs=P, out=y))
+            elif kind == "row":
+                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
+                fns["prod"] = lambda: gemm.linear(x, ws[nxt()], wt=None if rm else wts[it[0]])
+                fns["tile"] = lambda: gemm.prefill_gemm(x, ws[nxt()])
+                for nf in (2, 4, 8):
+                    fns[f"ch_bf16_nf{nf}"] = lambda nf=nf: gemm.splitk_bf16(x, wts[nxt()], N, nf, rowmajor=rm)
+                for S, nf in ((2, 4), (4, 4), (2, 8)):
+                    if K % (64 * S) or N % (16 * nf):
+                        continue
+                    P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                    y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+                    fns[f"ch_S{S}nf{nf}+red"] = (lambda S=S, nf=nf, P=P, y=y: gemm.splitk_reduce(
+                        gemm.splitk_partials(x, wts[nxt()], N, S, nf, out=P, rowmajor=rm), out=y))
+            else:
+                fns["lib"] = lambda: torch.nn.functional.linear(x, ws[nxt()])
+                fns["prod"] = lambda: gemm.linear(x, ws[nxt()], wt=None if rm else wts[it[0]], slabs=True)
+                for S in (2, 4):
+                    if K % (64 * S) == 0:
+                        fns[f"tileS{S}"] = lambda S=S: gemm.prefill_gemm(x, ws[nxt()], "slabs", S)
+                        extra[f"tileS{S}"] = (4 * S - 2) * M * N / 5e6
+                for S in (1, 2, 4, 8):
+                    for nf in (2, 4, 6, 8):
+                        if K % (64 * S) or N % (16 * nf):
+                            continue
+                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
+                        fns[f"ch_S{S}nf{nf}"] = (lambda S=S, nf=nf, P=P: gemm.splitk_partials(
+                            x, wts[nxt()], N, S, nf, out=P, rowmajor=rm))
+                        extra[f"ch_S{S}nf{nf}"] = (4 * S - 2) * M * N / 5e6
+            t = interleaved(fns, rounds=5, iters=copies)
+            adj = {k: t[k] + extra.get(k, 0.0) for k in t}
+            best = min((k for k in t if k.startswith("ch_")), key=lambda k: adj[k])
+            row = {"op": "chunked_prefill", "name": name, "N": N, "K": K, "kind": kind, "rowmajor": rm, "M": M,
+                   **{k: round(v, 1) for k, v in t.items()}, "best_chunked": best, "best_adj_us": round(adj[best], 1),
+                   "prod_us": round(t["prod"], 1), "chunked_vs_prod": round(adj["prod"] / adj[best], 3),
+                   "chunked_vs_lib": round(t["lib"] / adj[best], 3)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del ws, wts
+        torch.cuda.empty_cache()
+    return out
+
+
 def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
                        prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
     """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
@@ -1302,7 +1383,7 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "chunked_prefill": bench_chunked_prefill,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
                 "lm_head_stream": bench_lm_head_stream, "decode_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down"), Ms=(32, 64, 96, 128, 160, 192, 256), prefill_Ms=()), "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),

@@ -172,7 +172,14 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, col = lane & 15;
   const int s = blockIdx.x % S, tile = blockIdx.x / S;
-  PENNY_DASSERT(M <= 16 * MT && (tile + 1) * 16 * NF <= N && K % (64 * BKM * S) == 0);
+  // token chunks (blockIdx.y): rows m0 .. m0 + 16*MT - 1 of X / Y / the slabs; one chunk for decode
+  // batches, ceil(M / (16*MT)) for the small prefill steps of narrow TP shards
+  const int Mtot = M, m0 = blockIdx.y * 16 * MT;
+  M = min(Mtot - m0, 16 * MT);
+  X += (long)m0 * ldx;
+  if constexpr (EPI == SK_SILU || EPI == SK_BF16) Y += (long)m0 * ldy;
+  PENNY_DASSERT(M > 0 && (EPI != SK_SAMPLE || gridDim.y == 1));
+  PENNY_DASSERT((tile + 1) * 16 * NF <= N && K % (64 * BKM * S) == 0);
   const int n0 = tile * 16 * NF;
   const int kc = K / S, k0 = s * kc;
   const int nst = kc / (64 * BKM);              // ring slots to stream
@@ -316,7 +323,7 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
     return;
   }
   // lane holds W rows n = 16f + 4g + r (r = 0..3) for token 16t + col: one 16-B store per tile
-  float* ps = P + (long)s * M * N;
+  float* ps = P + (long)s * Mtot * N + (long)m0 * N;
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     const int m = (wb * TW + t) * 16 + col;
@@ -387,14 +394,14 @@ int launch_any(int wrow, bool pair_ok, dim3 grid, hipStream_t st, A... args) {
 
 template <int NF, int MT, int WA>
 int launch(const void* X, int ldx, const void* Wt, int K, float* P, int M, int N, int S, int wrow, hipStream_t st) {
-  return launch_any<NF, MT, WA, SK_SLAB, 8>(wrow, (K / S) % 128 == 0, dim3((N / (16 * NF)) * S), st, (const bf16*)X,
+  return launch_any<NF, MT, WA, SK_SLAB, 8>(wrow, (K / S) % 128 == 0, dim3((N / (16 * NF)) * S, (M + 16 * MT - 1) / (16 * MT)), st, (const bf16*)X,
                                             ldx, (const bf16*)Wt, K, P, M, N, S, (bf16*)nullptr, 0, SkSample{});
 }
 
 template <int NF, int MT, int WA>
 int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
-  return launch_any<NF, MT, WA, SK_SILU, NF == 2 ? 16 : 8>(wrow, K % 128 == 0, dim3(N / (16 * NF)), st, (const bf16*)X,
+  return launch_any<NF, MT, WA, SK_SILU, NF == 2 ? 16 : 8>(wrow, K % 128 == 0, dim3(N / (16 * NF), (M + 16 * MT - 1) / (16 * MT)), st, (const bf16*)X,
                                                           ldx, (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y,
                                                           ldy, SkSample{});
 }
@@ -402,7 +409,7 @@ int launch_silu(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy,
 template <int NF, int MT, int WA>
 int launch_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N, int wrow,
                 hipStream_t st) {
-  return launch_any<NF, MT, WA, SK_BF16, 16>(wrow, K % 128 == 0, dim3(N / (16 * NF)), st, (const bf16*)X, ldx,
+  return launch_any<NF, MT, WA, SK_BF16, 16>(wrow, K % 128 == 0, dim3(N / (16 * NF), (M + 16 * MT - 1) / (16 * MT)), st, (const bf16*)X, ldx,
                                              (const bf16*)Wt, K, (float*)nullptr, M, N, 1, (bf16*)Y, ldy, SkSample{});
 }
 
@@ -438,14 +445,14 @@ extern "C" int penny_lm_sample_final(const float* pv, const int* pi, int P, int 
 
 // Fused gate|up + SiLU*up for 16 < M <= 256 (K9 at mid-batch decode): W = tile_weight(interleave16
 // gate|up) [N = 2F rows], Y [M, F] bf16 with row stride ldy.  No split-K: N = 28672 already gives
-// N/(16*nf) = 224 (nf 8) or 448 (nf 4) workgroups.  Contract (checked): N % (16*nf) == 0,
-// nf in {4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0.
+// N/(16*nf) = 224 (nf 8) or 448 (nf 4) workgroups.  M > 256: 256-row token chunks side by side on
+// grid y.  Contract (checked): N % (16*nf) == 0, nf in {2, 4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0.
 PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
                                      int nf, int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
+  if (M > (1 << 20) || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
-  const int mt = (M + 15) / 16;
+  const int mt = min((M + 15) / 16, 16);   // > 256 rows: 256-row token chunks on grid y
   // nf = 2 (one (gate, up) pair per workgroup, WA = 1): twice the workgroups of nf = 4 for narrow
   // TP shards (Llama-3-70B TP=8 gate|up: N = 7168 -> 224 workgroups)
   if (nf == 2) {   // WA = 1 -> 4 token-tile wave columns: token tiles rounded up to a multiple of 4
@@ -469,15 +476,16 @@ PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int
   return (int)hipErrorInvalidValue;
 }
 
-// Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, M <= 16*MT <= 256, X rows 16-B
+// Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, X rows 16-B
 // aligned (ldx % 8 == 0).  wrow: bit 0 row-major W instead of tile_weight's copy, bit 1 paired stages.  nf: W row groups per workgroup (2, 4, 6 or 8;
 // 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4).  P is [S, M, N] f32.
+// M > 256: 256-row token chunks side by side on grid y (small prefill steps of narrow TP shards).
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
                                 int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 256 || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8) || N % (16 * nf))
+  if (M > (1 << 20) || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
-  const int mt = (M + 15) / 16;
+  const int mt = min((M + 15) / 16, 16);   // > 256 rows: 256-row token chunks on grid y
   float* p = static_cast<float*>(P);
 #define SK_CASE(MT_, WA2_, WA4_, WA8_)                                                 \
   if (mt <= MT_) {                                                                     \
@@ -553,13 +561,13 @@ PENNY_API int penny_splitk_reduce(const void* P, int S, int M, int N, void* Y, i
 // X [M, K] x W [N, K]^T, one workgroup per 16*nf W rows -- the TP shards of O / down whose output
 // feeds the all-reduce directly (Llama-3-70B TP=8: N = 8192 -> 256 workgroups at nf = 2).
 // Contract (checked): N % (16*nf) == 0, nf in {2, 4, 8}, K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0,
-// 1 <= M <= 256.
+// M >= 1 (> 256: 256-row token chunks on grid y).
 PENNY_API int penny_splitk_gemm_bf16(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
                                      int nf, int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 256 || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
+  if (M > (1 << 20) || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
-  const int mt = (M + 15) / 16;
+  const int mt = min((M + 15) / 16, 16);   // > 256 rows: 256-row token chunks on grid y
 #define BF_CASE(MT_, WA2_, WA4_, WA8_)                                                          \
   if (mt <= MT_) {                                                                            \
     if (nf == 2) return launch_bf16<2, MT_, WA2_>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);  \

@@ -403,6 +403,35 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [257, 600, 1100])
+def test_splitk_kernels_token_chunks(M):
+    """M > 256 on the decode kernels: 256-row token chunks side by side (grid y) -- slabs, bf16 output
+    and the fused gate|up, row-major and fragment-tiled W, single and paired stages, vs fp32."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(21)
+    N_, K = 512, 1024
+    x = rnd(M, K, gen=g).to(DEV)
+    w = rnd(N_, K, scale=0.05, gen=g).to(DEV)
+    wt = gemm.tile_weight(w)
+    ref = x.float() @ w.float().t()
+    for S, nf in ((1, 4), (2, 8), (4, 2)):
+        P = gemm.splitk_partials(x, wt, N_, S, nf)
+        close(P.sum(0), ref, atol=2e-3)
+        assert torch.equal(gemm.splitk_partials(x, w, N_, S, nf, rowmajor=True), P)
+        assert torch.equal(_paired(lambda: gemm.splitk_partials(x, wt, N_, S, nf)), P)
+    for nf in (2, 4, 8):
+        y = gemm.splitk_bf16(x, w, N_, nf)
+        close(y, ref, atol=2e-2)
+        assert torch.equal(gemm.splitk_bf16(x, wt, N_, nf, rowmajor=False), y)
+    gate, up = rnd(N_ // 2, K, scale=0.05, gen=g).to(DEV), rnd(N_ // 2, K, scale=0.05, gen=g).to(DEV)
+    wi = gemm.interleave16(gate, up).contiguous()
+    ys = torch.nn.functional.silu(x.float() @ gate.float().t()) * (x.float() @ up.float().t())
+    for nf in (2, 4, 8):
+        yg = gemm.gateup_silu(x, gemm.tile_weight(wi), N_, nf)
+        close(yg, ys, atol=3e-2)
+        assert torch.equal(gemm.gateup_silu(x, wi, N_, nf, rowmajor=True), yg)
+
+
 @pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])
 def test_splitk_rowmajor_tp_and_70b_shapes(N_, K, S, nf):
     """The table shapes that stream the row-major weight (70B, TP=8 shards) vs the fp32 reference."""
