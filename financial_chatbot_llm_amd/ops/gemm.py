@@ -86,6 +86,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
     if M > 256 and prefill_ok(x, w) and epilogue in (None, "silu", "residual"):
         fr = fuse_residual is not None and epilogue is None and residual is None
         c = prefill_choice(M, N_, K, epilogue, slabs and residual is None, fused_residual=fr)
+        if c.startswith("K"):
+            return splitk_bf16(x, w, N_, int(c[1:]))
         if c == "R":
             prefill_gemm(x, w, "residual", residual=fuse_residual, out=fuse_residual)
             return ResidualSum(fuse_residual)
@@ -463,6 +465,8 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 #   "R"    tile kernel adding the residual stream in place (ResidualSum; the consumer's RMSNorm
 #          then skips the add): O from M = 2816 is 3-5 % faster than hipBLASLt + add&norm; only
 #          where the caller passes fuse_residual
+#   "K<nf>" the decode kernel's bf16-output form (row-major W, nf row groups per workgroup) with
+#          256-row token chunks side by side -- narrow row-parallel TP shards at small prefill steps
 # QKV (r4): the fused RoPE + paged-KV-write tile kernel at every M > 256 as well (hipBLASLt was
 # 7-15 us per layer faster at 257-1280 rows; at the driver config the bench is unchanged, 32.2
 # turns/s, profiles/r4_bench128_20x5_all_prefill_gemms_tile_kernel.json).
@@ -491,7 +495,10 @@ PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     # TP=8 per-rank shards: the 256x256 tile underfills the CUs at these N up to ~1.5-2k rows (5 / 28
     # / 32 column tiles), so the library keeps those; the tile kernel where it measured ahead
     (1280, 8192): [(1536, "lib"), (3072, "S4"), (1 << 30, "S2")],                        # QKV shard
-    (8192, 1024): [(1536, "lib"), (2048, "hip"), (1 << 30, "lib")],                      # O shard
+    # O shard: 256-row token chunks of the bf16 decode kernel at <= 512 rows (18.0-18.6 vs hipBLASLt
+    # 20.3-20.8 us; profiles/r5_chunked_splitk_prefill_ab.jsonl -- the chunked form lost everywhere
+    # else it was measured: 8B QKV / O, 70B TP=1 QKV, the other TP=8 shards)
+    (8192, 1024): [(512, "K4"), (1536, "lib"), (2048, "hip"), (1 << 30, "lib")],          # O shard
     (7168, 8192): [(1024, "lib"), (3072, "hip"), (1 << 30, "lib")],                      # gate|up shard
     (8192, 3584): [(1 << 30, "lib")],                                                    # down shard
 }
@@ -527,6 +534,8 @@ def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slab
         choice = "hip" if force else "lib"
     if choice == "fused":           # only the QKV entry point (qkv_rope_choice) fuses RoPE
         choice = "hip"
+    if choice.startswith("K") and epilogue is not None:
+        choice = "lib"
     return choice
 
 

@@ -20,6 +20,10 @@ def test_policy_table_choices(monkeypatch):
     # gate|up + SiLU on the tile kernel from 512 rows
     assert gemm.prefill_choice(512, 28672, 4096, "silu") == "hip"
     assert gemm.prefill_choice(256, 28672, 4096, "silu") == "lib"
+    # 70B TP=8 O shard: the chunked bf16 decode kernel at small prefill steps, then the library
+    assert gemm.prefill_choice(384, 8192, 1024, None) == "K4"
+    assert gemm.prefill_choice(768, 8192, 1024, None) == "lib"
+    assert gemm.prefill_choice(384, 8192, 1024, "silu") == "lib"
     # force: every tile path, the residual epilogue where offered
     monkeypatch.setenv("PENNY_PREFILL_GEMM", "force")
     assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "R"
