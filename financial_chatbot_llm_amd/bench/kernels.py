@@ -133,12 +133,13 @@ def bench_decode_lean(dev) -> List[Dict]:
         ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
         o = torch.empty_like(q)
 
-        def mk(lean):
+        def mk(lean, flags=0):
             def f():
-                A.DECODE_LEAN = lean
+                A.DECODE_LEAN, A.LEAN_FLAGS = lean, flags
                 ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o)
+                A.LEAN_FLAGS = 0
             return f
-        fns = {"part": mk(False), "lean": mk(True)}
+        fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1)}
         ref = None
         errs = {}
         for k, f in fns.items():
@@ -165,7 +166,7 @@ def bench_decode_lean(dev) -> List[Dict]:
                 torch.cuda.current_stream().wait_stream(side)
             return g2
         tp = interleaved({"prefill_only": lambda: ops.prefill(pq, pcu, plens, ptab, pkc, pvc, 0.088, True, 512, out=po),
-                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean")}},
+                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean", "lean_nt")}},
                          rounds=7, iters=20)
         A.DECODE_LEAN = True
         uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2

@@ -709,7 +709,20 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
 // balanced: 185 vs 140 us at B = 64, profiles/r3_decode_lean_vs_partitioned.jsonl; removed in r5.)
 constexpr int LEAN_META0 = 64;   // meta[LEAN_META0..]: the plan, published for the merge kernel
 
-template <int D>
+// K/V fragment load of the lean kernel: default cache policy, or (NT) non-temporal -- the stream is
+// read once per step except the shared-prefix blocks (A/B: lean_flags bit 0)
+template <bool NT>
+__device__ __forceinline__ uint4 kv_load(const uint4* p) {
+  if constexpr (NT) {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+    return *p;
+  }
+}
+
+template <int D, bool NT = false>
 __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
@@ -773,11 +786,11 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int c = 0; c < KC; ++c) kf[t][c].u = kb[(t * KC + c) * 64 + lane];
+        for (int c = 0; c < KC; ++c) kf[t][c].u = kv_load<NT>(kb + (t * KC + c) * 64 + lane);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int st = 0; st < 2; ++st) vf[dt][st].u = vb[(dt * 2 + st) * 64 + lane];
+        for (int st = 0; st < 2; ++st) vf[dt][st].u = kv_load<NT>(vb + (dt * 2 + st) * 64 + lane);
       const int j = k;
       f32x4 sc[4];
       float mt = -INFINITY;
@@ -1230,7 +1243,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                                      const void* v_cache, void* out, float* part_m, float* part_l, float* part_o,
                                      int B, int Hq, int Hkv, int D, int max_blocks, int pb, int nparts,
                                      int part_stride, float scale, int lean_grid, int* lean_meta,
-                                     int lean_min_per_wave, hipStream_t stream) {
+                                     int lean_min_per_wave, int lean_flags, hipStream_t stream) {
   if (B <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || pb <= 0 || nparts <= 0 || part_stride < nparts) return (int)hipErrorInvalidValue;
   // lean_grid > 0: the work-balanced kernel (decode_lean_kernel) and its merge; otherwise the
@@ -1251,9 +1264,16 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
   const float sl2 = scale * LOG2E;
 #define DECODE_LAUNCH(DD)                                                                                         \
   if (lean) {                                                                                                   \
-    hipLaunchKernelGGL(decode_lean_kernel<DD>, dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, ctx_lens,     \
-                       block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m, part_l,     \
-                       part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride, lean_min_per_wave); \
+    if (lean_flags & 1)                                                                                         \
+      hipLaunchKernelGGL((decode_lean_kernel<DD, true>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q,  \
+                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
+                         part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
+                         lean_min_per_wave);                                                                     \
+    else                                                                                                        \
+      hipLaunchKernelGGL((decode_lean_kernel<DD, false>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, \
+                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
+                         part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
+                         lean_min_per_wave);                                                                     \
     hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
                        part_o, (bf16*)out, B, Hq, part_stride);                                                  \
   } else {                                                                                                      \

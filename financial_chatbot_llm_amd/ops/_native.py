@@ -59,7 +59,7 @@ _SIGS = {
                                      c_int, P, P, P],
     "penny_splitk_reduce_silu": [P, c_int, c_int, c_int, P, c_int, P],
     "penny_attention_decode": [P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                               c_float, c_int, P, c_int, P],
+                               c_float, c_int, P, c_int, c_int, P],
     "penny_sample": [P, c_int, c_long, P, P, P, P, P, P, c_int, c_int, P],
     "penny_lm_head_sample": [P, c_int, P, c_int, c_int, c_int, P, P, P, P, P],
     "penny_lm_head_sample_shard": [P, c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P],

@@ -395,6 +395,8 @@ DECODE_LEAN = os.environ.get("PENNY_DECODE_LEAN", "1") != "0"
 LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
+# lean kernel flags (attention.hip penny_attention_decode lean_flags): bit 0 = non-temporal K/V loads
+LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "0"))
 LEAN_META0 = 64             # lean_meta[64:]: the plan published for the merge (attention.hip LEAN_META0)
 _CU_COUNT = {}
 
@@ -449,8 +451,8 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale)]
-        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE)
-                     if lean else (0, None, 1))
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_FLAGS)
+                     if lean else (0, None, 1, 0))
         N.call("penny_attention_decode", *args, *lean_args, N.stream() if stream is None else stream)
         return out
     out = torch.empty_like(q) if out is None else out
