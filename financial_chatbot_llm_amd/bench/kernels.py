@@ -139,7 +139,8 @@ def bench_decode_lean(dev) -> List[Dict]:
                 ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o)
                 A.LEAN_FLAGS = 0
             return f
-        fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1)}
+        fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1), "lean_nt16": mk(True, 1 | 16 << 8),
+               "lean_nt32": mk(True, 1 | 32 << 8)}
         ref = None
         errs = {}
         for k, f in fns.items():
@@ -166,7 +167,7 @@ def bench_decode_lean(dev) -> List[Dict]:
                 torch.cuda.current_stream().wait_stream(side)
             return g2
         tp = interleaved({"prefill_only": lambda: ops.prefill(pq, pcu, plens, ptab, pkc, pvc, 0.088, True, 512, out=po),
-                          **{"with_" + k: pair(fns[k]) for k in ("part", "lean", "lean_nt")}},
+                          **{"with_" + k: pair(fns[k]) for k in fns}},
                          rounds=7, iters=20)
         A.DECODE_LEAN = True
         uniq = (sum(ctxs) - (B - 1) * shared) * Hkv * D * 2 * 2

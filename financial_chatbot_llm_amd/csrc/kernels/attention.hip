@@ -26,6 +26,8 @@
 // (every turn's system prompt is a prefix-cache hit) are in flight together and hit in L2/MALL.
 #include "common.h"
 
+#include <type_traits>
+
 #include <cstdlib>
 #include "kv_layout.h"
 
@@ -710,7 +712,8 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
 constexpr int LEAN_META0 = 64;   // meta[LEAN_META0..]: the plan, published for the merge kernel
 
 // K/V fragment load of the lean kernel: default cache policy, or (NT) non-temporal -- the stream is
-// read once per step except the shared-prefix blocks (A/B: lean_flags bit 0)
+// read once per step except the shared-prefix blocks, which keep the default policy (their L2 / MALL
+// reuse across rows): lean_flags bit 0 = NT from block index lean_flags >> 8 of each row
 template <bool NT>
 __device__ __forceinline__ uint4 kv_load(const uint4* p) {
   if constexpr (NT) {
@@ -727,7 +730,8 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
     float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta,
-    float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride, int min_per_wave) {
+    float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride, int min_per_wave,
+    int nt_from) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
@@ -783,14 +787,19 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
       const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
       const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
       Frag kf[4][KC], vf[DT][2];
+      auto load_kv = [&](auto ntc) {
+        constexpr bool NTB = decltype(ntc)::value;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int c = 0; c < KC; ++c) kf[t][c].u = kv_load<NT>(kb + (t * KC + c) * 64 + lane);
+          for (int c = 0; c < KC; ++c) kf[t][c].u = kv_load<NTB>(kb + (t * KC + c) * 64 + lane);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int st = 0; st < 2; ++st) vf[dt][st].u = kv_load<NT>(vb + (dt * 2 + st) * 64 + lane);
+          for (int st = 0; st < 2; ++st) vf[dt][st].u = kv_load<NTB>(vb + (dt * 2 + st) * 64 + lane);
+      };
+      if (NT && k >= nt_from) load_kv(std::true_type{});    // wave-uniform branch
+      else load_kv(std::false_type{});
       const int j = k;
       f32x4 sc[4];
       float mt = -INFINITY;
@@ -1268,12 +1277,12 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
       hipLaunchKernelGGL((decode_lean_kernel<DD, true>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q,  \
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
-                         lean_min_per_wave);                                                                     \
+                         lean_min_per_wave, lean_flags >> 8);                                                    \
     else                                                                                                        \
       hipLaunchKernelGGL((decode_lean_kernel<DD, false>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, \
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
-                         lean_min_per_wave);                                                                     \
+                         lean_min_per_wave, 0);                                                                  \
     hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
                        part_o, (bf16*)out, B, Hq, part_stride);                                                  \
   } else {                                                                                                      \
