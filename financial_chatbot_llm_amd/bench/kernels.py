@@ -14,6 +14,7 @@ import math
 import statistics
 from typing import Callable, Dict, List
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -133,14 +134,18 @@ def bench_decode_lean(dev) -> List[Dict]:
         ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
         o = torch.empty_like(q)
 
-        def mk(lean, flags=0):
+        marked_d = torch.from_numpy(A.mark_shared_blocks(tables.numpy().copy(), np.asarray(ctxs))).to(dev)
+
+        def mk(lean, flags=0, bt=tables_d):
             def f():
                 A.DECODE_LEAN, A.LEAN_FLAGS = lean, flags
-                ops.decode(q, lens, tables_d, kc, vc, 0.088, workspace=ws, out=o)
+                ops.decode(q, lens, bt, kc, vc, 0.088, workspace=ws, out=o)
                 A.LEAN_FLAGS = 0
             return f
-        fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1), "lean_nt16": mk(True, 1 | 16 << 8),
-               "lean_nt32": mk(True, 1 | 32 << 8)}
+        # lean_nt: every block non-temporal; lean_ntm: the shared-prefix blocks (marked in the table by
+        # the host, as the engine does) on the default policy, the rest non-temporal
+        fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1), "lean_ntm": mk(True, 1, marked_d),
+               "part_marked": mk(False, 0, marked_d)}
         ref = None
         errs = {}
         for k, f in fns.items():

@@ -518,8 +518,8 @@ __global__ void __launch_bounds__(256) decode_kernel(
       ids = jl < blk1 ? bt[jl] : 0;
     }
     const int j = blk0 + w + 4 * it;
-    const long phys = __builtin_amdgcn_readlane(ids, it & 63);
-    PENNY_DASSERT(phys >= 0);
+    const int id = __builtin_amdgcn_readlane(ids, it & 63);
+    const long phys = id < 0 ? -(long)id - 1 : id;     // < 0: marked shared (decode_lean_kernel)
     const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
     Frag kf[4][KC], vf[DT][2];
@@ -711,9 +711,10 @@ __device__ __forceinline__ LeanPlan lean_plan(int* s_pre, int* s_w, const int* _
 // balanced: 185 vs 140 us at B = 64, profiles/r3_decode_lean_vs_partitioned.jsonl; removed in r5.)
 constexpr int LEAN_META0 = 64;   // meta[LEAN_META0..]: the plan, published for the merge kernel
 
-// K/V fragment load of the lean kernel: default cache policy, or (NT) non-temporal -- the stream is
-// read once per step except the shared-prefix blocks, which keep the default policy (their L2 / MALL
-// reuse across rows): lean_flags bit 0 = NT from block index lean_flags >> 8 of each row
+// K/V fragment load of the lean kernel: default cache policy, or (NT) non-temporal.  A row's own
+// blocks are read once per step; blocks several rows of the step share (the common system prompt --
+// marked in the decode block table as -id - 1 by the host, engine/model_runner.mark_shared_blocks)
+// keep the default policy for their L2 / MALL reuse.  lean_flags bit 0: NT for unmarked blocks.
 template <bool NT>
 __device__ __forceinline__ uint4 kv_load(const uint4* p) {
   if constexpr (NT) {
@@ -730,8 +731,7 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
     const bf16* __restrict__ q, const int* __restrict__ ctx_lens, const int* __restrict__ block_tables,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache, bf16* __restrict__ out,
     float* __restrict__ part_m, float* __restrict__ part_l, float* __restrict__ part_o, int* __restrict__ meta,
-    float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride, int min_per_wave,
-    int nt_from) {
+    float scale_log2, int B, int Hq, int Hkv, int max_blocks, int nparts, int part_stride, int min_per_wave) {
   constexpr int KC = D / 32, DT = D / 16;
   __shared__ int s_pre[LEAN_MAX_B + 1];
   __shared__ int s_w[8];
@@ -782,8 +782,9 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
         const int kl = k + lane;
         ids = kl < k1 ? bt[kl] : 0;
       }
-      const long phys = __builtin_amdgcn_readlane(ids, it & 63);
-      PENNY_DASSERT(phys >= 0);
+      const int id = __builtin_amdgcn_readlane(ids, it & 63);
+      const bool shared = id < 0;                          // marked by the host: several rows read it
+      const long phys = shared ? -(long)id - 1 : id;
       const uint4* kb = reinterpret_cast<const uint4*>(k_cache + (phys * Hkv + h) * (long)(KV_BS * D));
       const uint4* vb = reinterpret_cast<const uint4*>(v_cache + (phys * Hkv + h) * (long)(KV_BS * D));
       Frag kf[4][KC], vf[DT][2];
@@ -798,7 +799,7 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
 #pragma unroll
           for (int st = 0; st < 2; ++st) vf[dt][st].u = kv_load<NTB>(vb + (dt * 2 + st) * 64 + lane);
       };
-      if (NT && k >= nt_from) load_kv(std::true_type{});    // wave-uniform branch
+      if (NT && !shared) load_kv(std::true_type{});    // wave-uniform branch
       else load_kv(std::false_type{});
       const int j = k;
       f32x4 sc[4];
@@ -1277,12 +1278,12 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
       hipLaunchKernelGGL((decode_lean_kernel<DD, true>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q,  \
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
-                         lean_min_per_wave, lean_flags >> 8);                                                    \
+                         lean_min_per_wave);                                                                     \
     else                                                                                                        \
       hipLaunchKernelGGL((decode_lean_kernel<DD, false>), dim3(lean_grid), dim3(256), 0, stream, (const bf16*)q, \
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
-                         lean_min_per_wave, 0);                                                                  \
+                         lean_min_per_wave);                                                                     \
     hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
                        part_o, (bf16*)out, B, Hq, part_stride);                                                  \
   } else {                                                                                                      \

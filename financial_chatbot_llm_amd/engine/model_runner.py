@@ -22,7 +22,8 @@ import torch
 
 from .. import ops
 from ..models.common import AttentionMetadata, KVCache
-from ..ops.attention import KV_BS, DecodeWorkspace, prefill_plan
+from ..ops import attention as _attn
+from ..ops.attention import KV_BS, DecodeWorkspace, mark_shared_blocks, prefill_plan
 from ..parallel import comm
 from ..utils.logging import get_logger
 from ..utils.profiling import marker
@@ -184,8 +185,11 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
     i32 = lambda x: np.asarray(x, np.int32)  # noqa: E731
     cat = lambda parts, tail: np.concatenate(parts + [i32(tail)]) if parts else i32(tail)  # noqa: E731
     src_a = i32(src) if any(x >= 0 for x in src) else None
+    bt_d = _table(tables_d)
+    if _attn.LEAN_FLAGS & 1 and _attn.DECODE_LEAN:
+        mark_shared_blocks(bt_d, ctx_d)          # the lean kernel's cache policy per block
     return StepInputs(cat(ids_parts, ids_d), cat(pos_parts, pos_d), cat(slot_parts, slots_d), i32(cu), i32(ctx_p),
-                      _table(tables_p), max_q, i32(ctx_d), _table(tables_d), np.asarray(logits_idx, np.int64),
+                      _table(tables_p), max_q, i32(ctx_d), bt_d, np.asarray(logits_idx, np.int64),
                       np.asarray(temps, np.float32), np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32),
                       src_a)
 

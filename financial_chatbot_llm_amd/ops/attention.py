@@ -396,7 +396,35 @@ LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
 # lean kernel flags (attention.hip penny_attention_decode lean_flags): bit 0 = non-temporal K/V loads
+# for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks)
 LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "0"))
+MARK_MAX_COLS = 64          # a shared prefix is looked for in the first 64 blocks (4k tokens)
+
+
+def mark_shared_blocks(bt: np.ndarray, ctx: np.ndarray) -> np.ndarray:
+    """Mark, in place as ``-id - 1``, each decode row's leading KV blocks that another row of the same
+    step reads at the same position (the shared prompt prefix the prefix cache deduplicated).  The
+    lean decode kernel keeps the default cache policy for those -- every row sharing them hits L2 /
+    MALL -- and streams each row's own blocks non-temporally.  Every decode attention path decodes
+    the marks."""
+    B, W = bt.shape
+    if B < 2 or W == 0:
+        return bt
+    J = min(W, MARK_MAX_COLS)
+    t = bt[:, :J]
+    o = np.argsort(t, axis=0, kind="stable")
+    srt = np.take_along_axis(t, o, 0)
+    eq = srt[1:] == srt[:-1]
+    d = np.zeros((B, J), bool)
+    d[1:] |= eq
+    d[:-1] |= eq
+    dup = np.empty_like(d)
+    np.put_along_axis(dup, o, d, 0)
+    dup &= np.arange(J)[None, :] < ((np.asarray(ctx) + KV_BS - 1) // KV_BS)[:, None]
+    lead = np.cumprod(dup, axis=1).sum(1)
+    mask = np.arange(J)[None, :] < lead[:, None]
+    t[mask] = -t[mask] - 1
+    return bt
 LEAN_META0 = 64             # lean_meta[64:]: the plan published for the merge (attention.hip LEAN_META0)
 _CU_COUNT = {}
 
@@ -457,6 +485,7 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         return out
     out = torch.empty_like(q) if out is None else out
     ctx = ctx_lens.tolist()
+    block_tables = torch.where(block_tables < 0, -block_tables - 1, block_tables)   # shared-block marks
     for b in range(B):
         k, v = gather_kv_ref(k_cache, v_cache, block_tables[b], ctx[b])
         out[b:b + 1] = _attend_ref(q[b:b + 1], k, v, scale, None).to(q.dtype)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r5 session 27: lean decode with non-temporal K/V loads (A/B) -- decode / engine GPU tests, the lean vs
+# r5 session 27: lean decode with non-temporal K/V loads from a block threshold (A/B) -- decode / engine GPU tests, the lean vs
 # partitioned decode bench.
 set -u
 mkdir -p gpurun_out

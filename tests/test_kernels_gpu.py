@@ -613,6 +613,13 @@ def test_shared_prefix_decode_matches_reference(D, Hq, Hkv, lean, monkeypatch):
     out = ops.decode(q.to(DEV), ctx.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV), scale, workspace=ws)
     ref = ops.decode(q, ctx, tables, kc, vc, scale)
     close(out, ref, atol=2e-2)
+    # the engine's shared-block marks (-id - 1) + non-temporal loads for the unmarked blocks: the
+    # cache policy changes, the result does not (bit-equal), on either decode kernel
+    marked = torch.from_numpy(ops.attention.mark_shared_blocks(tables.numpy().copy(), ctx.numpy()))
+    assert (marked[:40, :10] < 0).all() and (marked[45:] >= 0).all()
+    monkeypatch.setattr(ops.attention, "LEAN_FLAGS", 1)
+    out_m = ops.decode(q.to(DEV), ctx.to(DEV), marked.to(DEV), kc.to(DEV), vc.to(DEV), scale, workspace=ws)
+    assert torch.equal(out_m, out)
 
 
 def _kept_ref(lg, k, p, t):

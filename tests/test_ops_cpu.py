@@ -223,3 +223,23 @@ def test_mx_block_grouping_round_trip_and_fake_quant_bounds():
     err = (moe.mx_blocks(q) - b).abs()
     # e4m3 has 3 mantissa bits: relative rounding <= 2^-4 of the element, or a subnormal step
     assert (err <= b.abs() * 2 ** -4 + torch.exp2(X - 9)[..., None] + 1e-30).all()
+
+
+def test_mark_shared_blocks_and_cpu_decode():
+    """Leading blocks shared with another row at the same position are marked -id - 1 (only inside the
+    rows' contexts); the torch decode path reads marked tables like unmarked ones."""
+    import numpy as np
+    from financial_chatbot_llm_amd.ops.attention import mark_shared_blocks
+    bt = np.array([[5, 6, 7, 8], [5, 6, 9, 0], [5, 10, 11, 12], [13, 14, 15, 16]], np.int32)
+    m = mark_shared_blocks(bt.copy(), np.array([256, 190, 256, 256]))
+    assert m.tolist() == [[-6, -7, 7, 8], [-6, -7, 9, 0], [-6, 10, 11, 12], [13, 14, 15, 16]]
+    assert mark_shared_blocks(bt[:1].copy(), np.array([256])).tolist() == bt[:1].tolist()
+    g = torch.Generator().manual_seed(0)
+    Hq, Hkv, D = 4, 2, 64
+    kc = torch.randn(17, Hkv, 64 * D, generator=g).bfloat16()
+    vc = torch.randn(17, Hkv, 64 * D, generator=g).bfloat16()
+    q = torch.randn(4, Hq, D, generator=g).bfloat16()
+    ctx = torch.tensor([256, 190, 256, 256], dtype=torch.int32)
+    a = ops.decode(q, ctx, torch.from_numpy(bt), kc, vc, 0.125)
+    b = ops.decode(q, ctx, torch.from_numpy(m), kc, vc, 0.125)
+    assert torch.equal(a, b)
