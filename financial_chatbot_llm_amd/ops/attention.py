@@ -396,8 +396,13 @@ LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
 # lean kernel flags (attention.hip penny_attention_decode lean_flags): bit 0 = non-temporal K/V loads
-# for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks)
-LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "0"))
+# for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks).
+# Measured on workload batches (bench/kernels.py decode_lean, profiles/r5_decode_lean_nt_marked_ab.jsonl):
+# -9..-13 % per call at B = 64-256 (-10 % with no shared prefix; every block non-temporal, shared
+# ones included, gains only 3-6 % and loses 3 % on a 2k shared prefix); +4 % at B = 16, so batches
+# below LEAN_NT_MIN_B keep the default policy.  Driver bench 33.29 vs 32.52 turns/s on one box.
+LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "1"))
+LEAN_NT_MIN_B = 32
 MARK_MAX_COLS = 64          # a shared prefix is looked for in the first 64 blocks (4k tokens)
 
 
@@ -479,8 +484,8 @@ def decode(q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor, 
         args = [N.ptr(q), N.ptr(ctx_lens), N.ptr(block_tables), N.ptr(k_cache), N.ptr(v_cache), N.ptr(out),
                 N.ptr(ws.part_m), N.ptr(ws.part_l), N.ptr(ws.part_o), B, Hq, Hkv, D, block_tables.shape[1], pb,
                 nparts, ws.part_stride, float(scale)]
-        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE, LEAN_FLAGS)
-                     if lean else (0, None, 1, 0))
+        lean_args = ((_lean_grid(q.device, Hkv), N.ptr(ws.lean_meta), LEAN_MIN_PER_WAVE,
+                      LEAN_FLAGS if B >= LEAN_NT_MIN_B else LEAN_FLAGS & ~1) if lean else (0, None, 1, 0))
         N.call("penny_attention_decode", *args, *lean_args, N.stream() if stream is None else stream)
         return out
     out = torch.empty_like(q) if out is None else out
