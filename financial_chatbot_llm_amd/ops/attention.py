@@ -406,30 +406,48 @@ LEAN_NT_MIN_B = 32
 MARK_MAX_COLS = 64          # a shared prefix is looked for in the first 64 blocks (4k tokens)
 
 
+@lru_cache(maxsize=1)
+def _runtime():
+    try:
+        from .. import _penny_runtime as rt
+        return rt if hasattr(rt, "mark_shared_blocks") else None
+    except ImportError:
+        return None
+
+
 def mark_shared_blocks(bt: np.ndarray, ctx: np.ndarray) -> np.ndarray:
     """Mark, in place as ``-id - 1``, each decode row's leading KV blocks that another row of the same
     step reads at the same position (the shared prompt prefix the prefix cache deduplicated).  The
     lean decode kernel keeps the default cache policy for those -- every row sharing them hits L2 /
     MALL -- and streams each row's own blocks non-temporally.  Every decode attention path decodes
-    the marks."""
+    the marks.  The native runtime's version (``_penny_runtime.mark_shared_blocks``, ~B log B per
+    column) when built; this numpy form otherwise (same result)."""
     B, W = bt.shape
     if B < 2 or W == 0:
         return bt
+    rt = _runtime()
+    if rt is not None and bt.dtype == np.int32 and bt.flags.c_contiguous:
+        rt.mark_shared_blocks(bt, np.ascontiguousarray(ctx, dtype=np.int32), MARK_MAX_COLS, KV_BS)
+        return bt
     J = min(W, MARK_MAX_COLS)
     t = bt[:, :J]
-    o = np.argsort(t, axis=0, kind="stable")
-    srt = np.take_along_axis(t, o, 0)
+    valid = np.arange(J)[None, :] < ((np.asarray(ctx) + KV_BS - 1) // KV_BS)[:, None]
+    # columns past a row's context are not read: unique negative stand-ins never match
+    key = np.where(valid, t.astype(np.int64), -1 - np.arange(B * J, dtype=np.int64).reshape(B, J))
+    o = np.argsort(key, axis=0, kind="stable")
+    srt = np.take_along_axis(key, o, 0)
     eq = srt[1:] == srt[:-1]
     d = np.zeros((B, J), bool)
     d[1:] |= eq
     d[:-1] |= eq
     dup = np.empty_like(d)
     np.put_along_axis(dup, o, d, 0)
-    dup &= np.arange(J)[None, :] < ((np.asarray(ctx) + KV_BS - 1) // KV_BS)[:, None]
     lead = np.cumprod(dup, axis=1).sum(1)
     mask = np.arange(J)[None, :] < lead[:, None]
     t[mask] = -t[mask] - 1
     return bt
+
+
 LEAN_META0 = 64             # lean_meta[64:]: the plan published for the merge (attention.hip LEAN_META0)
 _CU_COUNT = {}
 

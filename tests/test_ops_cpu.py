@@ -243,3 +243,34 @@ def test_mark_shared_blocks_and_cpu_decode():
     a = ops.decode(q, ctx, torch.from_numpy(bt), kc, vc, 0.125)
     b = ops.decode(q, ctx, torch.from_numpy(m), kc, vc, 0.125)
     assert torch.equal(a, b)
+
+
+def test_mark_shared_blocks_native_matches_numpy():
+    """The runtime's C++ marking and the numpy form agree on prefix-closed tables (disjoint groups of
+    rows sharing a leading run, contexts of any length)."""
+    import numpy as np
+    from financial_chatbot_llm_amd.ops import attention as A
+    if A._runtime() is None:
+        import pytest
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(1)
+    for _ in range(100):
+        B, W = int(rng.integers(2, 160)), int(rng.integers(1, 100))
+        bt = rng.permutation(B * W + 1000)[:B * W].reshape(B, W).astype(np.int32)
+        rows = rng.permutation(B)
+        i = 0
+        while i < B - 1:
+            n = int(rng.integers(2, 9))
+            grp = rows[i:i + n]
+            L = int(rng.integers(1, W + 1))
+            bt[grp, :L] = bt[grp[0], :L]
+            i += n
+        ctx = rng.integers(0, W * 64 + 1, B).astype(np.int32)
+        native = A.mark_shared_blocks(bt.copy(), ctx)
+        orig = A._runtime
+        try:
+            A._runtime = lambda: None
+            ref = A.mark_shared_blocks(bt.copy(), ctx)
+        finally:
+            A._runtime = orig
+        assert np.array_equal(native, ref)
