@@ -1390,7 +1390,10 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "chunked_prefill": bench_chunked_prefill,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair,
+                "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",
+                                                                  "70b_tp8_gate_up", "70b_tp8_down"),
+                                                        Ms=(96, 112, 128, 144, 160, 192, 256)), "chunked_prefill": bench_chunked_prefill,
                 "shard_shapes_tp8": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp8" in n]),
                 "shard_shapes_tp1": lambda d: bench_shard_shapes(d, [n for n in SHARD_SHAPES if "tp1" in n]),
                 "lm_head_stream": bench_lm_head_stream, "decode_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down"), Ms=(32, 64, 96, 128, 160, 192, 256), prefill_Ms=()), "gateup_shapes": lambda d: bench_shard_shapes(d, names=("70b_tp8_gate_up", "70b_tp1_gate_up", "8b_gate_up"), prefill_Ms=()),
