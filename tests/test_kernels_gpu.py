@@ -432,6 +432,20 @@ def test_splitk_kernels_token_chunks(M):
         assert torch.equal(gemm.gateup_silu(x, wi, N_, nf, rowmajor=True), yg)
 
 
+def test_linear_tp8_o_shard_small_prefill_on_chunked_kernel(monkeypatch):
+    """The 70B TP=8 O shard at a 384-row prefill step takes the chunked bf16 decode kernel (policy K4)
+    and equals the fp32 reference; the library form agrees."""
+    from financial_chatbot_llm_amd.ops import gemm
+    monkeypatch.delenv("PENNY_PREFILL_GEMM", raising=False)
+    assert gemm.prefill_choice(384, 8192, 1024, None) == "K4"
+    g = torch.Generator().manual_seed(31)
+    x = rnd(384, 1024, gen=g).to(DEV)
+    w = rnd(8192, 1024, scale=0.03, gen=g).to(DEV)
+    y = gemm.linear(x, w)
+    close(y, x.float() @ w.float().t(), atol=2e-2)
+    close(y, torch.nn.functional.linear(x, w), atol=2e-2)
+
+
 @pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])
 def test_splitk_rowmajor_tp_and_70b_shapes(N_, K, S, nf):
     """The table shapes that stream the row-major weight (70B, TP=8 shards) vs the fp32 reference."""
