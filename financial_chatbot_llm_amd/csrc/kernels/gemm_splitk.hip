@@ -160,8 +160,7 @@ __global__ void __launch_bounds__(256, 1) splitk_gemm_kernel(const bf16* __restr
   static_assert(NF % WA == 0 && MT % WB == 0, "wave split");
   static_assert(!SILU || FW % 2 == 0, "SiLU epilogue needs (gate, up) row-group pairs per wave");
   constexpr int NBUF = Ring<NF, MT, RKB, MAXB, BKM>::NBUF;   // ring slots of BKM stages each
-  // paired slots may double-buffer (one slot = two stages in flight while the other is consumed)
-  static_assert(NBUF >= (BKM > 1 ? 2 : 3), "ring too shallow");
+  static_assert(NBUF >= 3, "ring too shallow");
   constexpr int WBYTES = NF * 2 * 1024;        // W pieces of one BK=64 stage
   constexpr int XBYTES = MT * 2 * 1024;        // X pieces (16*MT rows x 128 B)
   constexpr int SBYTES = WBYTES + XBYTES;
@@ -369,11 +368,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 }
 
 // wrow bit 0: W is the row-major [N, K] weight (else tile_weight's fragment-tiled copy); bit 1: BK=64
-// stages issued in pairs (BKM = 2) -- taken where the ring still holds >= 2 slots (double-buffered
-// pairs for the widest tiles) and each K slice is a multiple of 128, else single stages
+// stages issued in pairs (BKM = 2) -- taken where the ring still holds >= 3 slots and each K slice
+// is a multiple of 128, else single stages.  (A double-buffered pair ring -- two slots, for the
+// widest tiles at M 97-256 -- measured 3-14 % slower than single stages:
+// profiles/r5_decode_gemm_pair_double_buffer_rejected.jsonl.)
 template <int NF, int MT, int RKB, int MAXB>
 constexpr bool pair_fits() {
-  return Ring<NF, MT, RKB, MAXB, 2>::NBUF >= 2;
+  return Ring<NF, MT, RKB, MAXB, 2>::NBUF >= 3;
 }
 
 // one launch of splitk_gemm_kernel<NF, MT, WA, EPI, *, 150, MAXB, *> with the W layout / stage pairing
