@@ -1211,6 +1211,38 @@ def bench_chunked_prefill(dev, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_
     return out
 
 
+def bench_gemm_group(dev, Ms=(1024, 2048, 2560, 3072, 4096), groups=(1, 2, 4, 8, 16)) -> List[Dict]:
+    """The tile GEMM's L2 grouping (token tiles per group of each XCD's tile range; gemm_prefill.hip
+    GM = 4) swept on the Llama-3-8B prefill projections with their production epilogues, interleaved
+    per M."""
+    from ..ops import gemm
+    from ..ops import _native as Nn
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    shapes = {"gate_up": (28672, 4096, "silu"), "down": (4096, 14336, "residual"), "qkv": (6144, 4096, None),
+              "o": (4096, 4096, "residual")}
+    for name, (N, K, epi) in shapes.items():
+        w = rnd(N, K)
+        for M in Ms:
+            x = rnd(M, K)
+            r = rnd(M, N) if epi == "residual" else None
+
+            def mk(g):
+                def f():
+                    Nn.call("penny_gemm_prefill_set_group", g)
+                    gemm.prefill_gemm(x, w, epi, residual=r, out=r if epi == "residual" else None)
+                    Nn.call("penny_gemm_prefill_set_group", 0)
+                return f
+            t = interleaved({f"gm{g}": mk(g) for g in groups}, rounds=5, iters=10)
+            fl = 2 * M * N * K
+            row = {"op": "gemm_group", "name": name, "M": M, "N": N, "K": K,
+                   **{k: round(v, 1) for k, v in t.items()},
+                   "best": min(t, key=t.get), "gm4_TF": round(fl / t["gm4"] / 1e6, 1)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+    return out
+
+
 def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
                        prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
     """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
@@ -1390,7 +1422,7 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",
                                                                   "70b_tp8_gate_up", "70b_tp8_down"),
                                                         Ms=(96, 112, 128, 144, 160, 192, 256)), "chunked_prefill": bench_chunked_prefill,

@@ -104,6 +104,7 @@ struct TailArgs {
   int dpn, L, s;
   float* part;
   int* cnt;
+  int gm = 0;             // token tiles per L2 group (0: GM); penny_gemm_prefill_set_group (A/B)
 };
 
 struct RopeArgs {
@@ -281,8 +282,9 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
     s = id / tiles;
     tile = id - s * tiles;
   }
-  const int grp = tile / (GM * Nt), first = grp * GM, gm = min(Mt - first, GM);
-  const int within = tile - grp * GM * Nt;
+  const int GMr = ta.gm > 0 ? ta.gm : GM;
+  const int grp = tile / (GMr * Nt), first = grp * GMr, gm = min(Mt - first, GMr);
+  const int within = tile - grp * GMr * Nt;
   const int tm = first + within % gm, tn = within / gm;
   int m0 = tm * TM, mend = M, e = 0;
   const int n0 = tn * TN;
@@ -791,9 +793,13 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
 
 }  // namespace
 
+// token tiles per L2 group of the bf16 launches below (0: GM); an A/B knob (bench/kernels.py gemm_group)
+static int g_group = 0;
+
 template <int EPI, int ABL = 0, int BAL = 1>
 static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
-                   const void* R, int ldr, int M, int N, int S, const RopeArgs& ra, const TailArgs& ta = TailArgs{}) {
+                   const void* R, int ldr, int M, int N, int S, const RopeArgs& ra, TailArgs ta = TailArgs{}) {
+  ta.gm = g_group;
   hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy,
                      (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{}, ta);
 }
@@ -817,6 +823,12 @@ static dim3 tail_plan(int M, int N, int K, int cus, float* ws, long ws_floats, i
     }
   }
   return dim3((unsigned)T);
+}
+
+PENNY_API int penny_gemm_prefill_set_group(int gm) {
+  if (gm < 0 || gm > 64) return (int)hipErrorInvalidValue;
+  g_group = gm;
+  return 0;
 }
 
 // Contract (checked): N % 256 == 0, K % (64*S) == 0, ldx % 8 == 0, rows 16-B aligned; EPI_SILU

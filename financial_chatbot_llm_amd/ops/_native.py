@@ -55,6 +55,7 @@ _SIGS = {
     "penny_attention_prefill": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P,
                                 c_int, P],
     "penny_attention_prefill_variant": [c_int],
+    "penny_gemm_prefill_set_group": [c_int],
     "penny_attention_prefill_lean": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P, P, c_int, P,
                                      c_int, P, P, P],
     "penny_splitk_reduce_silu": [P, c_int, c_int, c_int, P, c_int, P],
