@@ -63,7 +63,9 @@ constexpr int TM = 256;              // token rows per tile
 constexpr int BK = 64;               // K per stage
 constexpr int HALF = 128 * 128;      // half-tile: 128 rows x 64 bf16 = 16 KiB
 constexpr int BUF = 4 * HALF;        // one K-tile (both operands)
-constexpr int GM = 4;                // token tiles per L2 group
+constexpr int GM = 4;                // token tiles per L2 group (r5 sweep of 1-16 on the 8B prefill
+                                     // projections: 4 within ~1 % of the best everywhere,
+                                     // profiles/r5_tile_gemm_l2_group_sweep.jsonl)
 enum { H_W0 = 0, H_X0 = 1, H_X1 = 2, H_W1 = 3 };
 enum { EPI_BF16 = 0, EPI_SILU = 1, EPI_SLAB = 2, EPI_RESID = 3, EPI_ROPE = 4, EPI_BIAS = 5, EPI_BIAS_GELU = 6,
        EPI_MOE_SILU = 7, EPI_MOE_ROUTE = 8, EPI_SAMPLE = 9, EPI_MOE_SILU_MX = 10, EPI_MOE_ROUTE_MX = 11 };
