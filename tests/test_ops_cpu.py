@@ -274,3 +274,18 @@ def test_mark_shared_blocks_native_matches_numpy():
         finally:
             A._runtime = orig
         assert np.array_equal(native, ref)
+
+
+def test_paired_stage_table(monkeypatch):
+    """W-layout flags of the decode GEMMs: bit 0 row-major, bit 1 paired stages -- per the PAIRED table
+    up to its row limit, always / never under PAIR_MODE 1 / 0."""
+    from financial_chatbot_llm_amd.ops import gemm
+    monkeypatch.setattr(gemm, "PAIR_MODE", "table")
+    assert gemm._wrow(False, 64, 4096, 4096) == 2 and gemm._wrow(True, 64, 4096, 4096) == 3
+    assert gemm._wrow(False, 129, 4096, 4096) == 0 and gemm._wrow(True, 200, 4096, 4096) == 1
+    assert gemm._wrow(True, 16, 57344, 8192) == 3 and gemm._wrow(True, 17, 57344, 8192) == 1
+    assert gemm._wrow(False, 8, 1000, 1000) == 0            # unmeasured shape
+    monkeypatch.setattr(gemm, "PAIR_MODE", "1")
+    assert gemm._wrow(False, 256, 1000, 1000) == 2
+    monkeypatch.setattr(gemm, "PAIR_MODE", "0")
+    assert gemm._wrow(True, 8, 4096, 4096) == 1
