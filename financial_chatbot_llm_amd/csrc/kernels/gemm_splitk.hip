@@ -489,7 +489,9 @@ PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int
 
 // Shape contract (checked): N % (16*NF) == 0, K % (64*S) == 0, X rows 16-B
 // aligned (ldx % 8 == 0).  wrow: bit 0 row-major W instead of tile_weight's copy, bit 1 paired stages.  nf: W row groups per workgroup (2, 4, 6 or 8;
-// 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4).  P is [S, M, N] f32.
+// 6 = 96 rows puts N = 6144 on exactly 64 tiles, i.e. 256 workgroups at S = 4; 16 -- half the X
+// bytes per W byte -- measured 5-53 % slower at M = 32-128 on every 8B / TP=8 shape: too few
+// workgroups, profiles/r5_decode_gemm_nf16_rejected.jsonl).  P is [S, M, N] f32.
 // M > 256: 256-row token chunks side by side on grid y (small prefill steps of narrow TP shards).
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
                                 int wrow, hipStream_t stream) {
