@@ -1243,63 +1243,6 @@ def bench_gemm_group(dev, Ms=(1024, 2048, 2560, 3072, 4096), groups=(1, 2, 4, 8,
     return out
 
 
-def bench_nf16(dev, names=("8b_gate_up", "8b_down", "8b_qkv", "8b_o", "70b_tp8_gate_up", "70b_tp8_qkv"),
-               Ms=(32, 64, 96, 112, 128)) -> List[Dict]:
-    """256-row workgroups (nf = 16: half the X bytes per W byte of nf = 8 through LDS) vs the table's
-    decode configs, interleaved, W rotated over >= 768 MB, in the layout the model streams."""
-    from ..ops import gemm
-    out = []
-    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
-    for name in names:
-        N, K, kind = SHARD_SHAPES[name]
-        rm = not gemm.uses_tiled_weight(N, K)
-        copies = max(2, min(16, (768 << 20) // (N * K * 2)))
-        ws = [rnd(N, K) for _ in range(copies)]
-        if not rm:
-            ws = [gemm.tile_weight(w) for w in ws]
-        it = [0]
-
-        def nxt():
-            it[0] = (it[0] + 1) % copies
-            return it[0]
-        for M in Ms:
-            x = rnd(M, K)
-            fns = {}
-            if kind == "gateup":
-                nf = gemm.gateup_config(M, N, K)
-                if nf is not None:
-                    fns["table"] = lambda nf=nf: gemm.gateup_silu(x, ws[nxt()], N, nf, rowmajor=rm)
-                else:
-                    S0, nf0, _ = gemm.gateup_splitk_config(M, N, K)
-                    P0 = torch.empty((S0, M, N), dtype=torch.float32, device=dev)
-                    fns["table"] = lambda: gemm.gateup_splitk(x, ws[nxt()], N, S0, nf0, rowmajor=rm, slabs=P0)
-                if N % 256 == 0:
-                    fns["gu_nf16"] = lambda: gemm.gateup_silu(x, ws[nxt()], N, 16, rowmajor=rm)
-                for S in (2, 4):
-                    if N % 512 == 0 and K % (64 * S) == 0:
-                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
-                        fns[f"guS{S}nf16"] = (lambda S=S, P=P: gemm.gateup_splitk(x, ws[nxt()], N, S, 16,
-                                                                                  rowmajor=rm, slabs=P))
-            else:
-                S0, nf0 = gemm.splitk_config(M, N, K)
-                P0 = torch.empty((S0, M, N), dtype=torch.float32, device=dev)
-                fns["table"] = lambda: gemm.splitk_partials(x, ws[nxt()], N, S0, nf0, out=P0, rowmajor=rm)
-                for S in (2, 4, 8):
-                    if N % 256 == 0 and K % (64 * S) == 0:
-                        P = torch.empty((S, M, N), dtype=torch.float32, device=dev)
-                        fns[f"S{S}nf16"] = (lambda S=S, P=P: gemm.splitk_partials(x, ws[nxt()], N, S, 16, out=P,
-                                                                                   rowmajor=rm))
-            t = interleaved(fns, rounds=5, iters=copies)
-            best = min((k for k in t if k != "table"), key=lambda k: t[k], default="table")
-            row = {"op": "nf16", "name": name, "M": M, **{k: round(v, 1) for k, v in t.items()},
-                   "best_nf16": best, "gain": round(t["table"] / t[best], 3)}
-            print(json.dumps(row), flush=True)
-            out.append(row)
-        del ws
-        torch.cuda.empty_cache()
-    return out
-
-
 def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
                        prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
     """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
@@ -1479,7 +1422,7 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "nf16": bench_nf16, "gemm_group": bench_gemm_group,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",
                                                                   "70b_tp8_gate_up", "70b_tp8_down"),
                                                         Ms=(96, 112, 128, 144, 160, 192, 256)), "chunked_prefill": bench_chunked_prefill,

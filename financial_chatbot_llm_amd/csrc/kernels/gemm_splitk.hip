@@ -452,18 +452,9 @@ extern "C" int penny_lm_sample_final(const float* pv, const int* pi, int P, int 
 PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, int M, int N,
                                      int nf, int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > (1 << 20) || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8 && nf != 16) ||
-      N % (16 * nf))
+  if (M > (1 << 20) || K % 64 || ldx % 8 || ldy % 4 || (nf != 2 && nf != 4 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
   const int mt = min((M + 15) / 16, 16);   // > 256 rows: 256-row token chunks on grid y
-  // nf = 16 (256 W rows per workgroup, M <= 128): half the X bytes per W byte through LDS of nf = 8
-  if (nf == 16) {
-    if (mt <= 2) return launch_silu<16, 2, 2>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
-    if (mt <= 4) return launch_silu<16, 4, 2>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
-    if (mt <= 6) return launch_silu<16, 6, 2>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
-    if (mt <= 8) return launch_silu<16, 8, 2>(X, ldx, Wt, K, Y, ldy, M, N, wrow, stream);
-    return (int)hipErrorInvalidValue;
-  }
   // nf = 2 (one (gate, up) pair per workgroup, WA = 1): twice the workgroups of nf = 4 for narrow
   // TP shards (Llama-3-70B TP=8 gate|up: N = 7168 -> 224 workgroups)
   if (nf == 2) {   // WA = 1 -> 4 token-tile wave columns: token tiles rounded up to a multiple of 4
@@ -496,18 +487,10 @@ PENNY_API int penny_gateup_silu_gemm(const void* X, int ldx, const void* Wt, int
 PENNY_API int penny_splitk_gemm(const void* X, int ldx, const void* Wt, int K, void* P, int M, int N, int S, int nf,
                                 int wrow, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > (1 << 20) || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8 && nf != 16) ||
-      N % (16 * nf))
+  if (M > (1 << 20) || S < 1 || K % (64 * S) || ldx % 8 || (nf != 2 && nf != 4 && nf != 6 && nf != 8) || N % (16 * nf))
     return (int)hipErrorInvalidValue;
   const int mt = min((M + 15) / 16, 16);   // > 256 rows: 256-row token chunks on grid y
   float* p = static_cast<float*>(P);
-  if (nf == 16) {   // 256 W rows per workgroup (M <= 128): half the X bytes per W byte of nf = 8
-    if (mt <= 2) return launch<16, 2, 2>(X, ldx, Wt, K, p, M, N, S, wrow, stream);
-    if (mt <= 4) return launch<16, 4, 2>(X, ldx, Wt, K, p, M, N, S, wrow, stream);
-    if (mt <= 6) return launch<16, 6, 2>(X, ldx, Wt, K, p, M, N, S, wrow, stream);
-    if (mt <= 8) return launch<16, 8, 2>(X, ldx, Wt, K, p, M, N, S, wrow, stream);
-    return (int)hipErrorInvalidValue;
-  }
 #define SK_CASE(MT_, WA2_, WA4_, WA8_)                                                 \
   if (mt <= MT_) {                                                                     \
     if (nf == 2) return launch<2, MT_, WA2_>(X, ldx, Wt, K, p, M, N, S, wrow, stream); \

@@ -403,29 +403,6 @@ def test_splitk_gemm(M, S, nf):
     close(P2, ref_p, atol=1e-3)
 
 
-@pytest.mark.parametrize("M", [3, 40, 100, 128])
-def test_splitk_nf16(M):
-    """256-row workgroups (nf = 16) on the split-K slabs and the fused gate|up vs fp32 and vs nf = 8
-    (same k order: bit-equal), tiled and row-major W."""
-    from financial_chatbot_llm_amd.ops import gemm
-    g = torch.Generator().manual_seed(23)
-    N_, K = 512, 2048
-    x = rnd(M, K, gen=g).to(DEV)
-    w = rnd(N_, K, scale=0.05, gen=g).to(DEV)
-    wt = gemm.tile_weight(w)
-    for S in (1, 2, 4):
-        P = gemm.splitk_partials(x, wt, N_, S, 16)
-        close(P.sum(0), x.float() @ w.float().t(), atol=2e-3)
-        assert torch.equal(P, gemm.splitk_partials(x, wt, N_, S, 8))
-        assert torch.equal(gemm.splitk_partials(x, w, N_, S, 16, rowmajor=True), P)
-    gate, up = rnd(N_ // 2, K, scale=0.05, gen=g).to(DEV), rnd(N_ // 2, K, scale=0.05, gen=g).to(DEV)
-    wi = gemm.interleave16(gate, up).contiguous()
-    y = gemm.gateup_silu(x, gemm.tile_weight(wi), N_, 16)
-    close(y, torch.nn.functional.silu(x.float() @ gate.float().t()) * (x.float() @ up.float().t()), atol=3e-2)
-    assert torch.equal(y, gemm.gateup_silu(x, gemm.tile_weight(wi), N_, 8))
-    assert torch.equal(gemm.gateup_silu(x, wi, N_, 16, rowmajor=True), y)
-
-
 @pytest.mark.parametrize("M", [257, 600, 1100])
 def test_splitk_kernels_token_chunks(M):
     """M > 256 on the decode kernels: 256-row token chunks side by side (grid y) -- slabs, bf16 output
