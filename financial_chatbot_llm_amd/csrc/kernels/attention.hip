@@ -1149,7 +1149,10 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   if (nitems <= 0) return 0;
   if (Hq % Hkv || (256 % (Hq / Hkv)) || !items || (nmerge > 0 && (!merge || !part_o || !part_ml)))
     return (int)hipErrorInvalidValue;
-  const float sl2 = scale * LOG2E;
+  // causal bit 1: q arrives prescaled by scale * log2(e) (penny_gemm_prefill_qkv_rope qscale)
+  const bool qpre = causal & 2;
+  causal &= 1;
+  const float sl2 = qpre ? 1.f : scale * LOG2E;
   const PrefillLean lean{items, part_o, part_ml};
   const int var = prefill_variant();
   const dim3 grid(Hkv, nitems, 1);
@@ -1158,7 +1161,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                      (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
                      (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
 #define LEAN_VARIANTS(DD)                                   \
-  if (var == 6) LEAN_LAUNCH(DD, true, true, 2);             \
+  if (var == 6 || qpre) LEAN_LAUNCH(DD, true, true, 2);    \
   else if (var == 4) LEAN_LAUNCH(DD, true, true, 0);        \
   else LEAN_LAUNCH(DD, true, true, 1);                      \
   if (nmerge > 0)                                           \
@@ -1206,7 +1209,12 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv;
   if (G > 128 || (128 % G)) return (int)hipErrorInvalidValue;
-  const float sl2 = scale * LOG2E;
+  // causal bit 1: q arrives prescaled by scale * log2(e) at its one bf16 rounding (the fused QKV
+  // epilogue's qscale): the big tiles then run the prescaled-Q fold (variant 6's loop without its
+  // in-kernel re-rounding of q * c -- it multiplies by 1), the exact scores of variant 5
+  const bool qpre = causal & 2;
+  causal &= 1;
+  const float sl2 = qpre ? 1.f : scale * LOG2E;
   // > 128 rows per (sequence, kv head): the 8-wave pipelined kernel; short chunks keep the
   // 4-wave tile (a 256-row tile would be mostly padding)
   const bool big = (long)max_q_len * G > 128;
@@ -1222,7 +1230,7 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   const dim3 grid2 = wl ? dim3(Hkv, nwork, 1) : dim3(Hkv, ntiles, num_seqs);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && pp_env == 6)                                                                                        \
+  if (big && (pp_env == 6 || qpre))                                                                              \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \

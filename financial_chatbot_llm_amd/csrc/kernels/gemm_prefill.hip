@@ -117,6 +117,9 @@ struct RopeArgs {
   bf16* k_cache;          // [num_blocks, Hkv, 64 * 128]
   bf16* v_cache;
   int Hq, Hkv;
+  // rotated q is stored as bf16(q * qscale): with qscale = softmax scale * log2(e) the attention
+  // kernels take q prescaled at its one rounding (no second bf16 rounding of q * c)
+  float qscale = 1.f;
 };
 
 // LDS row swizzle of 16-B chunks, per fragment-read pattern (ds_read_b128 16-lane phases, 2 rows
@@ -708,6 +711,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       const int off = slot >= 0 ? slot % KV_BS : 0;
       if (hd < ra.Hq + ra.Hkv) {
         const float* cs = ra.cos_sin + (long)ra.positions[m] * D;
+        const float qs = hd < ra.Hq ? ra.qscale : 1.f;
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
           const int d = f * 16 + 4 * g;       // this lane's dims d..d+3 and d+64..d+67
@@ -717,8 +721,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
           for (int r = 0; r < 4; ++r) {
             // GEMM output rounded to bf16 first, as the unfused GEMM -> rope_kv path does
             const float x1 = (float)(bf16)acc[f][t][r], x2 = (float)(bf16)acc[f + 4][t][r];
-            o1[r] = (bf16)(x1 * co[r] - x2 * si[r]);
-            o2[r] = (bf16)(x2 * co[r] + x1 * si[r]);
+            o1[r] = (bf16)((x1 * co[r] - x2 * si[r]) * qs);
+            o2[r] = (bf16)((x2 * co[r] + x1 * si[r]) * qs);
           }
           if (hd < ra.Hq) {
             bf16* q = ra.q_out + ((long)m * ra.Hq + hd) * D;
@@ -870,13 +874,14 @@ PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, v
 // Contract (checked): N == (Hq + 2*Hkv)*128, N % 256 == 0, K % 64 == 0, ldx % 8 == 0.
 PENNY_API int penny_gemm_prefill_qkv_rope(const void* X, int ldx, const void* W, int K, int M, const int* positions,
                                           const float* cos_sin, const int* slots, void* q_out, void* k_cache,
-                                          void* v_cache, int Hq, int Hkv, float* tail_ws, long tail_ws_floats,
+                                          void* v_cache, int Hq, int Hkv, float qscale, float* tail_ws,
+                                          long tail_ws_floats,
                                           int* tail_cnt, int tail_ncnt, int cus, hipStream_t stream) {
   if (M <= 0) return 0;
   const int N = (Hq + 2 * Hkv) * 128;
   if (Hq <= 0 || Hkv <= 0 || N % TN || K % BK || ldx % 8 || !positions || !cos_sin || !slots || !q_out)
     return (int)hipErrorInvalidValue;
-  const RopeArgs ra{positions, cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv};
+  const RopeArgs ra{positions, cos_sin, slots, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, qscale};
   TailArgs ta{};
   const dim3 grid = tail_plan(M, N, K, cus, tail_ws, tail_ws_floats, tail_cnt, tail_ncnt, ta);
   launch<EPI_ROPE>(grid, stream, X, ldx, W, K, nullptr, 0, nullptr, 0, M, N, 1, ra, ta);

@@ -46,6 +46,10 @@ from .configs import ModelConfig
 # mixed prefill+decode steps overlap the two attention kernels on two streams (PENNY_ATTN_OVERLAP=0:
 # one stream, prefill then decode)
 ATTN_OVERLAP = os.environ.get("PENNY_ATTN_OVERLAP", "1") != "0"
+# fused-QKV prefill steps hand the attention q prescaled by scale * log2(e) (ops.gemm.prefill_qkv_rope
+# qscale; ops.prefill q_prescaled); PENNY_PRESCALE_Q=0 keeps q unscaled (A/B)
+PRESCALE_Q = os.environ.get("PENNY_PRESCALE_Q", "0") != "0"
+LOG2E = 1.4426950408889634
 
 
 class DecoderModel:
@@ -217,10 +221,18 @@ class DecoderModel:
         p = f"layers.{i}."
         T = h.shape[0]
         kc, vc = kv.k(i), kv.v(i)
+        scale, qpre = self.scale, False
         if qkv_rope_fused(h, self.w[p + "qkv"], self.D):
-            # prefill step: QKV GEMM with RoPE + paged KV write in its epilogue (K3+K4+K5, one pass)
+            # prefill step: QKV GEMM with RoPE + paged KV write in its epilogue (K3+K4+K5, one pass).
+            # PRESCALE_Q: q leaves it times scale * log2(e) at its one bf16 rounding, so the prefill
+            # attention's block loop needs no per-score multiply (the prescaled-Q fold) without the
+            # extra rounding of q * c that its in-kernel form pays; every attention call of the step
+            # then takes scale 1 / log2(e)
+            qpre = PRESCALE_Q and h.is_cuda
             q = prefill_qkv_rope(h, self.w[p + "qkv"], positions, self.cos_sin, meta.slots, kc, vc, self.hq,
-                                 self.hkv)
+                                 self.hkv, qscale=self.scale * LOG2E if qpre else 1.0)
+            if qpre:
+                scale = 1.0 / LOG2E
         else:
             # QKV is column-parallel: even under TP its split-K slabs go straight to the RoPE/KV-write
             # pass (no all-reduce in between), unlike the row-parallel O / down projections
@@ -240,17 +252,17 @@ class DecoderModel:
             ev_fork, ev_join = fork_join_events(q.device)
             ev_fork.record(main)
             side.wait_event(ev_fork)
-            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
+            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, scale,
                        workspace=meta.decode_ws, out=attn[tp:], stream=side.cuda_stream)
         if tp > 0:
-            ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, self.scale,
+            ops.prefill(q[:tp], meta.cu_q, meta.ctx_lens_p, meta.block_tables_p, kc, vc, scale,
                         causal=meta.causal, max_q_len=meta.max_q_len, out=attn[:tp], work=meta.prefill_work,
-                        lean=meta.prefill_lean)
+                        lean=meta.prefill_lean, q_prescaled=qpre)
         if side is not None:
             ev_join.record(side)
             main.wait_event(ev_join)
         elif meta.num_decode > 0:
-            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, self.scale,
+            ops.decode(q[tp:], meta.ctx_lens_d, meta.block_tables_d, kc, vc, scale,
                        workspace=meta.decode_ws, out=attn[tp:])
         out = linear(attn.view(T, self.hq * self.D), self.w[p + "o"], wt=self.wt.get(p + "o"),
                      slabs=self.tp_size == 1, fuse_residual=fuse_residual)

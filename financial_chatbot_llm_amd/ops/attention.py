@@ -295,14 +295,17 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
             k_cache: torch.Tensor, v_cache: torch.Tensor, scale: float, causal: bool = True,
             max_q_len: Optional[int] = None, out: Optional[torch.Tensor] = None,
             lse: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
-            lean: Optional[Tuple[int, int, int]] = None) -> torch.Tensor:
+            lean: Optional[Tuple[int, int, int]] = None, q_prescaled: bool = False) -> torch.Tensor:
     """Varlen paged attention for the new tokens of S sequences (chunked prefill / prefix hits:
     query i of sequence s sits at absolute position ctx_lens[s] - q_len[s] + i).  ``lse`` [T, Hq]
     f32 (optional) receives each row's natural-log sum-exp of the scaled scores (-inf: no key
     visible) -- what a ring-attention merge needs.  ``work``: :func:`prefill_work_list` of the same
     step on the device (optional; LPT tile order), or :func:`prefill_lean_list`'s split-KV list
-    (``lean`` = its (items, merges, slots) counts, read from the header when not given)."""
+    (``lean`` = its (items, merges, slots) counts, read from the header when not given).
+    ``q_prescaled``: q already carries ``scale * log2(e)`` (``prefill_qkv_rope(qscale=...)``) and
+    ``scale`` is ``1 / log2(e)``; the big tiles then run the prescaled-Q fold."""
     T, Hq, D = q.shape
+    flags = int(causal) | (2 if q_prescaled else 0)
     Hkv = k_cache.shape[1]
     S = block_tables.shape[0]
     assert k_cache.shape[-1] == KV_BS * D
@@ -314,14 +317,14 @@ def prefill(q: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_t
             po, pml = _lean_workspace(q.device, max(nslots, 1), Hkv, D)
             N.call("penny_attention_prefill_lean", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),
                    N.ptr(k_cache), N.ptr(v_cache), N.ptr(out), Hq, Hkv, D, block_tables.shape[1], float(scale),
-                   int(causal), N.ptr(lse) if lse is not None else None, N.ptr(work[1:]), int(ni),
+                   flags, N.ptr(lse) if lse is not None else None, N.ptr(work[1:]), int(ni),
                    N.ptr(work[1 + ni:]) if nm else None, int(nm), N.ptr(po), N.ptr(pml), N.stream())
             return out
         if max_q_len is None:
             max_q_len = int((cu_q[1:] - cu_q[:-1]).max().item())
         N.call("penny_attention_prefill", N.ptr(q), N.ptr(cu_q), N.ptr(ctx_lens), N.ptr(block_tables),
                N.ptr(k_cache), N.ptr(v_cache), N.ptr(out), S, int(max_q_len), Hq, Hkv, D, block_tables.shape[1],
-               float(scale), int(causal), N.ptr(lse) if lse is not None else None,
+               float(scale), flags, N.ptr(lse) if lse is not None else None,
                N.ptr(work) if work is not None else None, int(work.shape[0]) if work is not None else 0, N.stream())
         return out
     out = torch.empty_like(q) if out is None else out

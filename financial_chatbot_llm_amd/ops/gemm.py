@@ -649,17 +649,25 @@ def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, gelu: bool = 
 
 def prefill_qkv_rope(x: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                      slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, Hq: int,
-                     Hkv: int) -> torch.Tensor:
+                     Hkv: int, qscale: float = 1.0) -> torch.Tensor:
     """Fused QKV projection + RoPE + paged KV write (head dim 128) on the prefill tile kernel:
-    returns the rotated q [M, Hq, 128]; k / v land in the caches (slots < 0 are skipped)."""
+    returns the rotated q [M, Hq, 128] -- times ``qscale`` before its one bf16 rounding (the
+    attention's prescaled-q form) -- while k / v land in the caches (slots < 0 are skipped)."""
     from .attention import rope_kv_write
     M, K = x.shape
     if not N.use_native(x):
-        return rope_kv_write(F.linear(x.float(), w.float()).to(x.dtype), positions, cos_sin, slots, k_cache,
-                             v_cache, Hq, Hkv, 128)
+        if qscale == 1.0:
+            return rope_kv_write(F.linear(x.float(), w.float()).to(x.dtype), positions, cos_sin, slots, k_cache,
+                                 v_cache, Hq, Hkv, 128)
+        from .attention import _rope_ref
+        qkv = F.linear(x.float(), w.float()).to(x.dtype)
+        rope_kv_write(qkv, positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, 128)
+        qr = _rope_ref(qkv[:, :Hq * 128].float().view(M, Hq, 128), positions, cos_sin)   # f32
+        return (qr * qscale).to(x.dtype)
     q = torch.empty((M, Hq, 128), dtype=x.dtype, device=x.device)
     N.call("penny_gemm_prefill_qkv_rope", N.ptr(x), x.stride(0), N.ptr(w), K, M, N.ptr(positions), N.ptr(cos_sin),
-           N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache), Hq, Hkv, *tail_workspace(x.device), N.stream())
+           N.ptr(slots), N.ptr(q), N.ptr(k_cache), N.ptr(v_cache), Hq, Hkv, float(qscale), *tail_workspace(x.device),
+           N.stream())
     return q
 
 

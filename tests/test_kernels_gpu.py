@@ -901,6 +901,48 @@ def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
     close(q, q_ref, atol=2e-2 * scale)
     close(kc[1], kc[0], atol=2e-2 * scale)
     close(vc[1], vc[0], atol=2e-2 * scale)
+    # qscale: q leaves the epilogue times c before its one rounding; k / v untouched (bit-equal)
+    c = 0.12753
+    kc2, vc2 = torch.zeros_like(kc[1]), torch.zeros_like(vc[1])
+    qc = gemm.prefill_qkv_rope(x, w, pos, cs, slots, kc2, vc2, Hq, Hkv, qscale=c)
+    close(qc, q.float() * c, atol=1e-2 * scale * c)
+    assert torch.equal(kc2, kc[1]) and torch.equal(vc2, vc[1])
+
+
+@pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
+    (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
+    (32, 8, 128, True, [(257, 257), (64, 3000)], 12.0),      # peaky rows
+    (8, 1, 128, True, [(40, 40), (33, 500)], 1.0),
+])
+def test_prefill_attention_prescaled_q(Hq, Hkv, D, causal, lens, qscale):
+    """q handed over prescaled by scale * log2(e) at its ONE bf16 rounding (what the fused QKV epilogue
+    does with qscale) on the prescaled-Q fold, with scale 1 / log2(e): as close to the fp32 reference
+    as the exact-Q variant 5 fed bf16(q) -- the in-kernel prescale's second rounding (variant 6) is
+    what costs precision on peaky rows -- plain and lean work lists."""
+    g = torch.Generator().manual_seed(70)
+    qlens = [a for a, _ in lens]
+    ctx = [b for _, b in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    qf = torch.randn(int(cu[-1]), Hq, D, generator=g) * qscale          # the rope output, f32
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    c = scale * 1.4426950408889634
+    ref = ops.prefill(qf, cu, ctx_t, tables, kc, vc, scale, causal)
+    q5 = qf.to(torch.bfloat16)
+    qp = (qf * c).to(torch.bfloat16)
+    args = (cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV))
+    out5 = ops.prefill(q5.to(DEV), *args, scale, causal, max_q_len=max(qlens))
+    outp = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens), q_prescaled=True)
+    e5 = (out5.float().cpu() - ref.float()).abs().max().item()
+    ep = (outp.float().cpu() - ref.float()).abs().max().item()
+    assert ep <= 2e-2 and ep <= 1.5 * e5 + 2e-3, (ep, e5)
+    wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, causal, cus=100000, min_chunk=1)
+    if wl is not None:
+        outl = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens),
+                           work=torch.from_numpy(wl).to(DEV), lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])),
+                           q_prescaled=True)
+        assert (outl.float().cpu() - ref.float()).abs().max().item() <= max(2e-2, 1.5 * e5 + 2e-3)
 
 
 @pytest.mark.parametrize("gelu", [False, True])
