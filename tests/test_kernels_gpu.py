@@ -936,13 +936,15 @@ def test_prefill_attention_prescaled_q(Hq, Hkv, D, causal, lens, qscale):
     outp = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens), q_prescaled=True)
     e5 = (out5.float().cpu() - ref.float()).abs().max().item()
     ep = (outp.float().cpu() - ref.float()).abs().max().item()
-    assert ep <= 2e-2 and ep <= 1.5 * e5 + 2e-3, (ep, e5)
+    # on the peaky rows (qscale 12) the ONE rounding of q itself already costs variant 5 ~0.1 against
+    # the f32-q reference; the prescaled form stays within 1.5x of that, and within 0.02 on typical rows
+    assert ep <= 1.5 * e5 + 2e-3 and (qscale > 1 or ep <= 2e-2), (ep, e5)
     wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, causal, cus=100000, min_chunk=1)
     if wl is not None:
         outl = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens),
                            work=torch.from_numpy(wl).to(DEV), lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])),
                            q_prescaled=True)
-        assert (outl.float().cpu() - ref.float()).abs().max().item() <= max(2e-2, 1.5 * e5 + 2e-3)
+        assert (outl.float().cpu() - ref.float()).abs().max().item() <= 1.5 * e5 + 2e-2
 
 
 @pytest.mark.parametrize("gelu", [False, True])
