@@ -47,8 +47,12 @@ from .configs import ModelConfig
 # one stream, prefill then decode)
 ATTN_OVERLAP = os.environ.get("PENNY_ATTN_OVERLAP", "1") != "0"
 # fused-QKV prefill steps hand the attention q prescaled by scale * log2(e) (ops.gemm.prefill_qkv_rope
-# qscale; ops.prefill q_prescaled); PENNY_PRESCALE_Q=0 keeps q unscaled (A/B)
-PRESCALE_Q = os.environ.get("PENNY_PRESCALE_Q", "0") != "0"
+# qscale; ops.prefill q_prescaled): the prescaled-Q fold's block loop (+7.5-8.6 % per prefill
+# attention call, profiles/r5_prefill_attn_fold_ab.jsonl variant 6) at the exact form's precision
+# (q rounded once either way: tests/test_kernels_gpu.py test_prefill_attention_prescaled_q).  Driver
+# bench A/B on one box: 32.53 vs 32.51 turns/s (the prefill attention shares its steps with the decode
+# rows' attention on the side stream).  PENNY_PRESCALE_Q=0 keeps q unscaled.
+PRESCALE_Q = os.environ.get("PENNY_PRESCALE_Q", "1") != "0"
 LOG2E = 1.4426950408889634
 
 
