@@ -878,12 +878,19 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
   }
 }
 
-// grid (Hq, B), D threads: merges a row's lean partials, skipping rows one wave already finished
+// grid (B), 256 threads: merges row b's lean partials for all Hq heads (256 / D heads per pass);
+// a row one wave finished is skipped by the whole workgroup (the decision depends on b only).  One
+// workgroup per row instead of one per (row, head): at B = 128, Hq = 32 that is 128 workgroups, not
+// 4,096 mostly-empty ones.
 template <int D>
-__global__ void decode_lean_reduce_kernel(const int* __restrict__ meta, const float* __restrict__ part_m,
-                                          const float* __restrict__ part_l, const float* __restrict__ part_o,
-                                          bf16* __restrict__ out, int B, int Hq, int part_stride) {
-  const int b = blockIdx.y, hq = blockIdx.x, d = threadIdx.x;
+__global__ void __launch_bounds__(256) decode_lean_reduce_kernel(const int* __restrict__ meta,
+                                                                 const float* __restrict__ part_m,
+                                                                 const float* __restrict__ part_l,
+                                                                 const float* __restrict__ part_o,
+                                                                 bf16* __restrict__ out, int B, int Hq,
+                                                                 int part_stride) {
+  static_assert(256 % D == 0, "heads per pass");
+  const int b = blockIdx.x;
   const int pre = meta[LEAN_META0 + b], n = meta[LEAN_META0 + b + 1] - pre, pw = meta[LEAN_META0 + B + 1];
   int np = 0;
   if (n > 0) {
@@ -891,16 +898,19 @@ __global__ void decode_lean_reduce_kernel(const int* __restrict__ meta, const fl
     if (fw == lw) return;   // written by its one wave
     np = lw - fw + 1;
   }
-  const long base = ((long)b * Hq + hq) * part_stride;
-  float M = -INFINITY;
-  for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
-  float L = 0.f, O = 0.f;
-  for (int i = 0; i < np; ++i) {
-    const float f = exp2f(part_m[base + i] - M);
-    L += part_l[base + i] * f;
-    O += part_o[(base + i) * D + d] * f;
+  const int d = threadIdx.x % D;
+  for (int hq = threadIdx.x / D; hq < Hq; hq += 256 / D) {
+    const long base = ((long)b * Hq + hq) * part_stride;
+    float M = -INFINITY;
+    for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
+    float L = 0.f, O = 0.f;
+    for (int i = 0; i < np; ++i) {
+      const float f = exp2f(part_m[base + i] - M);
+      L += part_l[base + i] * f;
+      O += part_o[(base + i) * D + d] * f;
+    }
+    out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
   }
-  out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 
 
@@ -1292,7 +1302,7 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
                          lean_min_per_wave);                                                                     \
-    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, part_l, \
+    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(B), dim3(256), 0, stream, lean_meta, part_m, part_l,   \
                        part_o, (bf16*)out, B, Hq, part_stride);                                                  \
   } else {                                                                                                      \
     if (head_fast)                                                                                              \
