@@ -145,7 +145,7 @@ def bench_decode_lean(dev) -> List[Dict]:
         # lean_nt: every block non-temporal; lean_ntm: the shared-prefix blocks (marked in the table by
         # the host, as the engine does) on the default policy, the rest non-temporal
         fns = {"part": mk(False), "lean": mk(True), "lean_nt": mk(True, 1), "lean_ntm": mk(True, 1, marked_d),
-               "part_marked": mk(False, 0, marked_d)}
+               "lean_ntm_wmerge": mk(True, 3, marked_d)}
         ref = None
         errs = {}
         for k, f in fns.items():

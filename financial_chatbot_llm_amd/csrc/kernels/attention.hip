@@ -878,19 +878,20 @@ __global__ void __launch_bounds__(256) decode_lean_kernel(
   }
 }
 
-// grid (B), 256 threads: merges row b's lean partials for all Hq heads (256 / D heads per pass);
-// a row one wave finished is skipped by the whole workgroup (the decision depends on b only).  One
-// workgroup per row instead of one per (row, head): at B = 128, Hq = 32 that is 128 workgroups, not
-// 4,096 mostly-empty ones.
-template <int D>
-__global__ void __launch_bounds__(256) decode_lean_reduce_kernel(const int* __restrict__ meta,
-                                                                 const float* __restrict__ part_m,
-                                                                 const float* __restrict__ part_l,
-                                                                 const float* __restrict__ part_o,
-                                                                 bf16* __restrict__ out, int B, int Hq,
-                                                                 int part_stride) {
-  static_assert(256 % D == 0, "heads per pass");
-  const int b = blockIdx.x;
+// grid (Hq / HPW, B), HPW * D threads: merges row b's lean partials for HPW heads per workgroup,
+// skipping rows one wave already finished (the decision depends on b only, so the whole workgroup
+// returns).  HPW = 1 is the r3 form (one workgroup per (head, row)); HPW = 4 (lean_flags bit 1)
+// quarters the workgroup count.  (One workgroup per row looping over all heads measured 24-178 us
+// per call against 8-10: the passes serialise their dependent loads.)
+template <int D, int HPW>
+__global__ void __launch_bounds__(HPW * D) decode_lean_reduce_kernel(const int* __restrict__ meta,
+                                                                     const float* __restrict__ part_m,
+                                                                     const float* __restrict__ part_l,
+                                                                     const float* __restrict__ part_o,
+                                                                     bf16* __restrict__ out, int B, int Hq,
+                                                                     int part_stride) {
+  const int b = blockIdx.y, hq = blockIdx.x * HPW + threadIdx.x / D, d = threadIdx.x % D;
+  if (hq >= Hq) return;
   const int pre = meta[LEAN_META0 + b], n = meta[LEAN_META0 + b + 1] - pre, pw = meta[LEAN_META0 + B + 1];
   int np = 0;
   if (n > 0) {
@@ -898,19 +899,16 @@ __global__ void __launch_bounds__(256) decode_lean_reduce_kernel(const int* __re
     if (fw == lw) return;   // written by its one wave
     np = lw - fw + 1;
   }
-  const int d = threadIdx.x % D;
-  for (int hq = threadIdx.x / D; hq < Hq; hq += 256 / D) {
-    const long base = ((long)b * Hq + hq) * part_stride;
-    float M = -INFINITY;
-    for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
-    float L = 0.f, O = 0.f;
-    for (int i = 0; i < np; ++i) {
-      const float f = exp2f(part_m[base + i] - M);
-      L += part_l[base + i] * f;
-      O += part_o[(base + i) * D + d] * f;
-    }
-    out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
+  const long base = ((long)b * Hq + hq) * part_stride;
+  float M = -INFINITY;
+  for (int i = 0; i < np; ++i) M = fmaxf(M, part_m[base + i]);
+  float L = 0.f, O = 0.f;
+  for (int i = 0; i < np; ++i) {
+    const float f = exp2f(part_m[base + i] - M);
+    L += part_l[base + i] * f;
+    O += part_o[(base + i) * D + d] * f;
   }
+  out[((long)b * Hq + hq) * D + d] = (bf16)(L > 0.f ? O / L : 0.f);
 }
 
 
@@ -1302,8 +1300,12 @@ PENNY_API int penny_attention_decode(const void* q, const int* ctx_lens, const i
                          ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, part_m,  \
                          part_l, part_o, lean_meta, sl2, B, Hq, Hkv, max_blocks, nparts, part_stride,            \
                          lean_min_per_wave);                                                                     \
-    hipLaunchKernelGGL(decode_lean_reduce_kernel<DD>, dim3(B), dim3(256), 0, stream, lean_meta, part_m, part_l,   \
-                       part_o, (bf16*)out, B, Hq, part_stride);                                                  \
+    if (lean_flags & 2)                                                                                         \
+      hipLaunchKernelGGL((decode_lean_reduce_kernel<DD, 4>), dim3((Hq + 3) / 4, B), dim3(4 * DD), 0, stream,     \
+                         lean_meta, part_m, part_l, part_o, (bf16*)out, B, Hq, part_stride);                      \
+    else                                                                                                        \
+      hipLaunchKernelGGL((decode_lean_reduce_kernel<DD, 1>), dim3(Hq, B), dim3(DD), 0, stream, lean_meta, part_m, \
+                         part_l, part_o, (bf16*)out, B, Hq, part_stride);                                         \
   } else {                                                                                                      \
     if (head_fast)                                                                                              \
       hipLaunchKernelGGL((decode_kernel<DD, true>), grid, dim3(256), 0, stream, (const bf16*)q, ctx_lens,          \

@@ -399,7 +399,8 @@ LEAN_MIN_B = int(os.environ.get("PENNY_DECODE_LEAN_MIN_B", "1"))
 LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgroups per CU
 LEAN_MIN_PER_WAVE = 2
 # lean kernel flags (attention.hip penny_attention_decode lean_flags): bit 0 = non-temporal K/V loads
-# for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks).
+# for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks);
+# bit 1 = the merge with 4 heads per workgroup (A/B).
 # Measured on workload batches (bench/kernels.py decode_lean, profiles/r5_decode_lean_nt_marked_ab.jsonl):
 # -9..-13 % per call at B = 64-256 (-10 % with no shared prefix; every block non-temporal, shared
 # ones included, gains only 3-6 % and loses 3 % on a 2k shared prefix); +4 % at B = 16, so batches
