@@ -400,12 +400,13 @@ LEAN_WG_PER_CU = 2          # 242 VGPRs per wave -> 2 waves per SIMD = 2 workgro
 LEAN_MIN_PER_WAVE = 2
 # lean kernel flags (attention.hip penny_attention_decode lean_flags): bit 0 = non-temporal K/V loads
 # for the blocks only one row of the step reads (the host marks the shared ones: mark_shared_blocks);
-# bit 1 = the merge with 4 heads per workgroup (A/B).
+# bit 1 = the merge with 4 heads per workgroup (7.5 vs 8.1 us per call, decode -0.4..-1.8 % standalone,
+# profiles/r5_decode_lean_merge_hpw_ab.jsonl).
 # Measured on workload batches (bench/kernels.py decode_lean, profiles/r5_decode_lean_nt_marked_ab.jsonl):
 # -9..-13 % per call at B = 64-256 (-10 % with no shared prefix; every block non-temporal, shared
 # ones included, gains only 3-6 % and loses 3 % on a 2k shared prefix); +4 % at B = 16, so batches
 # below LEAN_NT_MIN_B keep the default policy.  Driver bench 33.29 vs 32.52 turns/s on one box.
-LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "1"))
+LEAN_FLAGS = int(os.environ.get("PENNY_DECODE_LEAN_FLAGS", "3"))
 LEAN_NT_MIN_B = 32
 MARK_MAX_COLS = 64          # a shared prefix is looked for in the first 64 blocks (4k tokens)
 

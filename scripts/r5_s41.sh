@@ -1,5 +1,5 @@
 #!/bin/bash
-# r5 session 41: the lean decode merge as one workgroup per row -- decode / engine GPU tests, then the
+# r5 session 41: the lean decode merge, 1 vs 4 heads per workgroup (A/B) -- decode / engine GPU tests, then the
 # decode_lean bench under rocprofv3 kernel stats (merge kernel time per call).
 set -u
 mkdir -p gpurun_out
