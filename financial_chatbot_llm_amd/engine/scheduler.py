@@ -27,6 +27,7 @@ lifts as soon as no decide call is decoding.
 """
 from __future__ import annotations
 
+import os
 import time
 from collections import deque
 from dataclasses import dataclass, field
@@ -67,6 +68,11 @@ class StepCostModel:
     def prefill_cap(self, decode_rows: int) -> int:
         room = self.target_ms - self.base_ms - self.per_row_ms * decode_rows
         return max(self.min_prefill_tokens, int(room / self.per_token_ms))
+
+
+# step-row quantisation may cut any chunk (not only the last one) to reach a multiple of the quantum;
+# PENNY_QUANTISE_ANY=0 restores the last-chunk-only form (A/B)
+QUANTISE_ANY = os.environ.get("PENNY_QUANTISE_ANY", "1") != "0"
 
 
 class Scheduler:
@@ -323,11 +329,14 @@ class Scheduler:
         return budget
 
     def _quantise(self, batch: ScheduledBatch) -> None:
-        """Round the step's row count DOWN to a multiple of ``token_quantum`` by shortening its last
-        prefill chunk (those tokens run next step; nothing is padded).  The prefill GEMMs' M is the
-        step's row count, and hipBLASLt's speed swings with M between neighbouring values (1139 vs
-        1417 TF/s at M = 2816 / 2560 on the default heuristic; profiles/r2_gemm_prefill_tunableop_sweep.jsonl):
-        multiples of 256 hit tuned solutions (tuning/gemm_*.csv) and no pathological shape."""
+        """Round the step's row count DOWN to a multiple of ``token_quantum`` by shortening prefill
+        chunks (those tokens run next step; nothing is padded).  The prefill GEMMs' M is the step's row
+        count: the tile kernel's last 256-row tile runs whole however few rows it holds, and
+        hipBLASLt's speed swings with M between neighbouring values (1139 vs 1417 TF/s at M = 2816 /
+        2560 on the default heuristic; profiles/r2_gemm_prefill_tunableop_sweep.jsonl).  The cut comes
+        from chunks that do not finish their prompt first, long-output ones before short-output ones,
+        the most recently added first; speculative chunks are never cut, and a step that cannot reach
+        a multiple stays as it is."""
         q = self.token_quantum
         if q <= 0 or not batch.prefill:
             return
@@ -335,11 +344,31 @@ class Scheduler:
         r = total % q
         if total <= q or r == 0:
             return
-        seq, start, n = batch.prefill[-1]
-        if n <= r or seq.spec_rows:
+
+        def rank(i: int):
+            seq, start, n = batch.prefill[i]
+            final = start + n >= seq.num_tokens
+            short = seq.params.max_tokens <= self.short_output_tokens
+            return (final, short, -i)
+        order = [i for i in sorted(range(len(batch.prefill)), key=rank)
+                 if not batch.prefill[i][0].spec_rows and batch.prefill[i][2] > 1]
+        if not QUANTISE_ANY:        # r2 form (A/B): the last chunk only
+            order = [len(batch.prefill) - 1] if (len(batch.prefill) - 1) in order else []
+        # one chunk that can take the whole cut, else the cut spread over several
+        one = next((i for i in order if batch.prefill[i][2] > r), None)
+        cuts, left = ({one: r}, 0) if one is not None else ({}, r)
+        for i in order if one is None else ():
+            c = min(left, batch.prefill[i][2] - 1)
+            cuts[i] = c
+            left -= c
+            if left == 0:
+                break
+        if left:
             return
-        batch.prefill[-1] = (seq, start, n - r)
-        seq.num_prefilled -= r
+        for i, c in cuts.items():
+            seq, start, n = batch.prefill[i]
+            batch.prefill[i] = (seq, start, n - c)
+            seq.num_prefilled -= c
 
     def finish(self, seq: Sequence, reason: str) -> None:
         seq.status = SeqStatus.FINISHED

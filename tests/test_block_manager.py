@@ -281,6 +281,18 @@ def test_scheduler_quantises_step_rows():
     c = _mk_params(list(range(200)), "c", 64, arrival=1.0)
     small.add(c)
     assert small.schedule().num_tokens == 200           # below one quantum: untouched
+    # the last chunk too short to absorb the remainder (a 150-token prompt): the cut comes from the
+    # earlier chunk instead of leaving the step unaligned
+    sch2 = Scheduler(PyBlockManager(256, BS, True), max_num_seqs=8, max_num_batched_tokens=1000,
+                     max_model_len=4096, token_quantum=256)
+    d = _mk_params(list(range(5000, 5850)), "d", 64, arrival=1.0)
+    e = _mk_params(list(range(8000, 8150)), "e", 64, arrival=2.0)
+    sch2.add(d)
+    sch2.add(e)
+    batch = sch2.schedule()
+    assert batch.num_tokens == 768
+    assert [(s.request_id, st, n) for s, st, n in batch.prefill] == [("d", 0, 618), ("e", 0, 150)]
+    assert d.num_prefilled == 618
 
 
 def test_step_time_bound_caps_prefill_only_while_a_decide_decodes():
