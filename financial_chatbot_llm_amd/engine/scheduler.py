@@ -71,7 +71,8 @@ class StepCostModel:
 
 
 # step-row quantisation may cut any chunk (not only the last one) to reach a multiple of the quantum;
-# PENNY_QUANTISE_ANY=0 restores the last-chunk-only form (A/B)
+# PENNY_QUANTISE_ANY=0 restores the last-chunk-only form.  Driver bench A/B, two runs each on one box:
+# 33.23 / 33.58 vs 33.26 / 33.45 turns/s (neutral; profiles/r5_bench128_20x5_quantise_any*_run*.json)
 QUANTISE_ANY = os.environ.get("PENNY_QUANTISE_ANY", "1") != "0"
 
 
