@@ -1243,6 +1243,31 @@ def bench_gemm_group(dev, Ms=(1024, 2048, 2560, 3072, 4096), groups=(1, 2, 4, 8,
     return out
 
 
+def bench_gemm_tiled_w(dev, Ms=(512, 1024, 2048, 3072, 4096)) -> List[Dict]:
+    """The prefill tile kernel on the fragment-tiled weight vs the row-major one (same epilogue),
+    interleaved per M: could a shape keep only the decode kernels' tiled copy?"""
+    from ..ops import gemm
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    shapes = {"8b_gate_up": (28672, 4096, "silu"), "8b_down": (4096, 14336, None), "8b_qkv": (6144, 4096, None),
+              "70b_tp1_gate_up": (57344, 8192, "silu")}
+    for name, (N, K, epi) in shapes.items():
+        w = rnd(N, K)
+        wt = gemm.tile_weight(w)
+        for M in Ms:
+            x = rnd(M, K)
+            t = interleaved({"rowmajor": lambda: gemm.prefill_gemm(x, w, epi),
+                             "tiled": lambda: gemm.prefill_gemm_tiled(x, wt, N, epi)}, rounds=5, iters=5)
+            row = {"op": "gemm_tiled_w", "name": name, "M": M, **{k: round(v, 1) for k, v in t.items()},
+                   "tiled_gain": round(t["rowmajor"] / t["tiled"], 3),
+                   "tiled_TF": round(2 * M * N * K / t["tiled"] / 1e6, 1)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del w, wt
+        torch.cuda.empty_cache()
+    return out
+
+
 def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256),
                        prefill_Ms=(384, 512, 768, 1024, 1536, 2048, 3072, 4096)) -> List[Dict]:
     """Decode and prefill kernels vs hipBLASLt at the 70B shard / TP=1 shapes, interleaved per M in
@@ -1422,7 +1447,7 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "gemm_group": bench_gemm_group,
+                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "gemm_tiled_w": bench_gemm_tiled_w, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",
                                                                   "70b_tp8_gate_up", "70b_tp8_down"),
                                                         Ms=(96, 112, 128, 144, 160, 192, 256)), "chunked_prefill": bench_chunked_prefill,

@@ -175,6 +175,16 @@ __device__ __forceinline__ void read_w(const char* __restrict__ h, FragPair (&a)
       a[f].f[kk].u = *reinterpret_cast<const uint4*>(h + (wa * 64 + f * 16) * 128 + rowoff + choff[kk]);
 }
 
+// WT (fragment-tiled W, ops/gemm.py tile_weight): a half-tile's row group rgi (16 rows) and k-step kk
+// is the lane-linear 1 KiB piece rgi * 2 + kk -- conflict-free by construction
+__device__ __forceinline__ void read_w_tiled(const char* __restrict__ h, FragPair (&a)[4], int wa, int lane) {
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      a[f].f[kk].u = *reinterpret_cast<const uint4*>(h + ((wa * 4 + f) * 2 + kk) * 1024 + lane * 16);
+}
+
 __device__ __forceinline__ void read_x(const char* __restrict__ h, FragPair (&b)[2], int wb, int rowoff,
                                        const int (&choff)[2]) {
 #pragma unroll
@@ -248,13 +258,15 @@ __device__ __forceinline__ void mma(f32x4 (&acc)[8][4], const FragPair (&a)[4], 
 // FP8: X and W are OCP e4m3 bytes (K-tile = 128 elements), the grouped MoE form: W is [E, N, K],
 // M counts sorted rows, the grid covers ceil(M/256) + E token tiles per column tile and the
 // surplus workgroups exit before touching LDS.
-template <int EPI, int ABL = 0, int BAL = 1, bool FP8 = false>
+// WT: W is the fragment-tiled copy (tile_weight) instead of the row-major [N, K] weight (bf16 only)
+template <int EPI, int ABL = 0, int BAL = 1, bool FP8 = false, bool WT = false>
 __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restrict__ Xv, int ldx,
                                                            const void* __restrict__ Wv, int K,
                                                            void* __restrict__ Y, int ldy,
                                                            const bf16* __restrict__ R, int ldr,
                                                            int M, int N, int S, RopeArgs ra, MoeArgs ma,
                                                            SampleArgs sa, TailArgs ta) {
+  static_assert(!(WT && FP8), "fragment-tiled W: bf16 only");
   constexpr int ESZ = FP8 ? 1 : 2;        // bytes per element
   constexpr int BKE = 128 / ESZ;          // elements per K-tile row (128 bytes)
   constexpr bool MXI = EPI == EPI_MOE_ROUTE_MX;   // X carries E8M0 block scales (GEMM2 of the MX hand-off)
@@ -335,7 +347,11 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       if (h == H_W0 || h == H_W1) {
         const int n = n0 + (lr >> 6) * 128 + (h == H_W1 ? 64 : 0) + (lr & 63);
         if constexpr (FP8) soff[h][i] = (unsigned)(((long)n * K + k0) + 16 * c);
-        else src[h][i] = W + ((long)n * K + k0) * ESZ + 16 * c;
+        else if constexpr (WT) {
+          // piece (w, i) of the half = row group rgi = w, k-step i: global row group G
+          const int G = n0 / 16 + (w >> 2) * 8 + (w & 3) + (h == H_W1 ? 4 : 0);
+          src[h][i] = W + (((long)G * (K / 32) + k0 / 32 + i) * 64 + lane) * 16;
+        } else src[h][i] = W + ((long)n * K + k0) * ESZ + 16 * c;
       } else {
         int m = min(m0 + (lr >> 5) * 64 + (h == H_X1 ? 32 : 0) + (lr & 31), mend - 1);
         if (FP8 && ma.rows) m = ma.rows[m];              // GEMM1 gathers the routed token rows
@@ -368,7 +384,8 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
                      : "v"(vo), "s"(dst), "s"(base)
                      : "memory");
       } else {
-        const char* gp = src[h][i] + (long)t * 128;
+        // one K-tile = 128 B of a row-major row, or two 1-KiB k-step pieces of a tiled row group
+        const char* gp = src[h][i] + (long)t * ((WT && (h == H_W0 || h == H_W1)) ? 2048 : 128);
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep)
                      : "v"(gp), "s"(dst)
@@ -407,6 +424,11 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   FragPair a[4], b0[2], b1[2];
+#define READ_W(half_)                                              \
+  do {                                                             \
+    if constexpr (WT) read_w_tiled((half_), a, wa, lane);         \
+    else read_w((half_), a, wa, rowoff, choff);                   \
+  } while (0)
 
   // ---- prologue: K-tile 0 whole, K-tile 1 halves W0, X0, X1 ----
 #pragma unroll
@@ -457,14 +479,14 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       const char* nx = smem + ((t + 1) & 1) * BUF;
       const unsigned lcur = lds0 + (t & 1) * BUF, lnxt = lds0 + ((t + 1) & 1) * BUF;
       const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
-      if (ABL != 2 || t == 0) read_w(cur + H_W0 * HALF, a, wa, rowoff, choff);
+      if (ABL != 2 || t == 0) READ_W(cur + H_W0 * HALF);
       sc = read_sc(t);
       if (more1) stage(H_W1, t + 1, lnxt);
       phase(I0{}, I0{}, a, bc, sc);
       if (ABL != 2 || t == 0) read_x(cur + H_X1 * HALF, b1, wb, rowoff, choff);
       if (more2) stage(H_W0, t + 2, lcur);
       phase(I0{}, I2{}, a, b1, sc);
-      if (ABL != 2 || t == 0) read_w(cur + H_W1 * HALF, a, wa, rowoff, choff);
+      if (ABL != 2 || t == 0) READ_W(cur + H_W1 * HALF);
       if (more2) {
         stage(H_X0, t + 2, lcur);
         if (ABL != 3) wait_vm<6 + XL0>();
@@ -495,7 +517,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
       // phase 1: W_q0 x X_q0          restage: W_q1 of tile t+1 (read last in phase 3 of t-1)
       if (ABL != 2 || t == 0) {
-        read_w(cur + H_W0 * HALF, a, wa, rowoff, choff);
+        READ_W(cur + H_W0 * HALF);
         read_x(cur + H_X0 * HALF, b0, wb, rowoff, choff);
       }
       if (more1) stage(H_W1, t + 1, lnxt);
@@ -505,7 +527,7 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
       if (more2) stage(H_W0, t + 2, lcur);
       phase(I0{}, I2{}, a, b1);
       // phase 3: W_q1 x X_q1          restage: X_q0 of tile t+2 (read in phase 1)
-      if (ABL != 2 || t == 0) read_w(cur + H_W1 * HALF, a, wa, rowoff, choff);
+      if (ABL != 2 || t == 0) READ_W(cur + H_W1 * HALF);
       if (more2) stage(H_X0, t + 2, lcur);
       phase(I4{}, I2{}, a, b1);
       // phase 4: W_q1 x X_q0          restage: X_q1 of tile t+2 (read in phase 2); retire tile t+1
@@ -799,15 +821,17 @@ __global__ void __launch_bounds__(512) gemm_prefill_kernel(const void* __restric
 
 }  // namespace
 
+#undef READ_W
+
 // token tiles per L2 group of the bf16 launches below (0: GM); an A/B knob (bench/kernels.py gemm_group)
 static int g_group = 0;
 
-template <int EPI, int ABL = 0, int BAL = 1>
+template <int EPI, int ABL = 0, int BAL = 1, bool WT = false>
 static void launch(dim3 grid, hipStream_t stream, const void* X, int ldx, const void* W, int K, void* Y, int ldy,
                    const void* R, int ldr, int M, int N, int S, const RopeArgs& ra, TailArgs ta = TailArgs{}) {
   ta.gm = g_group;
-  hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL>), grid, dim3(512), 0, stream, X, ldx, W, K, Y, ldy,
-                     (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{}, ta);
+  hipLaunchKernelGGL((gemm_prefill_kernel<EPI, ABL, BAL, false, WT>), grid, dim3(512), 0, stream, X, ldx, W, K, Y,
+                     ldy, (const bf16*)R, ldr, M, N, S, ra, MoeArgs{}, SampleArgs{}, ta);
 }
 
 static dim3 grid_for(int M, int N, int S) { return dim3((unsigned)(((M + TM - 1) / TM) * (N / TN) * S)); }
@@ -865,6 +889,31 @@ PENNY_API int penny_gemm_prefill(const void* X, int ldx, const void* W, int K, v
     case EPI_BIAS: launch<EPI_BIAS>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
     case EPI_BIAS_GELU: launch<EPI_BIAS_GELU>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
     default: launch<EPI_RESID>(grid, stream, X, ldx, W, K, Y, ldy, R, ldr, M, N, S, ra, ta);
+  }
+  return (int)hipGetLastError();
+}
+
+// penny_gemm_prefill on the fragment-tiled weight (ops/gemm.py tile_weight: [N/16, K/32, 64, 8]) instead
+// of the row-major one -- the layout the decode kernels stream, so a shape could keep ONE copy.
+// Epilogues BF16 / SILU / SLAB / RESID; same contract otherwise.
+PENNY_API int penny_gemm_prefill_wt(const void* X, int ldx, const void* Wt, int K, void* Y, int ldy, const void* R,
+                                    int ldr, int M, int N, int S, int epi, float* tail_ws, long tail_ws_floats,
+                                    int* tail_cnt, int tail_ncnt, int cus, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % TN || S < 1 || K % (BK * S) || ldx % 8 || (epi != EPI_BF16 && epi != EPI_SILU && epi != EPI_SLAB &&
+                                                    epi != EPI_RESID))
+    return (int)hipErrorInvalidValue;
+  if (epi != EPI_SLAB && (S != 1 || ldy % 8)) return (int)hipErrorInvalidValue;
+  if (epi == EPI_RESID && (!R || ldr % 8)) return (int)hipErrorInvalidValue;
+  TailArgs ta{};
+  const dim3 grid = S == 1 ? tail_plan(M, N, K, cus, tail_ws, tail_ws_floats, tail_cnt, tail_ncnt, ta)
+                           : grid_for(M, N, S);
+  const RopeArgs ra{};
+  switch (epi) {
+    case EPI_BF16: launch<EPI_BF16, 0, 1, true>(grid, stream, X, ldx, Wt, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
+    case EPI_SILU: launch<EPI_SILU, 0, 1, true>(grid, stream, X, ldx, Wt, K, Y, ldy, R, ldr, M, N, S, ra, ta); break;
+    case EPI_SLAB: launch<EPI_SLAB, 0, 1, true>(grid, stream, X, ldx, Wt, K, Y, ldy, R, ldr, M, N, S, ra); break;
+    default: launch<EPI_RESID, 0, 1, true>(grid, stream, X, ldx, Wt, K, Y, ldy, R, ldr, M, N, S, ra, ta);
   }
   return (int)hipGetLastError();
 }

@@ -40,6 +40,8 @@ _SIGS = {
     "penny_gateup_silu_gemm": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gemm_prefill": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
                            P, c_long, P, c_int, c_int, P],
+    "penny_gemm_prefill_wt": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                              P, c_long, P, c_int, c_int, P],
     "penny_gemm_prefill_qkv_rope": [P, c_int, P, c_int, c_int, P, P, P, P, P, P, c_int, c_int,
                                     c_float, P, c_long, P, c_int, c_int, P],
     "penny_gemm_prefill_ablate": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P],

@@ -601,6 +601,28 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = Non
     return y
 
 
+def prefill_gemm_tiled(x: torch.Tensor, wt: torch.Tensor, N_: int, epilogue: Optional[str] = None, S: int = 1,
+                       residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``prefill_gemm`` on the fragment-tiled weight (``tile_weight``'s copy, the layout the decode
+    kernels stream) instead of the row-major one: same MFMA sequence, bit-equal output.  Epilogues
+    None / "silu" / "slabs" / "residual"."""
+    M, K = x.shape
+    if not N.use_native(x):
+        return prefill_gemm(x, untile_weight(wt), epilogue, S, residual=residual, out=out)
+    if epilogue == "slabs":
+        y = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
+        ldy = N_
+    else:
+        S = 1
+        cols = N_ // 2 if epilogue == "silu" else N_
+        y = out if out is not None else torch.empty((M, cols), dtype=x.dtype, device=x.device)
+        ldy = y.stride(0)
+    N.call("penny_gemm_prefill_wt", N.ptr(x), x.stride(0), N.ptr(wt), K, N.ptr(y), ldy, N.ptr(residual),
+           residual.stride(0) if residual is not None else 0, M, N_, S, PREFILL_EPI[epilogue],
+           *tail_workspace(x.device), N.stream())
+    return y
+
+
 # Wave-quantisation tail of the tile kernel (gemm_prefill.hip TailArgs): one workspace per
 # (device, stream) -- f32 partial tiles of at most one round of tail workgroups (64 MB) and
 # self-resetting ticket counters.  PENNY_GEMM_TAIL=0 launches whole tiles only (A/B).

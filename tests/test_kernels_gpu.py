@@ -875,6 +875,25 @@ def test_prefill_gemm_silu_and_residual_epilogues():
     close(y2, ref2, atol=2e-2 * ref2.abs().max().item())
 
 
+@pytest.mark.parametrize("M", [300, 700, 1300])
+def test_prefill_gemm_fragment_tiled_weight(M):
+    """The tile kernel reading the fragment-tiled weight (tile_weight, the decode kernels' layout) is
+    bit-equal to the row-major form: bf16, SiLU, split-K slabs and the residual epilogue."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(M)
+    N_, K = 768, 1024
+    x = rnd(M, K, gen=g).to(DEV)
+    w = rnd(N_, K, scale=0.05, gen=g).to(DEV)
+    wt = gemm.tile_weight(w)
+    assert torch.equal(gemm.prefill_gemm_tiled(x, wt, N_), gemm.prefill_gemm(x, w))
+    assert torch.equal(gemm.prefill_gemm_tiled(x, wt, N_, "silu"), gemm.prefill_gemm(x, w, "silu"))
+    assert torch.equal(gemm.prefill_gemm_tiled(x, wt, N_, "slabs", 2), gemm.prefill_gemm(x, w, "slabs", 2))
+    r = rnd(M, N_, gen=g).to(DEV)
+    assert torch.equal(gemm.prefill_gemm_tiled(x, wt, N_, "residual", residual=r),
+                       gemm.prefill_gemm(x, w, "residual", residual=r))
+    close(gemm.prefill_gemm_tiled(x, wt, N_), x.float() @ w.float().t(), atol=2e-2)
+
+
 @pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (333, 32, 8), (1500, 8, 1)])
 def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
     """Fused QKV + RoPE + paged KV write == GEMM -> rope_kv_write (the unfused path), including
