@@ -37,7 +37,8 @@ def _dual_stream(device) -> "torch.cuda.Stream":
     if key not in _DUAL_STREAMS:
         _DUAL_STREAMS[key] = torch.cuda.Stream(device=device)
     return _DUAL_STREAMS[key]
-from ..ops.gemm import interleave16, linear, prefill_qkv_rope, qkv_rope_fused, tile_weight, uses_tiled_weight
+from ..ops.gemm import (interleave16, linear, linear_tiled, prefill_qkv_rope, qkv_rope_fused, tile_weight,
+                        tiled_only, uses_tiled_weight)
 from ..parallel.layers import shard_cols, shard_rows, shard_sections, vocab_range
 from .common import AttentionMetadata, KVCache, random_tensor
 from .configs import ModelConfig
@@ -164,6 +165,8 @@ class DecoderModel:
                 continue
             if name.endswith((".qkv", ".o", ".down", ".gate_up")) and uses_tiled_weight(*t.shape):
                 self.wt[name] = tile_weight(t)
+                if name.endswith(".gate_up") and tiled_only(*t.shape):
+                    self.w[name] = None          # the tiled copy is the only one (ops.gemm.TILED_ONLY)
         self._pad_vocab_shard()
         lm = self._lm_pad
         if lm is not None and lm.shape[0] % 64 == 0 and lm.shape[1] % 64 == 0 and self._tile_lm_head():
@@ -201,7 +204,9 @@ class DecoderModel:
         self._lm_pad = buf
 
     def num_bytes(self) -> int:
-        return sum(t.numel() * t.element_size() for t in self.w.values())
+        b = sum(t.numel() * t.element_size() for t in self.w.values() if t is not None)
+        return b + sum(self.wt[n].numel() * self.wt[n].element_size() for n, t in self.w.items()
+                       if t is None and n in self.wt)
 
     # ------------------------------------------------------------------------------------
     # forward
@@ -213,7 +218,12 @@ class DecoderModel:
     def mlp(self, i: int, h: torch.Tensor, reduce: bool = True,
             fuse_residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         p = f"layers.{i}."
-        a = linear(h, self.w[p + "gate_up"], epilogue="silu", wt=self.wt.get(p + "gate_up"))  # fused SiLU(gate)*up
+        w = self.w[p + "gate_up"]
+        if w is None:                             # kept only fragment-tiled (ops.gemm.TILED_ONLY)
+            wt = self.wt[p + "gate_up"]
+            a = linear_tiled(h, wt, wt.shape[0] * 16, epilogue="silu")
+        else:
+            a = linear(h, w, epilogue="silu", wt=self.wt.get(p + "gate_up"))  # fused SiLU(gate)*up
         # TP=1: decode-size batches return split-K slabs, reduced by the next add+RMSNorm; prefill
         # sizes may add the residual stream in the GEMM epilogue (fuse_residual -> ResidualSum)
         out = linear(a, self.w[p + "down"], wt=self.wt.get(p + "down"), slabs=self.tp_size == 1,

@@ -274,11 +274,44 @@ def _wrow(rowmajor: bool, M: int = 0, N_: int = 0, K: int = 0) -> int:
     return int(bool(rowmajor)) | (2 if pair else 0)
 
 
+# Shapes that keep ONLY the fragment-tiled copy (no row-major weight): every path runs on it -- the
+# prefill tile kernel's tiled form (penny_gemm_prefill_wt, bit-equal and at speed parity,
+# profiles/r5_tile_gemm_fragment_tiled_w.jsonl) and the decode kernels.  Llama-3-70B TP=1 gate|up: its
+# row-major decode stream lost to hipBLASLt from 17 rows (4.3 TB/s), the tiled fused kernel wins
+# (168-198 vs 184-205 us at M = 16-128, profiles/r5_gateup_shapes.jsonl), and a second copy would cost
+# 75 GB of KV pool.  PENNY_TILED_ONLY=0: row-major as before.
+TILED_ONLY = {(57344, 8192)} if os.environ.get("PENNY_TILED_ONLY", "1") != "0" else set()
+# decode configs on the tiled-only gate|up: [(max M, S, nf)], S = 1 -> the fused kernel
+TILED_ONLY_GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
+    (57344, 8192): [(1, 8, 2), (8, 2, 2), (256, 1, 8)],      # guS8nf2 155 us, guS2nf2 165, gu_nf8 168-320
+}
+
+
+def tiled_only(N_: int, K: int) -> bool:
+    return (N_, K) in TILED_ONLY
+
+
+def linear_tiled(x: torch.Tensor, wt: torch.Tensor, N_: int, epilogue: Optional[str] = None) -> torch.Tensor:
+    """``linear`` for a weight kept only as its fragment-tiled copy (``TILED_ONLY``): the prefill tile
+    kernel's tiled form above 256 rows, the decode kernels below (gate|up + SiLU only)."""
+    M, K = x.shape
+    if epilogue != "silu":
+        raise ValueError("tiled-only weights: gate|up with the SiLU epilogue only")
+    if not N.use_native(x) or x.stride(1) != 1 or x.stride(0) % 8:
+        return linear(x, untile_weight(wt).contiguous(), epilogue=epilogue)
+    if M > 256:
+        return prefill_gemm_tiled(x, wt, N_, "silu")
+    for max_m, S, nf in TILED_ONLY_GATEUP.get((N_, K), [(256, 1, 8)]):
+        if M <= max_m:
+            return gateup_silu(x, wt, N_, nf) if S == 1 else gateup_splitk(x, wt, N_, S, nf)
+    return gateup_silu(x, wt, N_, 8)
+
+
 def uses_tiled_weight(N_: int, K: int) -> bool:
     """Does any decode kernel stream a fragment-tiled copy of an [N, K] weight?  Only shapes with a
     measured entry (``TUNING`` skinny, ``SPLITK``, ``GATEUP``) do; everything else stays on
     hipBLASLt and a tiled copy would only take HBM from the KV pool (Llama-3-70B at TP=1: 62 GB)."""
-    if (N_, K) in TUNING:                 # the skinny kernel reads tiled weights only
+    if (N_, K) in TUNING or (N_, K) in TILED_ONLY:   # the skinny kernel reads tiled weights only
         return True
     if DECODE_WEIGHTS == "rowmajor" or (N_, K) in TILE_FREE:
         return False
