@@ -78,7 +78,6 @@ def test_tiled_only_gate_up_weights(monkeypatch):
 
 
 @pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
-def test_graph_decode_matches_eager(model):@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
 def test_graph_decode_matches_eager(model):
     """bf16 Mixtral included: its decode MoE must be capturable (no host sync)."""
     base = dict(model=model, device="cuda", num_kv_blocks=128, max_model_len=2048, max_num_seqs=16,
