@@ -279,7 +279,9 @@ def _wrow(rowmajor: bool, M: int = 0, N_: int = 0, K: int = 0) -> int:
 # profiles/r5_tile_gemm_fragment_tiled_w.jsonl) and the decode kernels.  Llama-3-70B TP=1 gate|up: its
 # row-major decode stream lost to hipBLASLt from 17 rows (4.3 TB/s), the tiled fused kernel wins
 # (168-198 vs 184-205 us at M = 16-128, profiles/r5_gateup_shapes.jsonl), and a second copy would cost
-# 75 GB of KV pool.  PENNY_TILED_ONLY=0: row-major as before.
+# 75 GB of KV pool.  Config 4 short run (6/2) A/B on one box: 3.25 vs 3.28 turns/s, p50 TTFT 4.38 vs
+# 4.63 s (neutral; profiles/r5_bench_llama70b_tp1_toolsteps3_6x2_tiled_only_gateup.json) -- and no
+# hipBLASLt on the 70B gate|up.  PENNY_TILED_ONLY=0: row-major as before.
 TILED_ONLY = {(57344, 8192)} if os.environ.get("PENNY_TILED_ONLY", "1") != "0" else set()
 # decode configs on the tiled-only gate|up: [(max M, S, nf)], S = 1 -> the fused kernel
 TILED_ONLY_GATEUP: Dict[Tuple[int, int], List[Tuple[int, int, int]]] = {
