@@ -144,7 +144,9 @@ def test_decode_gemm_dispatch_tables(monkeypatch):
     assert gemm.gateup_splitk_config(200, 7168, 8192) == (4, 8, False)
     assert gemm.gateup_splitk_config(1, 57344, 8192) == (8, 2, True)
     assert gemm.gateup_splitk_config(32, 57344, 8192) is None
-    assert gemm.uses_tiled_weight(7168, 8192) and not gemm.uses_tiled_weight(57344, 8192)
+    # the 70B TP=1 gate|up keeps only its tiled copy (TILED_ONLY), else no tiled copy at all (75 GB)
+    assert gemm.uses_tiled_weight(7168, 8192)
+    assert gemm.uses_tiled_weight(57344, 8192) == gemm.tiled_only(57344, 8192)
     assert gemm.uses_tiled_weight(6144, 4096) and gemm.uses_tiled_weight(28672, 4096)
     # Llama-3-70B TP=1 (r5 re-measure): split-K on the row-major stream at every decode M, no copies
     assert gemm.splitk_config(32, 8192, 8192) == (8, 2) and gemm.splitk_config(128, 8192, 8192) == (8, 8)
