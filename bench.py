@@ -12,7 +12,10 @@ One step = one wave of ``--convs`` concurrent turns per GPU (weak scaling: per-G
 ``value`` = whole-job completed turns / max-over-ranks wall time of the K timed waves.
 
     python bench.py --gpus 1 --steps 3 --warmup 1
+    python bench.py --gpus 8 --steps 3 --warmup 1      # spawns its own 8 ranks (torch.distributed.run child)
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 3 --warmup 1
+
+``--gpus N`` must equal the launcher's WORLD_SIZE (non-zero exit otherwise).
 """
 from __future__ import annotations
 
@@ -279,8 +282,47 @@ def _share_host_cpus() -> None:
         torch.set_num_threads(min(per, 16))
 
 
+def _launch_ranks(args, argv) -> int:
+    """``bench.py --gpus N`` started without a launcher: run N local ranks (one per GPU) under
+    ``torch.distributed.run`` as a CHILD process -- never exec, and nothing here has touched the GPU
+    (``import torch`` / ``device_count`` do not initialise it) -- forward its output and exit code.
+    The reference's scale-out is likewise N worker processes (gunicorn.conf.py:8-9)."""
+    import socket
+    import subprocess
+    if args.device == "cuda" and not os.environ.get("PENNY_DIST_BACKEND"):
+        import torch
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            log(f"error: --gpus {args.gpus} but only {ndev} visible GPU(s); set PENNY_DIST_BACKEND=gloo to "
+                "rehearse several ranks on one GPU")
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, PENNY_BENCH_SPAWNED="1")
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main(argv=None) -> int:
     args = parse(argv)
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus < 1:
+        log(f"error: --gpus {args.gpus}")
+        return 2
+    if not launched and args.gpus > 1:
+        return _launch_ranks(args, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # a silent mismatch would print n_gpus for a different job than the one asked for
+        log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE {world} ranks")
+        return 2
+    if args.gpus % args.tp:
+        log(f"error: --gpus {args.gpus} not divisible by --tp {args.tp}")
+        return 2
     if args.max_batched_tokens is None:
         args.max_batched_tokens = 16384 if args.model.startswith("mixtral") else 4096
     os.environ.setdefault("LOG_LEVEL", "WARNING")
@@ -292,8 +334,6 @@ def main(argv=None) -> int:
 
     from financial_chatbot_llm_amd.parallel.dist import init_distributed
     ps = init_distributed(tp_size=args.tp, device_type=args.device)
-    if ps.world_size != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ps.world_size}")
     res = asyncio.run(run(args, ps))
     if ps.world_size > 1:
         # every rank joins (TP followers contribute None); the replicas' results are the leaders'
@@ -346,6 +386,9 @@ def main(argv=None) -> int:
             "host": {"cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
                      "world_size": ps.world_size, "backend": ps.backend,
                      "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                     "launcher": ("bench.py self-spawn (torch.distributed.run child)"
+                                  if os.environ.get("PENNY_BENCH_SPAWNED") else
+                                  "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process"),
                      "ranks": hosts},
         }
         line = json.dumps(out)

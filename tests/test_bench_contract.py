@@ -25,6 +25,14 @@ def _json_lines(out: str):
     return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
 
 
+def _clean_env(**kw):
+    """The environment of a plain shell: no launcher variables leaking in from the test runner."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
 def _check(d, n):
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
     assert d["metric"] == base["metric"]
@@ -43,6 +51,40 @@ def test_bench_single_process_json_contract():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 1)
+
+
+@pytest.mark.timeout(400)
+def test_bench_self_spawns_ranks_without_launcher():
+    """a plain ``bench.py --gpus 2`` (no torchrun) starts its own 2 ranks and reports
+    them -- the driver's 1->8 scaling run must never silently measure one GPU."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, capture_output=True, text=True,
+                       timeout=380, env=_clean_env(OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    assert lines[0]["host"]["world_size"] == 2 and lines[0]["host"]["launcher"].startswith("bench.py self-spawn")
+
+
+@pytest.mark.timeout(400)
+def test_bench_self_spawns_tensor_parallel_without_launcher():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--tp", "2", *ARGS], cwd=ROOT, capture_output=True,
+                       text=True, timeout=380, env=_clean_env(OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["host"]["world_size"] == 2 and d["config"]["parallelism"] == "dp1tp2"
+    assert d["turn_errors"] == 0 and d["value"] > 0
+
+
+def test_bench_world_mismatch_fails_loudly():
+    """--gpus disagreeing with the launcher's WORLD_SIZE is an error, not a warning."""
+    env = _clean_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE 1" in r.stderr
+    assert _json_lines(r.stdout) == []
 
 
 @pytest.mark.timeout(400)
@@ -88,6 +130,21 @@ def test_bench_tensor_parallel_replica_gloo_json_contract():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp1tp2" and d["config"]["global_batch"] == 3
     assert d["turn_errors"] == 0 and d["value"] > 0
     assert abs(d["ms_per_step"] - 1e3 * 3 / d["value"]) / d["ms_per_step"] < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_self_spawn_on_one_gpu():
+    """``bench.py --gpus 2`` with no launcher on the device (two ranks share cuda:0 over gloo)."""
+    env = _clean_env(OMP_NUM_THREADS="2", PENNY_DIST_BACKEND="gloo", PENNY_KV_FRACTION="0.05")
+    gpu_args = ["--device" if a == "--device" else ("cuda" if a == "cpu" else a) for a in ARGS]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *gpu_args], cwd=ROOT, capture_output=True,
+                       text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    assert lines[0]["host"]["world_size"] == 2
 
 
 @pytest.mark.gpu
