@@ -110,7 +110,7 @@ class EngineConfig:
     custom_all_reduce: bool = True          # TP decode all-reduces on the one-shot xGMI P2P kernel
     custom_ar_self_test: bool = True        # init-time check of the custom kernels vs the exact sum
     step_ring: bool = True                  # C4 step broadcast over the node-local shm ring (else gloo)
-    tp_dual_decode: bool = True             # TP graph decode as two micro-batch chains on two streams
+    tp_dual_decode: bool = False            # TP graph decode as two micro-batch chains on two streams (opt-in until an 8-GPU A/B exists)
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
@@ -191,7 +191,7 @@ class EngineConfig:
             custom_all_reduce=_env_bool("PENNY_CUSTOM_AR", True),
             step_ring=_env_bool("PENNY_STEP_RING", True),
             custom_ar_self_test=_env_bool("PENNY_AR_SELF_TEST", True),
-            tp_dual_decode=_env_bool("PENNY_TP_DUAL_DECODE", True),
+            tp_dual_decode=_env_bool("PENNY_TP_DUAL_DECODE", False),
             use_cuda_graph=_env_bool("PENNY_HIPGRAPH", True),
             device=_env("PENNY_DEVICE", cls.device),
         )

@@ -19,8 +19,15 @@
 //     system-scope acquire, barrier, system-scope acquire fence, then reads;
 //   * buffers are allocated uncached (hipDeviceMallocUncached): remote reads never hit a stale
 //     L2 line of an earlier round;
-//   * every wait is bounded (wall clock, 5 s): a missing peer sets *err and the kernel exits, so
-//     a dead rank can never wedge the GPU -- the host raises on the error flag.
+//   * every wait is bounded (wall clock, 5 s).  A rank whose wait expires FAILS the collective
+//     instead of summing whatever the peer buffers hold: it sets *err, POISONS its flag slots in
+//     every peer's signal area (a negative value, which every later poll of that slot sees at no
+//     extra cost: the poll already loads it), and writes NaN into its output.  A rank that polls a
+//     poisoned slot fails the same way, and a rank whose *err is set fails at its next launch
+//     without publishing -- so one stalled peer turns every rank's collectives into NaN + err
+//     within one round, the host sees err with the step's sampled ids (model_runner.PendingStep)
+//     and the TP group falls back to RCCL together (parallel/comm.py).  A dead rank can never
+//     wedge the GPU and never yields a silently wrong sum.
 #include <string.h>
 
 #include "common.h"
@@ -28,10 +35,11 @@
 #define AR_MAX_RANKS 8
 #define AR_MAX_BLOCKS 64
 #define AR_TIMEOUT_TICKS (5ull * 100000000ull)  // wall_clock64() runs at 100 MHz
+#define AR_POISON (-1)
 
 struct ArPeers {
   bf16* data[AR_MAX_RANKS];  // each rank's registered data buffer (2 halves of half_elems)
-  int* sig[AR_MAX_RANKS];    // each rank's signal area: [AR_MAX_RANKS source][AR_MAX_BLOCKS]
+  int* sig[AR_MAX_RANKS];    // each rank's signal area: [2 region][AR_MAX_RANKS source][AR_MAX_BLOCKS]
 };
 
 // publish `round` for (region, this rank, this block) in every peer's signal area, after every
@@ -44,22 +52,53 @@ __device__ __forceinline__ void ar_publish(const ArPeers& peers, int region, int
                        __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// wait (bounded) until every peer published `round` for (region, this block), then acquire
-__device__ __forceinline__ void ar_wait(const ArPeers& peers, int region, int rank, int nranks, int round,
-                                        int* err) {
+// this rank failed: every slot it publishes into, in every peer, reads AR_POISON from now on
+__device__ __forceinline__ void ar_poison(const ArPeers& peers, int rank, int nranks) {
+  for (int i = threadIdx.x; i < nranks * 2 * AR_MAX_BLOCKS; i += blockDim.x) {
+    const int q = i / (2 * AR_MAX_BLOCKS), region = (i / AR_MAX_BLOCKS) & 1, b = i % AR_MAX_BLOCKS;
+    if (q != rank)
+      __hip_atomic_store(peers.sig[q] + (region * AR_MAX_RANKS + rank) * AR_MAX_BLOCKS + b, AR_POISON,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+}
+
+// wait (bounded) until every peer published `round` for (region, this block), then acquire.
+// Returns false (block-uniform) when a peer is late past the bound or has poisoned its slot; the
+// caller then fails the collective (ar_fail) instead of reading the peer buffers.
+__device__ __forceinline__ bool ar_wait(const ArPeers& peers, int region, int rank, int nranks, int round,
+                                        int* err, int* s_fail) {
+  if (threadIdx.x == 0) *s_fail = 0;
+  __syncthreads();
   if (threadIdx.x < nranks) {
     const int* slot = peers.sig[rank] + (region * AR_MAX_RANKS + threadIdx.x) * AR_MAX_BLOCKS + blockIdx.x;
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
-      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
-        atomicExch(err, 1);
+    while (true) {
+      const int v = __hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (v < 0 || wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
+        *s_fail = 1;
         break;
       }
+      if (v >= round) break;
       __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
+  if (*s_fail) {
+    if (threadIdx.x == 0) atomicExch(err, 1);
+    ar_poison(peers, rank, nranks);
+    return false;
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  return true;
+}
+
+// NaN over out[base + q * stride + [lo, hi)) for q < reps: a failed collective's output
+__device__ __forceinline__ void ar_fill_nan(bf16* out, long base, long stride, int reps, long lo, long hi) {
+  const uint4 nan8 = make_uint4(0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u, 0x7FC07FC0u);
+  for (int q = 0; q < reps; ++q)
+    for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
+      *reinterpret_cast<uint4*>(out + base + q * stride + i) = nan8;
 }
 
 // out[i..i+7] (or any bf16 destination) <- sum over ranks q = 0..n-1 of peers.data[q][src + i], f32,
@@ -80,16 +119,24 @@ __global__ void __launch_bounds__(256) ar_oneshot_kernel(const bf16* __restrict_
                                                          long n, ArPeers peers, const int* __restrict__ counter,
                                                          int* __restrict__ err, int rank, int nranks,
                                                          long half_elems) {
+  __shared__ int s_fail;
   const int round = *counter + 1;
+  const int dead = *err;                         // loaded beside the counter: no extra latency
   const long off = (round & 1) * half_elems;
   const long per = ((n + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
   const long lo = blockIdx.x * per, hi = min(n, lo + per);
-
+  if (dead) {                                    // failed earlier: never publish again
+    ar_fill_nan(out, 0, 0, 1, lo, hi);
+    return;
+  }
   bf16* mine = peers.data[rank] + off;
   for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
     *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
   ar_publish(peers, 0, rank, nranks, round);
-  ar_wait(peers, 0, rank, nranks, round, err);
+  if (!ar_wait(peers, 0, rank, nranks, round, err, &s_fail)) {
+    ar_fill_nan(out, 0, 0, 1, lo, hi);
+    return;
+  }
   for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
     *reinterpret_cast<uint4*>(out + i) = ar_sum8(peers, nranks, off + i);
 }
@@ -105,23 +152,34 @@ __global__ void __launch_bounds__(256) ar_twoshot_kernel(const bf16* __restrict_
                                                          long n, ArPeers peers, const int* __restrict__ counter,
                                                          int* __restrict__ err, int rank, int nranks,
                                                          long half_elems) {
+  __shared__ int s_fail;
   const int round = *counter + 1;
+  const int dead = *err;
   const long off = (round & 1) * half_elems;
   const long chunk = n / nranks;
   const long per = ((chunk + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
   const long lo = blockIdx.x * per, hi = min(chunk, lo + per);
-
+  if (dead) {
+    ar_fill_nan(out, 0, chunk, nranks, lo, hi);
+    return;
+  }
   bf16* mine = peers.data[rank] + off;
   for (int q = 0; q < nranks; ++q)
     for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
       *reinterpret_cast<uint4*>(mine + q * chunk + i) = *reinterpret_cast<const uint4*>(in + q * chunk + i);
   ar_publish(peers, 0, rank, nranks, round);
-  ar_wait(peers, 0, rank, nranks, round, err);
+  if (!ar_wait(peers, 0, rank, nranks, round, err, &s_fail)) {
+    ar_fill_nan(out, 0, chunk, nranks, lo, hi);
+    return;
+  }
   const long base = (long)rank * chunk;
   for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
     *reinterpret_cast<uint4*>(mine + base + i) = ar_sum8(peers, nranks, off + base + i);
   ar_publish(peers, 1, rank, nranks, round);
-  ar_wait(peers, 1, rank, nranks, round, err);
+  if (!ar_wait(peers, 1, rank, nranks, round, err, &s_fail)) {
+    ar_fill_nan(out, 0, chunk, nranks, lo, hi);
+    return;
+  }
   for (int q = 0; q < nranks; ++q)
     for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
       *reinterpret_cast<uint4*>(out + q * chunk + i) =
@@ -134,15 +192,24 @@ __global__ void __launch_bounds__(256) ar_twoshot_kernel(const bf16* __restrict_
 __global__ void __launch_bounds__(256) ag_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, long n,
                                                  ArPeers peers, const int* __restrict__ counter,
                                                  int* __restrict__ err, int rank, int nranks, long half_elems) {
+  __shared__ int s_fail;
   const int round = *counter + 1;
+  const int dead = *err;
   const long off = (round & 1) * half_elems;
   const long per = ((n + gridDim.x - 1) / gridDim.x + 7) / 8 * 8;
   const long lo = blockIdx.x * per, hi = min(n, lo + per);
+  if (dead) {
+    ar_fill_nan(out, 0, n, nranks, lo, hi);
+    return;
+  }
   bf16* mine = peers.data[rank] + off;
   for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
     *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
   ar_publish(peers, 0, rank, nranks, round);
-  ar_wait(peers, 0, rank, nranks, round, err);
+  if (!ar_wait(peers, 0, rank, nranks, round, err, &s_fail)) {
+    ar_fill_nan(out, 0, n, nranks, lo, hi);
+    return;
+  }
   for (int q = 0; q < nranks; ++q)
     for (long i = lo + threadIdx.x * 8; i < hi; i += 256 * 8)
       *reinterpret_cast<uint4*>(out + q * n + i) = *reinterpret_cast<const uint4*>(peers.data[q] + off + i);

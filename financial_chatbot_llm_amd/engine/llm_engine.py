@@ -21,9 +21,10 @@ from ..ops.attention import KV_BS
 from ..parallel import comm
 from ..parallel.dist import state as pstate
 from ..utils.logging import get_logger
+from ..utils.metrics import METRICS
 from ..utils.profiling import StepProfiler, marker
 from .block_manager import make_block_manager
-from .model_runner import ModelRunner, build_step_inputs, sample_rows
+from .model_runner import CollectiveTimeout, ModelRunner, StepInputs, build_step_inputs, sample_rows
 from .scheduler import Scheduler, StepCostModel
 from .sequence import PENDING, SamplingParams, Sequence, SeqStatus
 from .speculative import PromptLookup, accept_draft
@@ -94,7 +95,7 @@ class LLMEngine:
         if self.ps.tp_size > 1 and device.type == "cuda" and getattr(cfg, "custom_all_reduce", True):
             try:   # collective over the TP group: every rank constructs its engine together
                 comm.enable_custom_all_reduce()
-                if getattr(cfg, "tp_dual_decode", True):
+                if getattr(cfg, "tp_dual_decode", False):
                     comm.enable_second_channel()     # the second decode micro-batch chain's AR
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
@@ -151,7 +152,33 @@ class LLMEngine:
             with marker("engine.cp_prefill"):
                 self.cp.run_pending()      # one layer slice of a long prompt; the step follows
         with marker("engine.step"):
-            return self._step_overlap() if self.async_scheduling else self._step_sync()
+            try:
+                return self._step_overlap() if self.async_scheduling else self._step_sync()
+            except CollectiveTimeout as e:
+                self._collective_failed(e)
+                raise
+
+    def _collective_failed(self, e: BaseException) -> None:
+        """A step's TP all-reduce failed on the device (custom xGMI kernel: a peer missed the bounded
+        wait; the kernels wrote NaN and set the error flag -- allreduce.hip).  Every request on the
+        engine saw stale hidden states, so all are failed (the caller re-raises: AsyncEngine turns it
+        into the reference's error event per waiting turn, main.py:112-122), and the whole TP group
+        switches to RCCL at this step boundary: the leader sends the fallback control message over
+        C4 before any further step, followers apply it in order (``follower_loop``)."""
+        logger.error(f"TP collective failed ({e}); failing {len(self.requests)} request(s), falling back to RCCL")
+        METRICS.inc("custom_ar_runtime_failures")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)      # the in-flight step (its sums are NaN) drains
+        self._inflight = None
+        for seq in list(self.requests.values()):
+            if not seq.finished:
+                self.scheduler.abort(seq)
+                seq.finish_reason = "error"
+        self.requests.clear()
+        if self.ps.tp_size > 1 and self.ps.is_tp_leader:
+            comm.broadcast_step(StepInputs.control(StepInputs.CTRL_RCCL_FALLBACK))
+        comm.fallback_to_rccl(str(e))
+        self.runner.drop_graphs()
 
     # -- overlap (one-step lookahead) ------------------------------------------------------------
     def _samplers(self, batch) -> List[Sequence]:
@@ -537,6 +564,16 @@ class LLMEngine:
         prev = None
         t = self.timing
         steps = 0
+
+        def collect(p) -> None:
+            # a follower's own collective failure is the leader's to act on: the device-side poison
+            # (allreduce.hip) fails the leader's collectives too, and it answers with the fallback
+            # control message; until then this rank keeps replaying in lockstep
+            try:
+                p.result()
+            except CollectiveTimeout as e:
+                logger.error(f"tp follower rank {self.ps.rank}: {e}; waiting for the leader's fallback")
+
         while True:
             t0 = time.perf_counter()
             si = comm.broadcast_step(None)
@@ -544,16 +581,25 @@ class LLMEngine:
             t["recv_s"] = t.get("recv_s", 0.0) + t1 - t0
             if si is None:
                 break
+            if si.control_code == StepInputs.CTRL_RCCL_FALLBACK:
+                if prev is not None:
+                    collect(prev)
+                    prev = None
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                comm.fallback_to_rccl("leader: TP collective failed")
+                self.runner.drop_graphs()
+                continue
             cur = self.runner.launch(si)
             t2 = time.perf_counter()
             t["execute_s"] += t2 - t1
             if prev is not None:
-                prev.result()
+                collect(prev)
             t["post_s"] += time.perf_counter() - t2
             prev = cur
             steps += 1
         if prev is not None:
-            prev.result()
+            collect(prev)
         # the C4 anatomy of this follower: time blocked receiving the leader's steps, launching them,
         # and waiting for its own previous step's results (its GPU time not hidden by the receive)
         logger.info(f"tp follower rank {self.ps.rank}: {steps} steps, recv {t.get('recv_s', 0.0):.2f}s, "

@@ -99,6 +99,19 @@ class StepInputs:
     def num_decode(self) -> int:
         return len(self.ctx_d)
 
+    # -- control messages on the C4 channel (max_q_len < 0, no arrays) -------------------------
+    CTRL_RCCL_FALLBACK = -2          # every TP rank: retire the custom all-reduce, RCCL from here on
+
+    @classmethod
+    def control(cls, code: int) -> "StepInputs":
+        e = np.zeros(0, np.int32)
+        return cls(e, e, e, np.zeros(1, np.int32), e, np.zeros((0, 1), np.int32), code, e, np.zeros((0, 1), np.int32),
+                   np.zeros(0, np.int64), np.zeros(0, np.float32), np.zeros(0, np.int64), e, np.zeros(0, np.float32))
+
+    @property
+    def control_code(self) -> int:
+        return self.max_q_len if self.max_q_len < 0 else 0
+
 
 _DT_NAME = ("<i4", "<i8", "<f4")
 _DT_CODE = {n: i for i, n in enumerate(_DT_NAME)}
@@ -212,7 +225,8 @@ class PendingStep:
             return []
         if self._cpu is not None:
             return self._cpu.tolist()
-        self._event.synchronize()
+        if self._event is not None:
+            self._event.synchronize()
         if self._start is not None:   # device time of the step (PENNY_STEP_GPU_TIMING=1)
             st = self._stats
             st[self._key] += self._start.elapsed_time(self._event) / 1e3
@@ -498,12 +512,16 @@ class ModelRunner:
                     self._staged = None
         n = len(si.logits_idx)
         self.last_sampled[:n].copy_(out[:n].to(torch.int32), non_blocking=True)
+        ar = comm.custom_all_reduce()
         if not self.on_gpu:
-            return PendingStep(out[:n].clone(), n, None, None)
+            cpu = out[:n].clone()
+            if ar is not None:           # a host-side stand-in (tests): its flag is host memory
+                return PendingStep(None, n, torch.cat([cpu.to(torch.int32), ar.err.to(torch.int32)[:1]]), None,
+                                   check_err=True)
+            return PendingStep(cpu, n, None, None)
         host = self._pinned_out[self._out_flip]
         self._out_flip ^= 1
         host[:n].copy_(out[:n], non_blocking=True)
-        ar = comm.custom_all_reduce()
         if ar is not None:
             # the xGMI all-reduce never raises from the device: a peer that missed its bounded wait
             # sets ar.err and the step's sums are stale, so the flag rides the per-step host sync
@@ -515,6 +533,16 @@ class ModelRunner:
 
     def _forward_only(self, si: StepInputs) -> None:
         self._hidden(si)
+
+    def drop_graphs(self) -> None:
+        """Forget every captured decode graph (they bake in the custom all-reduce kernels and its
+        buffers): after a runtime fallback to RCCL (comm.fallback_to_rccl) decode runs eagerly."""
+        if self.on_gpu:
+            torch.cuda.synchronize(self.device)
+        self.graphs.clear()
+        self.graphs_filt.clear()
+        self.use_graphs = False
+        self._dual = False
 
     # ------------------------------------------------------------------------------------
     # hipGraph decode

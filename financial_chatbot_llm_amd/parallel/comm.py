@@ -126,6 +126,31 @@ def disable_custom_all_reduce() -> None:
         if ar is not None:
             ar.close()
     _CUSTOM_AR = _CUSTOM_AR_2 = None
+    while _RETIRED:
+        _RETIRED.pop().close()
+
+
+_RETIRED: List[Any] = []   # instances retired at runtime: mapped until shutdown (a late peer may still read)
+
+
+def fallback_to_rccl(reason: str) -> None:
+    """Runtime failure of the custom all-reduce (a peer missed the bounded wait, the kernels
+    returned NaN with the error flag set): from the next collective on, RCCL carries every TP
+    all-reduce / all-gather of this rank.  Called by EVERY TP rank at the same step boundary (the
+    leader decides and sends ``StepInputs.CTRL_RCCL_FALLBACK`` over C4 before its next step), so the
+    group never mixes RCCL and custom collectives.  The IPC buffers stay mapped until shutdown: a
+    stalled peer can still be inside a kernel that reads them.  The reference's failure contract
+    (main.py:112-122): errors reach the client, never a silently wrong answer."""
+    import logging
+    global _CUSTOM_AR, _CUSTOM_AR_2
+    for ar in (_CUSTOM_AR, _CUSTOM_AR_2):
+        if ar is not None:
+            _RETIRED.append(ar)
+    _CUSTOM_AR = _CUSTOM_AR_2 = None
+    AR_STATUS.update(custom=False, runtime_fallback=reason,
+                     runtime_fallbacks=int(AR_STATUS.get("runtime_fallbacks", 0)) + 1)
+    logging.getLogger(__name__).error(f"custom all-reduce failed at runtime ({reason}); RCCL carries every TP "
+                                      "collective from now on")
 
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:

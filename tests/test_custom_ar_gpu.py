@@ -22,10 +22,15 @@ def _free_port() -> int:
 
 
 def _timeout_worker(rank, world, port, q):
-    """Rank 1 never joins the last all-reduce: rank 0's bounded wait expires, the kernel exits with
-    the error flag set, and the engine's per-step sync (PendingStep) raises CollectiveTimeout."""
+    """Rank 1 misses an all-reduce: rank 0's bounded wait expires and the kernel FAILS the
+    collective -- NaN output (never a sum of stale peer buffers), the error flag set, its slots in
+    the peer poisoned -- and the engine's per-step sync (PendingStep) raises CollectiveTimeout.
+    Rank 0's next call fails at once (a dead rank never publishes again); the late rank 1 polls a
+    poisoned slot and fails at once too (allreduce.hip)."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
+        import time
+
         import torch.distributed as dist
 
         from financial_chatbot_llm_amd.engine.model_runner import CollectiveTimeout, PendingStep
@@ -42,9 +47,9 @@ def _timeout_worker(rank, world, port, q):
         torch.cuda.synchronize()
         ar.check()
         dist.barrier()
-        raised = None
+        out = {}
         if rank == 0:
-            ar.all_reduce(x)                    # the peer never arrives
+            y = ar.all_reduce(x)                # the peer never arrives
             host = torch.zeros(3, dtype=torch.int32).pin_memory()
             host[2:3].copy_(ar.err, non_blocking=True)
             ev = torch.cuda.Event()
@@ -52,10 +57,24 @@ def _timeout_worker(rank, world, port, q):
             try:
                 PendingStep(None, 2, host, ev, check_err=True).result()
             except CollectiveTimeout as e:
-                raised = str(e)
+                out["raised"] = str(e)
+            out["nan"] = bool(torch.isnan(y.float()).all())
+            t0 = time.perf_counter()
+            y2 = ar.all_reduce(x)               # dead rank: fails without waiting
+            torch.cuda.synchronize()
+            out["dead_s"] = time.perf_counter() - t0
+            out["dead_nan"] = bool(torch.isnan(y2.float()).all())
+        dist.barrier()
+        if rank == 1:
+            t0 = time.perf_counter()
+            y = ar.all_reduce(x)                # the late peer: rank 0's slots are poisoned
+            torch.cuda.synchronize()
+            out["late_s"] = time.perf_counter() - t0
+            out["late_nan"] = bool(torch.isnan(y.float()).all())
+            out["late_err"] = int(ar.err.item())
         dist.barrier()
         ar.close()
-        q.put((rank, "OK", raised))
+        q.put((rank, "OK", out))
         dist.destroy_process_group()
     except Exception:  # noqa: BLE001
         import traceback
@@ -172,5 +191,7 @@ def test_custom_all_reduce_processes(world):
 @pytest.mark.timeout(120)
 def test_custom_all_reduce_missing_peer_fails_the_step():
     res = _run(_timeout_worker, 2)
-    assert res[0][1] is not None and "missed the bounded wait" in res[0][1]
-    assert res[1][1] is None
+    r0, r1 = res[0][1], res[1][1]
+    assert "missed the bounded wait" in r0["raised"]
+    assert r0["nan"] and r0["dead_nan"] and r0["dead_s"] < 1.0, r0
+    assert r1["late_nan"] and r1["late_err"] == 1 and r1["late_s"] < 1.0, r1
