@@ -1364,6 +1364,14 @@ def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)
                                     gemm.prefill_gemm(x, w, "slabs", S, out=P), out=y))
                             else:
                                 fns[f"hipS{S}"] = lambda S=S, P=P: gemm.prefill_gemm(x, w, "slabs", S, out=P)
+            # the 128 x 128 tile kernel (gemm_mid.hip) with S K-slices, in the form each consumer takes
+            for S in (1, 2, 3, 4, 8):
+                if K % (64 * S) or N % 128:
+                    continue
+                if kind == "gateup":
+                    fns[f"mid{S}"] = lambda S=S: gemm.mid_linear(x, w, S, "silu")
+                else:
+                    fns[f"mid{S}"] = lambda S=S: gemm.mid_linear(x, w, S, None, slabs=kind == "col")
             t = interleaved(fns, rounds=5, iters=5)
             best = min((k for k in t if k != "lib"), key=lambda k: t[k]) if len(t) > 1 else "lib"
             row = {"op": "shard_shapes_prefill", "name": name, "N": N, "K": K, "kind": kind, "M": M,
@@ -1447,7 +1455,9 @@ def main(argv=None) -> int:
                 "gateup70b": lambda d: bench_gateup(d, 57344, 8192),
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
-                "shard_shapes": bench_shard_shapes, "rm_pair": bench_rm_pair, "gemm_tiled_w": bench_gemm_tiled_w, "gemm_group": bench_gemm_group,
+                "shard_shapes": bench_shard_shapes,
+                "mid_shards": lambda d: bench_shard_shapes(d, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_up",
+                                                                     "70b_tp8_down", "70b_tp1_qkv"), Ms=()), "rm_pair": bench_rm_pair, "gemm_tiled_w": bench_gemm_tiled_w, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",
                                                                   "70b_tp8_gate_up", "70b_tp8_down"),
                                                         Ms=(96, 112, 128, 144, 160, 192, 256)), "chunked_prefill": bench_chunked_prefill,

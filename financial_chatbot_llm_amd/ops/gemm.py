@@ -95,6 +95,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None,
             return prefill_gemm(x, w, epilogue, residual=residual)
         if c.startswith("S"):
             return Slabs(prefill_gemm(x, w, "slabs", int(c[1:])))
+        if c.startswith("M"):
+            return mid_linear(x, w, int(c[1:]), epilogue, slabs and residual is None, residual)
     # the decode kernels stream either the fragment-tiled copy or (DECODE_WEIGHTS == "rowmajor",
     # or no copy was made) the row-major weight itself
     src = wt if wt is not None else (w if w.is_contiguous() else None)
@@ -571,7 +573,59 @@ def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slab
         choice = "hip"
     if choice.startswith("K") and epilogue is not None:
         choice = "lib"
+    if choice.startswith("M") and (N_ % 128 or K % (64 * int(choice[1:])) or
+                                   (epilogue == "residual" and int(choice[1:]) > 1)):
+        choice = "lib"
     return choice
+
+
+# ----------------------------------------------------------------------------------------------
+# 128 x 128 tile kernel (gemm_mid.hip): the narrow TP shards and small prefill steps, where the
+# 256 x 256 tile leaves most CUs idle.  PREFILL_POLICY choice "M<S>": S = 1 fused epilogue, S > 1
+# split-K slabs (the consumer's reduce, or penny_splitk_reduce{,_silu} for bf16 / SiLU outputs).
+# ----------------------------------------------------------------------------------------------
+MID_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3}
+
+
+def mid_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None, S: int = 1,
+             residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ w.T on the 128 x 128 tile kernel: bf16 [M, N]; "silu" -> silu(gate)*up bf16 [M, N/2] of the
+    interleave16 gate|up weight; "slabs" -> f32 split-K partials [S, M, N]; "residual" -> bf16 + R."""
+    M, K = x.shape
+    N_ = w.shape[0]
+    if not N.use_native(x):
+        return prefill_gemm(x, w, epilogue, S, residual=residual, out=out)
+    if epilogue == "slabs":
+        y = out if out is not None else torch.empty((S, M, N_), dtype=torch.float32, device=x.device)
+        ldy = N_
+    else:
+        S = 1
+        cols = N_ // 2 if epilogue == "silu" else N_
+        y = out if out is not None else torch.empty((M, cols), dtype=x.dtype, device=x.device)
+        ldy = y.stride(0)
+    N.call("penny_gemm_mid", N.ptr(x), x.stride(0), N.ptr(w), K, N.ptr(y), ldy, N.ptr(residual),
+           residual.stride(0) if residual is not None else 0, M, N_, S, MID_EPI[epilogue], N.stream())
+    return y
+
+
+def mid_linear(x: torch.Tensor, w: torch.Tensor, S: int, epilogue: Optional[str] = None, slabs: bool = False,
+               residual: Optional[torch.Tensor] = None) -> Union[torch.Tensor, "Slabs"]:
+    """``linear`` on the 128 x 128 tile kernel with S K-slices: the fused epilogue at S = 1; at S > 1
+    the slabs themselves where the consumer reduces them (``slabs``), else the reduce pass with the
+    bf16 / SiLU output."""
+    if S == 1:
+        return mid_gemm(x, w, epilogue, residual=residual)
+    P = mid_gemm(x, w, "slabs", S)
+    if epilogue == "silu":
+        M, N_ = x.shape[0], w.shape[0]
+        if not N.use_native(x):
+            return silu_mul(P.sum(0).to(x.dtype), interleave16=True)
+        y = torch.empty((M, N_ // 2), dtype=x.dtype, device=x.device)
+        N.call("penny_splitk_reduce_silu", N.ptr(P), S, M, N_, N.ptr(y), y.stride(0), N.stream())
+        return y
+    if slabs and residual is None:
+        return Slabs(P)
+    return splitk_reduce(P, residual=residual)
 
 
 def qkv_rope_fused(x: torch.Tensor, w: torch.Tensor, D: int) -> bool:

@@ -1550,3 +1550,50 @@ def test_rope_qk_matches_reference(D):
     ref = _rope_ref(qkv.view(T, -1, D)[:, :Hq + Hkv].float(), pos, cs)
     assert got.shape == (T, Hq + Hkv, D)
     close(got, ref, atol=2e-2)
+
+
+# ---- 128 x 128 tile kernel (gemm_mid.hip): the Llama-3-70B TP=8 shard shapes ----
+@pytest.mark.parametrize("name,M,S", [("qkv", 384, 4), ("qkv", 1000, 1), ("o", 300, 1), ("o", 1536, 2),
+                                       ("gate_up", 513, 1), ("gate_up", 384, 2), ("down", 257, 1), ("down", 768, 2)])
+def test_mid_gemm_tp8_shard_shapes_vs_fp32(name, M, S):
+    """Every epilogue form of the mid tile kernel at the 70B TP=8 shards against fp32 on the GPU:
+    QKV (1280 x 8192) slabs for the RoPE pass, O (8192 x 1024) and down (8192 x 3584) bf16 for the
+    all-reduce (S > 1: slabs + penny_splitk_reduce), gate|up (7168 x 8192 interleave16) + SiLU (S > 1:
+    slabs + reduce-SiLU); M not a multiple of the 128-row tile included."""
+    from financial_chatbot_llm_amd.ops import gemm
+    N_, K = {"qkv": (1280, 8192), "o": (8192, 1024), "gate_up": (7168, 8192), "down": (8192, 3584)}[name]
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + S)
+    x = torch.randn((M, K), generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((N_, K), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    if name == "gate_up":
+        y = gemm.mid_linear(x, w, S, "silu")
+        gt = ref.to(torch.bfloat16).float().view(M, N_ // 32, 2, 16)
+        ref = (torch.nn.functional.silu(gt[:, :, 0]) * gt[:, :, 1]).reshape(M, N_ // 2)
+        assert y.shape == (M, N_ // 2)
+        close(y, ref, atol=2e-2 * ref.abs().max().item())
+        return
+    if name == "qkv" and S > 1:
+        out = gemm.mid_linear(x, w, S, None, slabs=True)
+        assert isinstance(out, gemm.Slabs) and out.P.shape == (S, M, N_)
+        close(out.P.sum(0), ref, atol=1e-3 * ref.abs().max().item(), rtol=1e-3)
+        return
+    y = gemm.mid_linear(x, w, S)
+    assert y.shape == (M, N_) and y.dtype == torch.bfloat16
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+
+
+def test_mid_gemm_residual_epilogue_and_slab_exactness():
+    """Residual epilogue (bf16(acc) + R, like GEMM-then-add) and split-K slabs equal to the f32
+    per-slice products."""
+    from financial_chatbot_llm_amd.ops import gemm
+    g = torch.Generator().manual_seed(11)
+    M, N_, K, S = 200, 384, 1024, 4
+    x, w, r = rnd(M, K, gen=g), rnd(N_, K, scale=0.05, gen=g), rnd(M, N_, gen=g)
+    y = gemm.mid_gemm(x.to(DEV), w.to(DEV), "residual", residual=r.to(DEV))
+    ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() + r.float()
+    close(y, ref, atol=2e-2 * ref.abs().max().item())
+    P = gemm.mid_gemm(x.to(DEV), w.to(DEV), "slabs", S)
+    refP = torch.einsum("smk,snk->smn", x.float().view(M, S, K // S).transpose(0, 1),
+                        w.float().view(N_, S, K // S).transpose(0, 1))
+    close(P, refP, atol=1e-3 * refP.abs().max().item(), rtol=1e-3)
