@@ -258,18 +258,21 @@ def bench_prefill_mixed(dev) -> List[Dict]:
         ld = torch.from_numpy(ln).to(dev) if ln is not None else None
         lc = (int(ln[0, 1]), int(ln[0, 2]), int(ln[0, 3])) if ln is not None else None
 
+        # production form: q prescaled by scale * log2(e) at the QKV epilogue's one rounding
+        qp = (q.float() * (0.088 * 1.4426950408889634)).to(torch.bfloat16)
+
         def run(v):
+            var, lean, qpre = v
+
             def f():
-                if isinstance(v, str):
-                    ops.attention.prefill_variant(int(v.split("_")[1]))
-                    ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o,
-                                work=ld if ld is not None else wd, lean=lc)
-                    return
-                ops.attention.prefill_variant(v)
-                ops.prefill(q, cu, lens, tables, kc, vc, 0.088, True, max(qlens), out=o, work=wd)
+                ops.attention.prefill_variant(var)
+                ops.prefill(qp if qpre else q, cu, lens, tables, kc, vc, 1 / 1.4426950408889634 if qpre else 0.088,
+                            True, max(qlens), out=o, work=(ld if ld is not None else wd) if lean else wd,
+                            lean=lc if lean else None, q_prescaled=qpre)
             return f
-        variants = {"pf2_sb": 4, "pf2_fold": 5, "pf2_foldq": 6, "pf2_sb_lean": "lean_4",
-                    "pf2_fold_lean": "lean_5", "pf2_foldq_lean": "lean_6"}
+        variants = {"pf2_sb": (4, False, False), "pf2_fold": (5, False, False), "pf3": (7, False, False),
+                    "pf2_fold_lean": (5, True, False), "pf3_lean": (7, True, False),
+                    "pf2_prod": (5, True, True), "pf3_prod": (7, True, True)}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():
@@ -1368,10 +1371,11 @@ def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)
             for S in (1, 2, 3, 4, 8):
                 if K % (64 * S) or N % 128:
                     continue
-                if kind == "gateup":
-                    fns[f"mid{S}"] = lambda S=S: gemm.mid_linear(x, w, S, "silu")
-                else:
-                    fns[f"mid{S}"] = lambda S=S: gemm.mid_linear(x, w, S, None, slabs=kind == "col")
+                for v in (0, 1, 2):
+                    def mf(S=S, v=v):
+                        gemm.mid_variant(v)
+                        return gemm.mid_linear(x, w, S, "silu" if kind == "gateup" else None, slabs=kind == "col")
+                    fns[f"mid{S}v{v}"] = mf
             t = interleaved(fns, rounds=5, iters=5)
             best = min((k for k in t if k != "lib"), key=lambda k: t[k]) if len(t) > 1 else "lib"
             row = {"op": "shard_shapes_prefill", "name": name, "N": N, "K": K, "kind": kind, "M": M,

@@ -1145,6 +1145,260 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
     lse[(long)(q0 + tok) * Hq + head] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
 }
 
+// ------------------------------------------------------------------------------------------
+// 32x32x16 prefill (variant 7): prefill2's staging pipeline with the block math on
+// v_mfma_f32_32x32x16_bf16.  Each MFMA holds the SIMD's vector issue for 8 of its 32 cycles instead
+// of 8 of 16 (16x16x32), so the softmax VALU (~100 instructions per block and wave, 32 of them
+// 8-cycle v_exp) fits in the shadow of a block's 32 MFMAs instead of bounding the loop
+// (MI355X_MICROARCH.md cycle constants: 'vector-instruction ISSUE cost').
+//
+// Orientation as in prefill2 (S^T = K.Q^T, O^T = V^T.P^T), one wave = 32 query rows = the 32 MFMA
+// columns: lane (c = lane & 31, h = lane >> 5) holds query row c and, per 32-key S^T tile, keys of
+// tile rows (reg & 3) + 8 (reg >> 2) + 4h.  Tile row rho of key tile T is key pi(32T + rho), pi
+// swapping bits 3 and 4 of the row index: with that permutation
+//   * the K fragment of (T, k-step c) is one 16-B piece of the fragment-native K block at
+//     lane base + 8192 T + 512 c (kv_layout.h k_index), and
+//   * the P^T operand of P.V k-step s is registers 8(s&1) .. +7 of S^T tile s >> 1 converted to
+//     bf16 in place (cdna_hip_programming.md §3 'An accumulator tile as the next MFMA's operand'),
+//     whose keys are exactly the 8 keys the fragment-native V block holds in ONE 16-B piece for
+//     lane group 2(s&1) + h: V fragment (dim tile dt, s) at lane base + 4096 dt + 512 s.
+// Every fragment read is a ds_read_b128 with an immediate offset from one per-lane base, and both
+// read patterns are bank-conflict free on the 16-lane phases (the stored KV layout is unchanged:
+// decode, the KV writers and the 16x16 kernels read the same blocks).
+// The row max is 31 v_max + one permlane32 swap (lane and lane ^ 32 hold the same query); the row
+// sum stays a per-lane f32 partial, combined once at the end.  Softmax: base 2 with the deferred
+// rescale (threshold 8) of attend_block_fold; QPRE = q arrives prescaled by scale * log2(e) and the
+// S^T chains start at -m (no per-score FMA).
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float lanepair_max(float v) {
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float lanepair_sum(float v) {
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+template <bool QPRE>
+__device__ __forceinline__ void attend_block32(const char* __restrict__ kl, const char* __restrict__ vl,
+                                               const Frag (&qf)[8], f32x16 (&o)[4], float& m, float& l,
+                                               bool causal, int j, int ctx, int qpos, float scale_log2, int h,
+                                               bool need_mask) {
+  Frag kf[2][8];
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kf[T][c].u = *reinterpret_cast<const uint4*>(kl + 8192 * T + 512 * c);
+  const bool fresh = m == -INFINITY;
+  const float m0 = (fresh || !QPRE) ? 0.f : -m;
+  f32x16 sc[2];
+#pragma unroll
+  for (int T = 0; T < 2; ++T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[T][r] = m0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sc[T] = mfma32(kf[T][c].v, qf[c].v, sc[T]);
+  }
+  Frag vf[4][4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) vf[dt][st].u = *reinterpret_cast<const uint4*>(vl + 4096 * dt + 512 * st);
+
+  if (need_mask) {
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = j * KV_BS + 32 * T + 16 * ((r >> 2) & 1) + 8 * (r >> 3) + 4 * h + (r & 3);
+        const bool ok = (key < ctx) & ((!causal) | (key <= qpos));
+        sc[T][r] = ok ? sc[T][r] : -INFINITY;
+      }
+  }
+  float mt = sc[0][0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) mt = vmax_raw(mt, sc[0][r]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) mt = vmax_raw(mt, sc[1][r]);
+  mt = lanepair_max(mt);                      // QPRE: max of s*c - m; else max of s
+  if constexpr (!QPRE) mt = fresh ? mt * scale_log2 : mt * scale_log2 - m;
+  const bool grow = mt > (fresh ? -INFINITY : 8.f);
+  if (__any(grow)) {
+    const float rise = grow ? mt : 0.f;
+    if (grow) {
+      const float alpha = fresh ? 1.f : fast_exp2(-rise);   // fresh: O and l are still 0
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+      m = fresh ? rise : m + rise;
+    }
+    if constexpr (QPRE) {
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[T][r] -= rise;
+    }
+  }
+  float ls = 0.f;
+  if constexpr (QPRE) {
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[T][r] = fast_exp2(sc[T][r]);
+        ls += sc[T][r];
+      }
+  } else {
+    const float mref = m == -INFINITY ? 0.f : m;
+#pragma unroll
+    for (int T = 0; T < 2; ++T)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[T][r] = fast_exp2(fmaf(sc[T][r], scale_log2, -mref));
+        ls += sc[T][r];
+      }
+  }
+  l += ls;
+  Frag pf[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pf[st].v[e] = (bf16)sc[st >> 1][8 * (st & 1) + e];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) o[dt] = mfma32(vf[dt][st].v, pf[st].v, o[dt]);
+}
+
+// prefill2_kernel's grid, work lists, lean slots and K/V staging ring with attend_block32 (D = 128)
+template <int NBUF, bool QPRE>
+__global__ void __launch_bounds__(512, 1) prefill3_kernel(
+    const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    bf16* __restrict__ out, float scale_log2, int Hq, int Hkv, int max_blocks, int causal,
+    float* __restrict__ lse, const int* __restrict__ work, PrefillLean lean = PrefillLean{}) {
+  constexpr int D = 128, NW = 8;
+  constexpr int TILE = KV_BS * D * 2;
+  constexpr int PIECES = TILE / 1024 / NW;
+  constexpr int LOADS = 2 * PIECES;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
+
+  const int item = blockIdx.y;
+  const int* li = lean.items ? lean.items + 6 * item : nullptr;
+  const int s = li ? li[0] : (work ? work[2 * item] : blockIdx.z);
+  const int hk = blockIdx.x;
+  const int tile = li ? li[1] : (work ? work[2 * item + 1] : gridDim.y - 1 - item);
+  const int G = Hq / Hkv;
+  const int TQ = NW * 32 / G;
+  const int q0 = cu_q[s], qlen = cu_q[s + 1] - q0;
+  const int tok0 = tile * TQ;
+  if (tok0 >= qlen) return;
+  const int ctx = ctx_lens[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+
+  const int last_tok = min(tok0 + TQ, qlen) - 1;
+  const int kv_end = causal ? min(ctx, ctx - qlen + last_tok + 1) : ctx;
+  const int nblk_tile = (kv_end + KV_BS - 1) / KV_BS;
+  const int jb = li ? li[2] : 0;
+  const int nblk = li ? min(li[3], nblk_tile) - jb : nblk_tile;
+  const int slot = li ? li[4] : -1;
+  const int* bt = block_tables + (long)s * max_blocks + jb;
+
+  auto stage = [&](int jj) {
+    const long phys = bt[jj];
+    PENNY_DASSERT(phys >= 0);
+    const char* kb = reinterpret_cast<const char*>(k_cache + (phys * Hkv + hk) * (long)(KV_BS * D));
+    const char* vb = reinterpret_cast<const char*>(v_cache + (phys * Hkv + hk) * (long)(KV_BS * D));
+    char* kls = smem + (jj % NBUF) * 2 * TILE;
+    char* vls = kls + TILE;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int piece = w * PIECES + i;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(kb + piece * 1024 + lane * 16), (lds_void_t*)(kls + piece * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(vb + piece * 1024 + lane * 16), (lds_void_t*)(vls + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int jj = 0; jj < NBUF - 1; ++jj)
+    if (jj < nblk) stage(jj);
+
+  // this lane's query row and its 8 Q fragments (B operand: dims 16c' + 8h .. +7 of the row)
+  const int r = w * 32 + c;
+  const int tok = tok0 + r / G, head = hk * G + r % G;
+  const bool valid = tok < qlen;
+  const int qpos = valid ? ctx - qlen + tok : ctx - 1;
+  Frag qf[8];
+  {
+    const bf16* qrow = q + ((long)(q0 + (valid ? tok : 0)) * Hq + head) * D;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc)
+      qf[cc].u = valid ? *reinterpret_cast<const uint4*>(qrow + cc * 16 + h * 8) : make_uint4(0, 0, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);        // vmcnt(0): Q resident (a wait hipcc can see)
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  // per-lane fragment bases: K key-row pi(r) at 16 (256 r3 + 16 h + 8 r4 + (r & 7)); V dim row r at
+  // 2048 (r >> 4) + 256 h + 16 (r & 15)
+  const int kbase = 16 * (256 * ((c >> 3) & 1) + 16 * h + 8 * (c >> 4) + (c & 7));
+  const int vbase = 2048 * (c >> 4) + 256 * h + 16 * (c & 15);
+
+  const int wave_tok0 = tok0 + (w * 32) / G;
+  const bool wave_live = wave_tok0 < qlen;
+  const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
+  const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
+  for (int jj = 0; jj < nblk; ++jj) {
+    if (jj + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
+    else wait_vmcnt_barrier<0>();
+    if (jj + NBUF - 1 < nblk) stage(jj + NBUF - 1);
+    const int ja = jb + jj;
+    if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
+    const char* kls = smem + (jj % NBUF) * 2 * TILE;
+    const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
+    attend_block32<QPRE>(kls + kbase, kls + TILE + vbase, qf, o, m, l, causal, ja, ctx, qpos, scale_log2, h,
+                         __builtin_amdgcn_readfirstlane((int)!full) != 0);
+  }
+
+  const float lt = lanepair_sum(l);
+  if (slot >= 0) {                            // a chunk of a split walk: partial state for the merge
+    const long pr = ((long)slot * Hkv + hk) * 256 + r;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg)
+        *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 32 * dt + 8 * rg + 4 * h) =
+            f32x4{o[dt][4 * rg], o[dt][4 * rg + 1], o[dt][4 * rg + 2], o[dt][4 * rg + 3]};
+    if (h == 0) {
+      lean.part_ml[2 * pr] = m;
+      lean.part_ml[2 * pr + 1] = lt;
+    }
+    return;
+  }
+  if (!valid) return;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  bf16* orow = out + ((long)(q0 + tok) * Hq + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      bf16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[dt][4 * rg + e] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * rg + 4 * h) = v4;
+    }
+  if (lse != nullptr && h == 0)
+    lse[(long)(q0 + tok) * Hq + head] = lt > 0.f ? (m + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
+}
+
 static int prefill_variant();
 
 // Lean big-tile prefill: items [nitems, 6] (see PrefillLean; LPT order), merge [nmerge, 6];
@@ -1169,7 +1423,16 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                      (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
                      (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
 #define LEAN_VARIANTS(DD)                                   \
-  if (var == 6 || qpre) LEAN_LAUNCH(DD, true, true, 2);    \
+  if (DD == 128 && var == 7) {                              \
+    if (qpre)                                               \
+      hipLaunchKernelGGL((prefill3_kernel<3, true>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens, \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,   \
+                         max_blocks, causal, lse, (const int*)nullptr, lean);                                  \
+    else                                                    \
+      hipLaunchKernelGGL((prefill3_kernel<3, false>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens, \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,    \
+                         max_blocks, causal, lse, (const int*)nullptr, lean);                                   \
+  } else if (var == 6 || qpre) LEAN_LAUNCH(DD, true, true, 2); \
   else if (var == 4) LEAN_LAUNCH(DD, true, true, 0);        \
   else LEAN_LAUNCH(DD, true, true, 1);                      \
   if (nmerge > 0)                                           \
@@ -1238,7 +1501,16 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   const dim3 grid2 = wl ? dim3(Hkv, nwork, 1) : dim3(Hkv, ntiles, num_seqs);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && (pp_env == 6 || qpre))                                                                              \
+  if (big && DD == 128 && pp_env == 7) {                                                                         \
+    if (qpre)                                                                                                    \
+      hipLaunchKernelGGL((prefill3_kernel<3, true>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens,  \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,     \
+                         max_blocks, causal, lse, wp);                                                           \
+    else                                                                                                         \
+      hipLaunchKernelGGL((prefill3_kernel<3, false>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens, \
+                         block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,      \
+                         max_blocks, causal, lse, wp);                                                            \
+  } else if (big && (pp_env == 6 || qpre))                                                                       \
     hipLaunchKernelGGL((prefill2_kernel<DD, 8, 3, true, true, true, 2>), grid2, dim3(512), 0, stream,            \
                        (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,   \
                        (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, wp);                                     \

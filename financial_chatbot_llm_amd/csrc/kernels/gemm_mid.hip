@@ -12,21 +12,20 @@
 // Structure (gfx950): 256 threads = 4 waves as 2 (W rows) x 2 (tokens), each wave a 64 x 64
 // (n x token) sub-tile of 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators (MFMA A = W: a lane's 4
 // accumulator registers are 4 consecutive output columns, as in gemm_prefill.hip).  Both operands
-// are staged by LDS-DMA (global_load_lds_dwordx4, 1-KiB lane-linear pieces of 8 rows x 128 B)
-// with the XOR chunk swizzle chunk ^ ((row >> 1) & 7) on the source address and on the fragment
-// read (conflict-free ds_read_b128 phases).  Two K-tile buffers of 32 KiB: the next K-tile's DMA
-// is in flight while the current one is on the MFMAs, one counted wait + barrier per K-tile
-// (the guide's minimum two-phase recipe), 64 KiB of LDS so two workgroups share a CU and one's
-// MFMAs cover the other's barrier.  Workgroup ids are remapped bijectively over the 8 XCDs with
+// are staged by LDS-DMA (global_load_lds_dwordx4, 1-KiB lane-linear pieces) with an XOR chunk
+// swizzle on the source address and on the fragment read (conflict-free ds_read_b128 phases), in a
+// ring of stages (mid_variant below): one wait + barrier per stage, the next stages' DMA in flight
+// while the current one is on the MFMAs, and LDS sized so two or three workgroups share a CU and
+// one's MFMAs cover the others' barriers.  Workgroup ids are remapped bijectively over the 8 XCDs with
 // the token tile fastest: an XCD's concurrent workgroups share W panels in its L2.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace {
 
 constexpr int MT = 128;                 // token rows per tile
 constexpr int NT_ = 128;                // W rows (output columns) per tile
-constexpr int IMG = 128 * 128;          // one operand's K-tile image: 128 rows x 128 B = 16 KiB
-constexpr int STAGE = 2 * IMG;          // W image, then X image
 enum { MEPI_BF16 = 0, MEPI_SILU = 1, MEPI_SLAB = 2, MEPI_RESID = 3 };
 
 union Frag {
@@ -37,8 +36,6 @@ union Pack8 {
   uint4 u;
   bf16 e[8];
 };
-
-__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 // lo = columns 16f + 4g .. +3 and hi = 16(f+1) + 4g .. +3 of lane row g -> 8 consecutive columns
 // 8*(g>>1) + 16*(g&1) .. +7 of this lane (v_permlane16_swap: one 16-B store instead of two 8-B ones)
@@ -54,12 +51,34 @@ __device__ __forceinline__ uint4 pair16(bf16x4 lo, bf16x4 hi) {
   return make_uint4(x[0], y[0], x[1], y[1]);
 }
 
-template <int EPI>
-__global__ void __launch_bounds__(256, 2) gemm_mid_kernel(const bf16* __restrict__ X, int ldx,
-                                                          const bf16* __restrict__ W, int K, void* __restrict__ Y,
-                                                          int ldy, const bf16* __restrict__ R, int ldr, int M, int N,
-                                                          int S) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+// Staging geometry: RB bytes of K per row per stage (128: BK = 64, two MFMA k-steps; 64: BK = 32, one
+// k-step), NST stages in the LDS ring (NST = 2: one vmcnt(0) + barrier per stage; NST >= 3: the
+// counted wait of prefill2 -- stage t+NST-1 streams in while stage t is on the MFMAs).
+// Chunk swizzles, conflict-free over the four 16-lane phases of the fragment ds_read_b128 (lanes of
+// a phase read rows l & 15 at chunk 4kk + (l >> 4)): 128-B rows (2 per bank row) chunk ^ ((r >> 1) & 7)
+// as gemm_prefill.hip; 64-B rows (4 per bank row) chunk ^ {0, 2, 3, 1}[(r >> 2) & 3] (checked by hand
+// over the phases: the four rows r = a + 4i of a phase land on distinct 16-B slots).
+template <int RB>
+__device__ __forceinline__ int mswz(int r) { return RB == 128 ? (r >> 1) & 7 : (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+template <int N_>
+__device__ __forceinline__ void mid_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N_) : "memory");
+}
+
+template <int EPI, int RB, int NST>
+__global__ void __launch_bounds__(256, (NST * 2 * 128 * RB <= 49152) ? 3 : (NST * 2 * 128 * RB <= 65536 ? 2 : 1))
+gemm_mid_kernel(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W, int K, void* __restrict__ Y, int ldy,
+                const bf16* __restrict__ R, int ldr, int M, int N, int S) {
+  constexpr int OPB = 128 * RB;            // one operand's stage image
+  constexpr int STG = 2 * OPB;             // W image, then X image
+  constexpr int CPR = RB / 16;             // 16-B chunks per row
+  constexpr int RPP = 1024 / RB;           // rows per 1-KiB DMA piece
+  constexpr int PPW = 128 / RPP / 4;       // pieces per operand per wave
+  constexpr int LPS = 2 * PPW;             // DMA instructions per wave per stage
+  constexpr int KS = RB / 64;              // MFMA k-steps per stage
+  constexpr int BKE = RB / 2;              // K elements per stage
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STG];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wa = w >> 1, wb = w & 1;     // wave grid 2 (W rows) x 2 (tokens)
@@ -74,30 +93,31 @@ __global__ void __launch_bounds__(256, 2) gemm_mid_kernel(const bf16* __restrict
   }
   const int tm = id % Mt, rest = id / Mt, tn = rest % Nt, s = rest / Nt;
   const int m0 = tm * MT, n0 = tn * NT_;
-  const int kc = K / S, k0 = s * kc, nt = kc / 64;
+  const int kc = K / S, k0 = s * kc, nt = kc / BKE;
   PENNY_DASSERT(N % NT_ == 0 && K % (64 * S) == 0 && nt >= 1 && s < S);
 
-  // ---- LDS-DMA sources: wave w owns pieces 4w .. 4w+3 of the W image and of the X image ----
-  // piece p = image rows 8p .. 8p+7; lane l -> row 8p + (l >> 3), LDS slot (l & 7) = logical chunk
-  // (l & 7) ^ swz(row) of the row's 128-B K-tile slice
-  const char* src[8];
+  // ---- LDS-DMA sources: wave w owns pieces w*PPW .. of the W image and of the X image ----
+  // piece p = image rows RPP*p ..; lane l -> row RPP*p + l / CPR, LDS slot l % CPR = logical chunk
+  // (l % CPR) ^ mswz(row) of the row's RB-byte K slice
+  const char* src[2 * PPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 32 * w + 8 * i + (lane >> 3);
-    const int c = (lane & 7) ^ swz(r);
+  for (int i = 0; i < PPW; ++i) {
+    const int r = RPP * (w * PPW + i) + lane / CPR;
+    const int c = (lane % CPR) ^ mswz<RB>(r);
     src[i] = reinterpret_cast<const char*>(W + (long)(n0 + r) * K + k0) + 16 * c;
     const int m = min(m0 + r, M - 1);
-    src[4 + i] = reinterpret_cast<const char*>(X + (long)m * ldx + k0) + 16 * c;
+    src[PPW + i] = reinterpret_cast<const char*>(X + (long)m * ldx + k0) + 16 * c;
   }
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   // inline-asm DMA: invisible to hipcc's waitcnt pass, so the fragment ds_reads of the current
-  // buffer are not held behind a vmcnt(0) for the next buffer's DMA (the counted wait below is the
-  // only one); M0 is set and restored inside the statement
-  auto stage = [&](int t, unsigned buf) {
+  // stage are not held behind a vmcnt(0) for the next stages' DMA (the explicit waits are the only
+  // ones); M0 is set and restored inside the statement
+  auto stage = [&](int t) {
+    const unsigned buf = lds0 + (t % NST) * STG;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const unsigned dst = buf + (i < 4 ? 0 : IMG) + (32 * w + 8 * (i & 3)) * 128;
-      const char* gp = src[i] + (long)t * 128;
+    for (int i = 0; i < 2 * PPW; ++i) {
+      const unsigned dst = buf + (i < PPW ? 0 : OPB) + RPP * (w * PPW + (i % PPW)) * RB;
+      const char* gp = src[i] + (long)t * RB;
       unsigned keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep)
@@ -107,8 +127,10 @@ __global__ void __launch_bounds__(256, 2) gemm_mid_kernel(const bf16* __restrict
   };
 
   // fragment chunk offsets of this lane's row (lane & 15): k-step kk reads logical chunk 4kk + g
-  const int rowoff = col * 128;
-  const int choff0 = ((g) ^ swz(col)) << 4, choff1 = ((4 + g) ^ swz(col)) << 4;
+  const int rowoff = col * RB;
+  int choff[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) choff[kk] = ((4 * kk + g) ^ mswz<RB>(col)) << 4;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -116,36 +138,32 @@ __global__ void __launch_bounds__(256, 2) gemm_mid_kernel(const bf16* __restrict
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, lds0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nt) stage(t);
   for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) stage(t + 1, lds0 + (cur ^ 1) * STAGE);
-    const char* wi = smem + cur * STAGE + (wa * 64) * 128 + rowoff;
-    const char* xi = smem + cur * STAGE + IMG + (wb * 64) * 128 + rowoff;
-    Frag a[4][2], b[4][2];
+    // this wave's pieces of stage t landed (younger stages may stay in flight), then publish it; the
+    // barrier also retires every wave's reads of the buffer restaged next (read at t - 1)
+    if (NST >= 3 && t + NST - 2 < nt) mid_wait_barrier<(NST >= 3 ? (NST - 2) * LPS : 0)>();
+    else mid_wait_barrier<0>();
+    if (t + NST - 1 < nt) stage(t + NST - 1);
+    const char* wi = smem + (t % NST) * STG + (wa * 64) * RB + rowoff;
+    const char* xi = smem + (t % NST) * STG + OPB + (wb * 64) * RB + rowoff;
+    Frag a[4][KS], b[4][KS];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      a[f][0].u = *reinterpret_cast<const uint4*>(wi + f * 16 * 128 + choff0);
-      a[f][1].u = *reinterpret_cast<const uint4*>(wi + f * 16 * 128 + choff1);
-    }
+    for (int f = 0; f < 4; ++f)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      b[u][0].u = *reinterpret_cast<const uint4*>(xi + u * 16 * 128 + choff0);
-      b[u][1].u = *reinterpret_cast<const uint4*>(xi + u * 16 * 128 + choff1);
-    }
+      for (int kk = 0; kk < KS; ++kk) {
+        a[f][kk].u = *reinterpret_cast<const uint4*>(wi + f * 16 * RB + choff[kk]);
+        b[f][kk].u = *reinterpret_cast<const uint4*>(xi + f * 16 * RB + choff[kk]);
+      }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[f][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk].v, b[u][kk].v, acc[f][u], 0, 0, 0);
-    // the next K-tile landed (this wave's pieces), and every wave is done reading this buffer
-    // before anyone restages it (next iteration's DMA targets the other buffer; the one after, this)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // ---- epilogue: lane holds Y[m0 + wb*64 + 16u + col][n0 + wa*64 + 16f + 4g + r], r = 0..3 ----
@@ -195,6 +213,23 @@ __global__ void __launch_bounds__(256, 2) gemm_mid_kernel(const bf16* __restrict
 
 }  // namespace
 
+// Staging variant (PENNY_MID_VARIANT, or penny_gemm_mid_variant for in-process A/B): 0 = BK 64, 2-stage
+// ring (64 KiB, 2 workgroups per CU), 1 = BK 64, 3-stage counted ring (96 KiB, 1 per CU), 2 = BK 32,
+// 3-stage counted ring (48 KiB, 3 per CU)
+static int g_mid_variant = -1;
+static int mid_variant() {
+  if (g_mid_variant < 0) {
+    const char* v = getenv("PENNY_MID_VARIANT");
+    g_mid_variant = v ? atoi(v) : 0;
+  }
+  return g_mid_variant;
+}
+PENNY_API int penny_gemm_mid_variant(int v) {
+  const int old = mid_variant();
+  if (v >= 0 && v <= 2) g_mid_variant = v;
+  return old;
+}
+
 // Contract (checked): N % 128 == 0, K % (64 * S) == 0, ldx % 8 == 0, 16-B aligned rows; epi 0 bf16
 // [M, N] (row stride ldy), 1 SiLU(gate)*up of the interleave16 gate|up weight -> bf16 [M, N/2], 2 f32
 // split-K slabs P [S, M, N] (ldy unused), 3 bf16 + R (row stride ldr); epilogues other than 2 need S = 1.
@@ -207,9 +242,18 @@ PENNY_API int penny_gemm_mid(const void* X, int ldx, const void* W, int K, void*
   const long nwg = (long)((M + MT - 1) / MT) * (N / NT_) * S;
   if (nwg > 0x7fffffff) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)nwg);
-#define MID_LAUNCH(E)                                                                                      \
-  hipLaunchKernelGGL(gemm_mid_kernel<E>, grid, dim3(256), 0, stream, (const bf16*)X, ldx, (const bf16*)W, K, Y, \
-                     ldy, (const bf16*)R, ldr, M, N, S)
+  const int var = mid_variant();
+  if (var == 2 && (K / S) % 32) return (int)hipErrorInvalidValue;
+#define MID_LAUNCH(E)                                                                                                \
+  if (var == 1)                                                                                                      \
+    hipLaunchKernelGGL((gemm_mid_kernel<E, 128, 3>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, (const bf16*)W, \
+                       K, Y, ldy, (const bf16*)R, ldr, M, N, S);                                                      \
+  else if (var == 2)                                                                                                 \
+    hipLaunchKernelGGL((gemm_mid_kernel<E, 64, 3>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, (const bf16*)W,  \
+                       K, Y, ldy, (const bf16*)R, ldr, M, N, S);                                                      \
+  else                                                                                                               \
+    hipLaunchKernelGGL((gemm_mid_kernel<E, 128, 2>), grid, dim3(256), 0, stream, (const bf16*)X, ldx, (const bf16*)W, \
+                       K, Y, ldy, (const bf16*)R, ldr, M, N, S)
   switch (epi) {
     case MEPI_BF16: MID_LAUNCH(MEPI_BF16); break;
     case MEPI_SILU: MID_LAUNCH(MEPI_SILU); break;

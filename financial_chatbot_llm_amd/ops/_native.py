@@ -44,6 +44,7 @@ _SIGS = {
                               P, c_long, P, c_int, c_int, P],
     "penny_gemm_prefill_qkv_rope": [P, c_int, P, c_int, c_int, P, P, P, P, P, P, c_int, c_int,
                                     c_float, P, c_long, P, c_int, c_int, P],
+    "penny_gemm_mid_variant": [c_int],
     "penny_gemm_mid": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, P],
     "penny_gemm_prefill_ablate": [P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P],
     "penny_moe_gemm_prefill_fp8": [P, c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],

@@ -587,6 +587,13 @@ def prefill_choice(M: int, N_: int, K: int, epilogue: Optional[str] = None, slab
 MID_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3}
 
 
+def mid_variant(v: int = -1) -> int:
+    """Select the mid kernel's staging variant (gemm_mid.hip: 0 = BK 64 x 2 stages, 1 = BK 64 x 3
+    counted stages, 2 = BK 32 x 3 counted stages) and return the previous one; -1 only reads it.
+    ``PENNY_MID_VARIANT`` sets the initial value.  In-process A/B runs and tests."""
+    return int(N.load().penny_gemm_mid_variant(int(v)))
+
+
 def mid_gemm(x: torch.Tensor, w: torch.Tensor, epilogue: Optional[str] = None, S: int = 1,
              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ w.T on the 128 x 128 tile kernel: bf16 [M, N]; "silu" -> silu(gate)*up bf16 [M, N/2] of the

@@ -130,7 +130,7 @@ def test_prefill_attention(Hq, Hkv, D, causal, lens, qscale):
     close(out, ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
     # respond chunk behind a cached prefix + decide-like and spec-like chunks (dead waves: 17 x 4 rows)
     (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
@@ -169,7 +169,7 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
         ops.attention.prefill_variant(old)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7])
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
     (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
@@ -206,7 +206,7 @@ def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal,
     close(lse, lse_ref, atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7])
 @pytest.mark.parametrize("spike_block", [0, 3, 9])
 def test_prefill_attention_late_max_spike_forces_rescale(variant, spike_block):
     """Rule 26: a rare rescale branch needs an input that FORCES it.  One query token's row is made to
@@ -928,12 +928,13 @@ def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
     assert torch.equal(kc2, kc[1]) and torch.equal(vc2, vc[1])
 
 
+@pytest.mark.parametrize("variant", [5, 7])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens,qscale", [
     (32, 8, 128, True, [(300, 1100), (17, 900), (70, 70), (130, 700)], 1.0),
     (32, 8, 128, True, [(257, 257), (64, 3000)], 12.0),      # peaky rows
     (8, 1, 128, True, [(40, 40), (33, 500)], 1.0),
 ])
-def test_prefill_attention_prescaled_q(Hq, Hkv, D, causal, lens, qscale):
+def test_prefill_attention_prescaled_q(variant, Hq, Hkv, D, causal, lens, qscale):
     """q handed over prescaled by scale * log2(e) at its ONE bf16 rounding (what the fused QKV epilogue
     does with qscale) on the prescaled-Q fold, with scale 1 / log2(e): as close to the fp32 reference
     as the exact-Q variant 5 fed bf16(q) -- the in-kernel prescale's second rounding (variant 6) is
@@ -951,18 +952,26 @@ def test_prefill_attention_prescaled_q(Hq, Hkv, D, causal, lens, qscale):
     q5 = qf.to(torch.bfloat16)
     qp = (qf * c).to(torch.bfloat16)
     args = (cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV))
-    out5 = ops.prefill(q5.to(DEV), *args, scale, causal, max_q_len=max(qlens))
-    outp = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens), q_prescaled=True)
+    old = ops.attention.prefill_variant(5)
+    try:
+        out5 = ops.prefill(q5.to(DEV), *args, scale, causal, max_q_len=max(qlens))
+        ops.attention.prefill_variant(variant)        # 7: the 32x32x16 kernel's prescaled-Q form
+        outp = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens), q_prescaled=True)
+        wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, causal, cus=100000,
+                                             min_chunk=1)
+        outl = None
+        if wl is not None:
+            outl = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens),
+                               work=torch.from_numpy(wl).to(DEV), lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])),
+                               q_prescaled=True)
+    finally:
+        ops.attention.prefill_variant(old)
     e5 = (out5.float().cpu() - ref.float()).abs().max().item()
     ep = (outp.float().cpu() - ref.float()).abs().max().item()
     # on the peaky rows (qscale 12) the ONE rounding of q itself already costs variant 5 ~0.1 against
     # the f32-q reference; the prescaled form stays within 1.5x of that, and within 0.02 on typical rows
     assert ep <= 1.5 * e5 + 2e-3 and (qscale > 1 or ep <= 2e-2), (ep, e5)
-    wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, causal, cus=100000, min_chunk=1)
-    if wl is not None:
-        outl = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, causal, max_q_len=max(qlens),
-                           work=torch.from_numpy(wl).to(DEV), lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])),
-                           q_prescaled=True)
+    if outl is not None:
         assert (outl.float().cpu() - ref.float()).abs().max().item() <= 1.5 * e5 + 2e-2
 
 
@@ -1553,15 +1562,24 @@ def test_rope_qk_matches_reference(D):
 
 
 # ---- 128 x 128 tile kernel (gemm_mid.hip): the Llama-3-70B TP=8 shard shapes ----
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("name,M,S", [("qkv", 384, 4), ("qkv", 1000, 1), ("o", 300, 1), ("o", 1536, 2),
                                        ("gate_up", 513, 1), ("gate_up", 384, 2), ("down", 257, 1), ("down", 768, 2)])
-def test_mid_gemm_tp8_shard_shapes_vs_fp32(name, M, S):
+def test_mid_gemm_tp8_shard_shapes_vs_fp32(variant, name, M, S):
     """Every epilogue form of the mid tile kernel at the 70B TP=8 shards against fp32 on the GPU:
     QKV (1280 x 8192) slabs for the RoPE pass, O (8192 x 1024) and down (8192 x 3584) bf16 for the
     all-reduce (S > 1: slabs + penny_splitk_reduce), gate|up (7168 x 8192 interleave16) + SiLU (S > 1:
     slabs + reduce-SiLU); M not a multiple of the 128-row tile included."""
     from financial_chatbot_llm_amd.ops import gemm
     N_, K = {"qkv": (1280, 8192), "o": (8192, 1024), "gate_up": (7168, 8192), "down": (8192, 3584)}[name]
+    old = gemm.mid_variant(variant)
+    try:
+        _mid_case(gemm, name, M, S, N_, K)
+    finally:
+        gemm.mid_variant(old)
+
+
+def _mid_case(gemm, name, M, S, N_, K):
     g = torch.Generator(device=DEV).manual_seed(M * 7 + S)
     x = torch.randn((M, K), generator=g, device=DEV).to(torch.bfloat16)
     w = (torch.randn((N_, K), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
