@@ -81,6 +81,11 @@ def parse(argv=None):
                          "PENNY_STEP_GPU_TIMING=1), ~60 ms higher p50 TTFT from the IPC hop")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: contract tests of the bench itself with tiny models (gloo for >1 rank)")
+    ap.add_argument("--tp-shard-estimate", type=int, default=0, metavar="N",
+                    help="estimate a TP=N replica on ONE GPU (VERDICT r5 item 6): the engine runs rank 0's shard "
+                         "(1/N of heads, FFN, vocab) with its collectives stubbed to identity, and the JSON adds "
+                         "the step's all-reduce volume priced at stated xGMI rates -- a projection, never a "
+                         "multi-GPU measurement")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -112,6 +117,7 @@ async def run(args, ps):
     ecfg = EngineConfig(model=args.model, max_num_seqs=max(sizes), max_num_batched_tokens=args.max_batched_tokens,
                         max_model_len=args.max_model_len, use_cuda_graph=not args.no_graph,
                         graph_batch_sizes=sizes, seed=0, device=args.device, dtype=args.dtype, tp_size=args.tp,
+                        shard_of_tp=args.tp_shard_estimate,
                         # PENNY_KV_FRACTION: several ranks sharing one GPU (gloo rehearsal of dpN) split its HBM
                         kv_mem_fraction=float(os.environ.get("PENNY_KV_FRACTION", EngineConfig.kv_mem_fraction)),
                         sched_aging_s=float(os.environ.get("PENNY_SCHED_AGING_S", EngineConfig.sched_aging_s)),
@@ -256,8 +262,11 @@ async def run(args, ps):
                                               - stats0.get("gpu_idle_between_steps_s", 0.0), 3),
             "max_rss_gib": round(ru1.ru_maxrss / 2**20, 2),      # host memory high-water mark (ru_maxrss is KiB)
             "custom_all_reduce": dict(comm.AR_STATUS) if args.tp > 1 else None}
+    steps_timed = {k: stats.get(k, 0) - stats0.get(k, 0) for k in ("steps", "graph_steps", "tokens")}
     return {"elapsed": elapsed, "turns": sum(r.turns for r in results), "errors": sum(r.errors for r in results),
-            "host": host,
+            "host": host, "steps_timed": steps_timed,
+            "prefill_timed": {k: stats.get("prefill_" + k2, 0) - stats0.get("prefill_" + k2, 0)
+                              for k, k2 in (("steps", "steps"), ("tokens", "step_tokens"))},
             "ttfts": [t for r in results for t in r.ttfts], "retrievals": sum(r.retrievals for r in results),
             "stages": stages, "engine": stats, "tokens": tokens, "latency": latency,
             "plots_ok": sum(r.plots_ok for r in results), "plots_failed": sum(r.plots_failed for r in results)}
@@ -305,6 +314,45 @@ def _launch_ranks(args, argv) -> int:
     env = dict(os.environ, PENNY_BENCH_SPAWNED="1")
     log(f"launching {args.gpus} ranks: {' '.join(cmd[1:])}")
     return subprocess.run(cmd, env=env).returncode
+
+
+# xGMI pricing of the stubbed collectives (tp_shard_projection): stated assumptions, not measurements
+XGMI_LINK_GBPS = 153.0          # one xGMI link, per direction (MI355X: 7 links per GPU)
+ONESHOT_LAT_US = 5.0            # custom one-shot all-reduce: flag round trip + in-graph launch boundary
+RCCL_LAT_US = 15.0              # RCCL ring all-reduce launch + latency (prefill-size messages)
+RCCL_BUSBW_GBPS = (300.0, 150.0)   # RCCL all-reduce bus bandwidth on 8 xGMI-meshed GPUs: optimistic, pessimistic
+
+
+def tp_shard_projection(args, res, tmax: float, turns: int) -> dict:
+    """Per-rank TP=N step estimate: the measured compute-only run of rank 0's shard plus the
+    all-reduce time its collectives would take -- 1 (vocab-parallel embedding) + 2 per layer (O and
+    down) of [T, hidden] bf16 per step: decode steps on the custom one-shot kernel (each rank reads
+    its 7 peers' buffers over 7 links at once: bytes / link rate), prefill steps on RCCL's ring
+    (2 (n-1)/n x bytes / bus bandwidth).  No overlap of the collectives with compute is assumed
+    (the prefill micro-batch pipeline would hide part of it), so this bounds the TP=N group's rate
+    from below for the given link rates."""
+    from financial_chatbot_llm_amd.models.configs import get_model_config
+    mc = get_model_config(args.model)
+    n = args.tp_shard_estimate
+    ars = 1 + 2 * mc.num_layers
+    row_bytes = mc.hidden_size * 2
+    st, pf = res["steps_timed"], res["prefill_timed"]
+    dec_steps = max(st["steps"] - pf["steps"], 0)
+    dec_tokens = max(st["tokens"] - pf["tokens"], 0)
+    dec_s = ars * (dec_steps * ONESHOT_LAT_US * 1e-6 + dec_tokens * row_bytes / (XGMI_LINK_GBPS * 1e9))
+    out = {"tp": n, "all_reduces_per_step": ars, "decode_steps": dec_steps, "decode_tokens": dec_tokens,
+           "prefill_steps": pf["steps"], "prefill_tokens": pf["tokens"],
+           "all_reduce_bytes": ars * st["tokens"] * row_bytes, "decode_comm_s": round(dec_s, 3),
+           "compute_only_s": round(tmax, 3), "compute_only_turns_per_s": round(turns / tmax, 3),
+           "assumptions": {"xgmi_link_GBps": XGMI_LINK_GBPS, "oneshot_latency_us": ONESHOT_LAT_US,
+                           "rccl_latency_us": RCCL_LAT_US, "rccl_busbw_GBps": list(RCCL_BUSBW_GBPS),
+                           "overlap": "none"}}
+    for tag, bw in zip(("optimistic", "pessimistic"), RCCL_BUSBW_GBPS):
+        pre_s = ars * (pf["steps"] * RCCL_LAT_US * 1e-6 + 2 * (n - 1) / n * pf["tokens"] * row_bytes / (bw * 1e9))
+        total = tmax + dec_s + pre_s
+        out[tag] = {"prefill_comm_s": round(pre_s, 3), "projected_s": round(total, 3),
+                    "projected_turns_per_s_per_group": round(turns / total, 3)}
+    return out
 
 
 def main(argv=None) -> int:
@@ -391,6 +439,9 @@ def main(argv=None) -> int:
                                   "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process"),
                      "ranks": hosts},
         }
+        if args.tp_shard_estimate > 1:
+            out["tp_shard_estimate"] = tp_shard_projection(args, allr[0], tmax, turns)
+            out["config"]["parallelism"] = f"tp{args.tp_shard_estimate} rank-0 shard on 1 GPU, collectives stubbed"
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

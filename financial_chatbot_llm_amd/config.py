@@ -114,6 +114,9 @@ class EngineConfig:
     weights: Optional[str] = None           # safetensors dir; None -> random init
     tokenizer: Optional[str] = None         # tokenizer.json; None -> built-in synthetic vocab
     tp_size: int = 1
+    # estimate mode (bench.py --tp-shard-estimate N): build only the rank-0 shard of a TP=N group on
+    # this one device, its collectives identity -- the per-rank compute of a TP step, measured
+    shard_of_tp: int = 0
     # context parallelism (SURVEY §5.7 stretch): cp_size ranks, each with the full weights, form one
     # replica; its leader serves, and a prompt with >= cp_min_tokens uncomputed tokens is prefilled
     # by all of them at once (zig-zag shards, ring attention over xGMI), its K/V gathered into the

@@ -639,6 +639,7 @@ class LLMEngine:
                 "tokens": self.runner.stats["tokens"], **{k: round(v, 3) for k, v in self.timing.items()},
                 "gemm_tuning": float(bool(getattr(self, "gemm_tuning", None))),
                 "prefill_steps": self.runner.stats["prefill_steps"],
+                "prefill_step_tokens": self.runner.stats["prefill_step_tokens"],
                 **(self.cp.stats if self.cp is not None else {}),
                 "prefill_step_tokens_mean": round(self.runner.stats["prefill_step_tokens"]
                                                   / max(1, self.runner.stats["prefill_steps"]), 1),

@@ -14,7 +14,10 @@ def build_model(engine_cfg, device, seed: int = 0):
         model = MixtralModel(cfg, device=device, fp8=getattr(engine_cfg, "dtype", "bf16") == "fp8",
                              moe_parallel=getattr(engine_cfg, "moe_parallel", "tp"))
     elif cfg.arch == "llama":
-        model = LlamaModel(cfg, device=device)
+        shard = int(getattr(engine_cfg, "shard_of_tp", 0) or 0)
+        # estimate mode: rank 0's shard of a TP=shard group, alone on this device (collectives are
+        # identity while the process group is TP=1)
+        model = LlamaModel(cfg, device=device, tp_rank=0, tp_size=shard) if shard > 1 else LlamaModel(cfg, device=device)
     else:
         raise ValueError(f"{cfg.name} is not a decoder")
     model.sequence_parallel = bool(getattr(engine_cfg, "sequence_parallel", False))

@@ -51,7 +51,7 @@ for spec in "$@"; do
               > "gpurun_out/${TAG}_prof_kernel_stats.md" 2>&1
           rm -rf /tmp/prof_$TAG ;;
     kbench) run "kbench_${rest//[^a-zA-Z0-9]/_}" 600 python -u -m financial_chatbot_llm_amd.bench.kernels --only "$rest" \
-              --out "gpurun_out/${TAG}_kbench.jsonl" || exit $? ;;
+              --out "gpurun_out/${TAG}_kbench_${rest//[^a-zA-Z0-9]/_}.jsonl" || exit $? ;;
     pmc) only=${rest%%:*}; ctrs=${rest#*:}; ctrs=${ctrs//+/ }
          rm -rf /tmp/pmc_$TAG
          run "pmc_${only//[^a-zA-Z0-9]/_}" 240 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d /tmp/pmc_$TAG \

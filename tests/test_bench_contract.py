@@ -162,3 +162,19 @@ def test_bench_tensor_parallel_replica_on_one_gpu_json_contract():
     assert len(lines) == 1
     d = lines[0]
     assert d["config"]["parallelism"] == "dp1tp2" and d["turn_errors"] == 0 and d["value"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_tp_shard_estimate_mode():
+    """``--tp-shard-estimate N``: one process runs rank 0's TP=N shard with its
+    collectives stubbed and projects the all-reduce time at stated xGMI rates."""
+    r = subprocess.run([sys.executable, "bench.py", *ARGS, "--tp-shard-estimate", "2"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=280, env=_clean_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_lines(r.stdout)[0]
+    e = d["tp_shard_estimate"]
+    assert e["tp"] == 2 and e["all_reduces_per_step"] == 1 + 2 * 2          # llama-tiny: 2 layers
+    assert e["prefill_tokens"] > 0 and e["all_reduce_bytes"] > 0
+    for k in ("optimistic", "pessimistic"):
+        assert e[k]["projected_s"] >= e["compute_only_s"]
+    assert "stubbed" in d["config"]["parallelism"]
