@@ -63,6 +63,11 @@ __device__ __forceinline__ float vmax_raw(float a, float b) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ __forceinline__ float vmax3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ float rowgroup_max_raw(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = vmax_raw(__uint_as_float(a[0]), __uint_as_float(a[1]));
@@ -1218,11 +1223,18 @@ __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, cons
         sc[T][r] = ok ? sc[T][r] : -INFINITY;
       }
   }
-  float mt = sc[0][0];
+  // a max3 tree over the lane's 32 scores (depth 4, 16 instructions): a serial v_max chain is 32
+  // dependent instructions on the wave's critical path between its QK^T and P.V MFMAs
+  float m3[11];
 #pragma unroll
-  for (int r = 1; r < 16; ++r) mt = vmax_raw(mt, sc[0][r]);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) mt = vmax_raw(mt, sc[1][r]);
+  for (int i = 0; i < 10; ++i) {
+    const int a = 3 * i, b = a + 1, c = a + 2;
+    m3[i] = vmax3_raw(sc[a >> 4][a & 15], sc[b >> 4][b & 15], sc[c >> 4][c & 15]);
+  }
+  m3[10] = vmax_raw(sc[1][14], sc[1][15]);
+  const float mt4[4] = {vmax3_raw(m3[0], m3[1], m3[2]), vmax3_raw(m3[3], m3[4], m3[5]),
+                        vmax3_raw(m3[6], m3[7], m3[8]), vmax_raw(m3[9], m3[10])};
+  float mt = vmax_raw(vmax_raw(mt4[0], mt4[1]), vmax_raw(mt4[2], mt4[3]));
   mt = lanepair_max(mt);                      // QPRE: max of s*c - m; else max of s
   if constexpr (!QPRE) mt = fresh ? mt * scale_log2 : mt * scale_log2 - m;
   const bool grow = mt > (fresh ? -INFINITY : 8.f);
@@ -1242,26 +1254,27 @@ __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, cons
         for (int r = 0; r < 16; ++r) sc[T][r] -= rise;
     }
   }
-  float ls = 0.f;
   if constexpr (QPRE) {
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sc[T][r] = fast_exp2(sc[T][r]);
-        ls += sc[T][r];
-      }
+      for (int r = 0; r < 16; ++r) sc[T][r] = fast_exp2(sc[T][r]);
   } else {
     const float mref = m == -INFINITY ? 0.f : m;
 #pragma unroll
     for (int T = 0; T < 2; ++T)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sc[T][r] = fast_exp2(fmaf(sc[T][r], scale_log2, -mref));
-        ls += sc[T][r];
-      }
+      for (int r = 0; r < 16; ++r) sc[T][r] = fast_exp2(fmaf(sc[T][r], scale_log2, -mref));
   }
-  l += ls;
+  // row-sum partial as a pairwise tree (hipcc keeps a written f32 add chain serial: 32 dependent adds)
+  float s16[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s16[r] = sc[0][r] + sc[1][r];
+#pragma unroll
+  for (int w2 = 8; w2 >= 1; w2 >>= 1)
+#pragma unroll
+    for (int r = 0; r < w2; ++r) s16[r] = s16[r] + s16[r + w2];
+  l += s16[0];
   Frag pf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st)

@@ -100,6 +100,10 @@ class LLMEngine:
             except Exception as e:  # noqa: BLE001 - no IPC on this host: RCCL carries everything
                 logger.warning(f"custom all-reduce unavailable ({e}); using RCCL for every TP all-reduce")
                 comm.AR_STATUS.update(custom=False, self_test=f"unavailable: {e}")
+            # every rank must hold the same custom instances before the self-test's collectives (an
+            # enable that raised on some ranks only would send the group down different collective
+            # sequences): agree on presence bits first, all ranks, raised or not
+            comm.agree_custom_all_reduce(want_second=bool(getattr(cfg, "tp_dual_decode", False)))
             # first contact: the custom kernels must reproduce the exact sum on THIS node before any
             # token depends on them; any rank's failure sends every rank to RCCL
             if comm.custom_all_reduce() is not None and getattr(cfg, "custom_ar_self_test", True):

@@ -199,8 +199,9 @@ def build_step_inputs(batch: ScheduledBatch) -> StepInputs:
     cat = lambda parts, tail: np.concatenate(parts + [i32(tail)]) if parts else i32(tail)  # noqa: E731
     src_a = i32(src) if any(x >= 0 for x in src) else None
     bt_d = _table(tables_d)
-    if _attn.LEAN_FLAGS & 1 and _attn.DECODE_LEAN:
-        mark_shared_blocks(bt_d, ctx_d)          # the lean kernel's cache policy per block
+    if _attn.LEAN_FLAGS & 1 and _attn.DECODE_LEAN and len(ctx_d) >= _attn.LEAN_NT_MIN_B:
+        # the lean kernel's cache policy per block -- only where ops.decode keeps the NT bit
+        mark_shared_blocks(bt_d, ctx_d)
     return StepInputs(cat(ids_parts, ids_d), cat(pos_parts, pos_d), cat(slot_parts, slots_d), i32(cu), i32(ctx_p),
                       _table(tables_p), max_q, i32(ctx_d), bt_d, np.asarray(logits_idx, np.int64),
                       np.asarray(temps, np.float32), np.asarray(seeds, np.int64), i32(tk), np.asarray(tp, np.float32),
@@ -275,6 +276,7 @@ class ModelRunner:
         self.decode_ws2 = None
         self.graphs: Dict[int, _DecodeGraph] = {}
         self.graphs_filt: Dict[int, _DecodeGraph] = {}   # top-k / top-p twins of fused buckets (lazy)
+        self._filt_failed: set = set()                    # buckets whose filtered twin could not be captured
         self._static = None
         self.graph_pool = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
@@ -295,6 +297,8 @@ class ModelRunner:
         self._pinned_out = ([torch.zeros(self.max_samplers + 1, dtype=torch.int32).pin_memory() for _ in range(2)]
                             if self.on_gpu else None)
         self._out_flip = 0
+        self._ev_ring: Optional[List[Tuple[torch.cuda.Event, torch.cuda.Event]]] = None
+        self._ev_i = 0
         # eager-step inputs: one pinned staging ring slot -> ONE H2D copy per step (see _stage_inputs)
         self._staged: Optional[Dict[int, torch.Tensor]] = None
         self._stage_ring: List[Optional[torch.Tensor]] = [None] * 4
@@ -491,10 +495,20 @@ class ModelRunner:
             finally:
                 self._staged = None
             return PendingStep(None, 0, None, None)
-        start_ev = None
-        if self._gpu_timing:
-            start_ev = torch.cuda.Event(enable_timing=True)
-            start_ev.record()
+        start_ev = end_ev = None
+        if self.on_gpu:
+            # a small ring of reused events (creating two timing events per step cost ~30 us of
+            # host time between launches); 4 pairs cover the step in flight, the one being collected and
+            # the previous step's end event the idle-gap measurement still reads
+            if self._ev_ring is None:
+                self._ev_ring = [(torch.cuda.Event(enable_timing=self._gpu_timing),
+                                  torch.cuda.Event(enable_timing=self._gpu_timing)) for _ in range(4)]
+            start_ev, end_ev = self._ev_ring[self._ev_i]
+            self._ev_i = (self._ev_i + 1) % len(self._ev_ring)
+            if self._gpu_timing:
+                start_ev.record()
+            else:
+                start_ev = None
         graph = False
         if (self.use_graphs and si.num_prefill_tokens == 0 and 0 < si.num_decode <= self.max_decode_batch
                 and not self._fused_graph_needs_eager(si)):
@@ -526,7 +540,7 @@ class ModelRunner:
             # the xGMI all-reduce never raises from the device: a peer that missed its bounded wait
             # sets ar.err and the step's sums are stale, so the flag rides the per-step host sync
             host[n:n + 1].copy_(ar.err, non_blocking=True)
-        ev = torch.cuda.Event(enable_timing=start_ev is not None)
+        ev = end_ev
         ev.record()
         return PendingStep(None, n, host, ev, start_ev, self.stats, "gpu_graph_s" if graph else "gpu_eager_s",
                            check_err=ar is not None)
@@ -660,8 +674,17 @@ class ModelRunner:
             return False
         if getattr(self.model, "tp_size", 1) > 1:
             return True
+        if B in self._filt_failed:
+            return True
         if B not in self.graphs_filt:
-            self._capture_filtered(B)
+            try:
+                self._capture_filtered(B)
+            except Exception as e:  # noqa: BLE001 - e.g. out of memory after the KV pool took HBM
+                # (ADVICE r5): this bucket's filtered rows stay on the eager path for good
+                logger.warning(f"filtered decode graph for batch {B} not captured ({e}); running it eagerly")
+                self._filt_failed.add(B)
+                torch.cuda.synchronize(self.device)
+                return True
         return False
 
     def _capture_filtered(self, B: int) -> None:
@@ -672,16 +695,18 @@ class ModelRunner:
         saved = (s["slots"][:B].clone(), s["src"][:B].clone())
         s["slots"][:B].fill_(-1)
         s["src"][:B].fill_(-1)
-        for _ in range(2):
-            self._run_static(B, filtered=True)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.graph_pool):
-            out = self._run_static(B, filtered=True)
-        self.graphs_filt[B] = _DecodeGraph(g, B, out, False)
-        s["slots"][:B].copy_(saved[0])
-        s["src"][:B].copy_(saved[1])
-        torch.cuda.synchronize()
+        try:
+            for _ in range(2):
+                self._run_static(B, filtered=True)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                out = self._run_static(B, filtered=True)
+            self.graphs_filt[B] = _DecodeGraph(g, B, out, False)
+        finally:                                  # the step in flight keeps its inputs either way
+            s["slots"][:B].copy_(saved[0])
+            s["src"][:B].copy_(saved[1])
+            torch.cuda.synchronize()
 
     def _bucket(self, n: int) -> int:
         for b in self.graph_sizes:

@@ -33,7 +33,10 @@ from collections import deque
 from dataclasses import dataclass, field
 from typing import Deque, Dict, List, Tuple
 
+from ..utils.logging import get_logger
 from .sequence import Sequence, SeqStatus
+
+logger = get_logger(__name__)
 
 
 @dataclass
@@ -120,6 +123,9 @@ class Scheduler:
         # share class 1 with the short ones and, sorted by arrival, could spend the reserved tokens
         #  -- so a reserve turns short_first on.
         self.short_first = short_first or short_reserve_tokens > 0
+        if short_reserve_tokens > 0 and not short_first:
+            logger.warning(f"short_reserve_tokens={short_reserve_tokens} turns sched_short_first on (the reserve "
+                           "needs short-output prompts in their own admission class)")
         # TTFT-tail anatomy: steps that ended with a short-output prompt still waiting, by what
         # stopped admission ("budget" / "grow" / "seqs" / "pending") and where those steps'
         # tokens went (decode rows, speculative chunks, continuing prefills, admitted prompts)

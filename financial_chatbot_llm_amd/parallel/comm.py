@@ -96,6 +96,31 @@ def _ar_instance():
 AR_STATUS = {"custom": False, "self_test": "not run"}
 
 
+def agree_custom_all_reduce(want_second: bool = False) -> bool:
+    """Presence consensus before the init self-test: one MIN all-reduce over the TP group of (instance 0
+    present, instance 1 present or not wanted).  If any rank lacks an instance the others hold, every
+    rank drops the custom path, so the group never issues different collective sequences.  Called by
+    every TP rank, including those whose enable raised.  Returns whether the custom path stays."""
+    s = state()
+    if s.tp_size == 1:
+        return _CUSTOM_AR is not None
+    dev = _CUSTOM_AR.device if _CUSTOM_AR is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+    if s.backend != "nccl":
+        dev = torch.device("cpu")
+    bits = torch.tensor([int(_CUSTOM_AR is not None), int(_CUSTOM_AR_2 is not None or not want_second)],
+                        dtype=torch.int32, device=dev)
+    dist.all_reduce(bits, op=dist.ReduceOp.MIN, group=s.tp_group)
+    ok = bool(int(bits[0])) and bool(int(bits[1]))
+    if not ok and (_CUSTOM_AR is not None or _CUSTOM_AR_2 is not None):
+        import logging
+        logging.getLogger(__name__).warning("custom all-reduce missing on a peer rank; RCCL carries every TP "
+                                            "collective")
+        disable_custom_all_reduce()
+        AR_STATUS.update(custom=False, self_test="a peer rank could not enable it")
+    return ok
+
+
 def verify_custom_all_reduce() -> bool:
     """Init-time first contact (every TP rank together): self-test each enabled custom instance
     against the exact sum (``custom_ar.self_test``: one-shot, two-shot, all-gather, bounded-wait
