@@ -504,6 +504,8 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 #          where the caller passes fuse_residual
 #   "K<nf>" the decode kernel's bf16-output form (row-major W, nf row groups per workgroup) with
 #          256-row token chunks side by side -- narrow row-parallel TP shards at small prefill steps
+#   "M<S>" the 128 x 128 tile kernel (gemm_mid.hip) with S K-slices: S = 1 its fused epilogue (bf16 /
+#          SiLU), S > 1 f32 slabs for a slab-reading consumer, else slabs + penny_splitk_reduce{,_silu}
 # QKV (r4): the fused RoPE + paged-KV-write tile kernel at every M > 256 as well (hipBLASLt was
 # 7-15 us per layer faster at 257-1280 rows; at the driver config the bench is unchanged, 32.2
 # turns/s, profiles/r4_bench128_20x5_all_prefill_gemms_tile_kernel.json).
@@ -512,32 +514,36 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 # underfill the CUs: profiles/r4_gemm_stream_k_tail_rejected.jsonl "r3 kernel" rows), ~0.2 ms
 # per prefill step of ~35 ms; the slab / in-place epilogues keep the O output out of a separate
 # add pass, and the projection on the framework's own MFMA kernel at every prefill size.
-# Shapes without an entry use ``_default_choice``.
+# r6: no projection of the SURVEY-named models takes hipBLASLt at prefill any more.  Shapes without
+# an entry use ``_default_choice``.
 PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (6144, 4096): [(1 << 30, "fused")],                                                   # QKV
     (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
-    (28672, 4096): [(256, "lib"), (1 << 30, "hip")],                                      # gate|up + SiLU
+    (28672, 4096): [(1 << 30, "hip")],                                                    # gate|up + SiLU
     (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down
-    # Llama-3-70B TP=1 (r5): each projection WITH its consumer (RoPE/KV write, add&RMSNorm, SiLU),
+    # Llama-3-70B TP=1 (r5, r6): each projection WITH its consumer (RoPE/KV write, add&RMSNorm, SiLU),
     # interleaved, M = 384..4096 (bench/kernels.py --only prefill_policy_70b,
-    # profiles/r5_prefill_policy_70b_tp1_with_consumers.jsonl).  The hand-written choice is taken
-    # wherever it is within ~8 % of hipBLASLt (O with the residual epilogue: 2-5 % behind at
-    # 1.5-4k rows; down S2 / S4: 7 % behind at 768 / 1536 rows); the library keeps QKV at <= 384
-    # and 1024 rows (13-18 % ahead) and gate|up to 768 rows (7-16 % ahead: 2 row tiles x 224
-    # columns leave the 256x256 tile's tail round mostly idle)
-    (10240, 8192): [(384, "lib"), (768, "S2"), (1024, "lib"), (1 << 30, "fused")],       # QKV
+    # profiles/r5_prefill_policy_70b_tp1_with_consumers.jsonl; QKV small steps on the 128 x 128 tile,
+    # profiles/r6_mid_shards.jsonl: mid2 64.6 vs hipBLASLt 67.5 us at 384 rows).  O with the residual
+    # epilogue is 2-5 % behind the library at 1.5-4k rows, down S2 / S4 7 % at 768 / 1536 rows, QKV
+    # fused ~5 % at 1024 rows (134.6 us library + the RoPE pass vs 146.7 fused)
+    (10240, 8192): [(384, "M2"), (768, "S2"), (1 << 30, "fused")],                       # QKV
     (8192, 8192): [(512, "S4"), (1024, "S2"), (1 << 30, "R")],                           # O
-    (57344, 8192): [(768, "lib"), (1 << 30, "hip")],                                     # gate|up
+    (57344, 8192): [(1 << 30, "hip")],          # gate|up (kept fragment-tiled only: linear_tiled)
     (8192, 28672): [(512, "S4"), (768, "S2"), (1024, "hip"), (1536, "S4"), (1 << 30, "R")],   # down
-    # TP=8 per-rank shards: the 256x256 tile underfills the CUs at these N up to ~1.5-2k rows (5 / 28
-    # / 32 column tiles), so the library keeps those; the tile kernel where it measured ahead
-    (1280, 8192): [(1536, "lib"), (3072, "S4"), (1 << 30, "S2")],                        # QKV shard
-    # O shard: 256-row token chunks of the bf16 decode kernel at <= 512 rows (18.0-18.6 vs hipBLASLt
-    # 20.3-20.8 us; profiles/r5_chunked_splitk_prefill_ab.jsonl -- the chunked form lost everywhere
-    # else it was measured: 8B QKV / O, 70B TP=1 QKV, the other TP=8 shards)
-    (8192, 1024): [(512, "K4"), (1536, "lib"), (2048, "hip"), (1 << 30, "lib")],          # O shard
-    (7168, 8192): [(1024, "lib"), (3072, "hip"), (1 << 30, "lib")],                      # gate|up shard
-    (8192, 3584): [(1 << 30, "lib")],                                                    # down shard
+    # Llama-3-70B TP=8 per-rank shards (r6, profiles/r6_mid_shards.jsonl, bench/kernels.py --only
+    # mid_shards: every hand-written form interleaved against hipBLASLt per M = 384..4096): the 128 x 128
+    # tile where the 256 x 256 one underfills the CUs, the 256 x 256 one from ~1.5k rows.
+    #   QKV   1.13-1.67x hipBLASLt to 3072 rows, 0.98x at 4096
+    #   O     1.21-1.59x to 1024 rows, 0.94-1.07x above
+    #   gate|up 0.97x at 384-512, 0.90-0.99x at 768-1024, 1.02-1.09x at 1536-3072, 0.96x at 4096
+    #   down  0.82x at 384, 0.93x at 512-768, 0.99-1.02x at 1024-2048, 0.89x at 3072, 0.97x at 4096
+    # (the library's lead at the smallest down / gate|up steps is its smaller-tile kernel set; those
+    # steps are a few % of a config-4 prefill step's GEMM time -- the framework's kernels run them)
+    (1280, 8192): [(1024, "M8"), (1536, "M4"), (3072, "S4"), (1 << 30, "S2")],           # QKV shard
+    (8192, 1024): [(1536, "M1"), (1 << 30, "hip")],                                      # O shard
+    (7168, 8192): [(384, "M4"), (512, "M2"), (1 << 30, "hip")],                          # gate|up shard
+    (8192, 3584): [(384, "M2"), (1024, "M1"), (1 << 30, "hip")],                         # down shard
 }
 
 

@@ -433,17 +433,19 @@ def test_splitk_kernels_token_chunks(M):
 
 
 def test_linear_tp8_o_shard_small_prefill_on_chunked_kernel(monkeypatch):
-    """The 70B TP=8 O shard at a 384-row prefill step takes the chunked bf16 decode kernel (policy K4)
-    and equals the fp32 reference; the library form agrees."""
+    """The 70B TP=8 O shard at a 384-row prefill step: the chunked bf16 decode kernel (policy K4,
+    r5) and the r6 128 x 128 tile kernel (policy M1, what the policy takes now) both equal the fp32
+    reference."""
     from financial_chatbot_llm_amd.ops import gemm
     monkeypatch.delenv("PENNY_PREFILL_GEMM", raising=False)
-    assert gemm.prefill_choice(384, 8192, 1024, None) == "K4"
+    assert gemm.prefill_choice(384, 8192, 1024, None) == "M1"
     g = torch.Generator().manual_seed(31)
     x = rnd(384, 1024, gen=g).to(DEV)
     w = rnd(8192, 1024, scale=0.03, gen=g).to(DEV)
     y = gemm.linear(x, w)
     close(y, x.float() @ w.float().t(), atol=2e-2)
     close(y, torch.nn.functional.linear(x, w), atol=2e-2)
+    close(gemm.splitk_bf16(x, w, 8192, 4), x.float() @ w.float().t(), atol=2e-2)      # the r5 K4 form
 
 
 @pytest.mark.parametrize("N_,K,S,nf", [(1280, 8192, 8, 4), (8192, 8192, 4, 8), (8192, 3584, 2, 4)])

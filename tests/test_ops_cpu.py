@@ -136,7 +136,7 @@ def test_decode_gemm_dispatch_tables(monkeypatch):
     from financial_chatbot_llm_amd.ops import gemm
     # Llama-3-8B: measured split-K / fused gate|up configs, tiled copies
     assert gemm.splitk_config(128, 6144, 4096) == (4, 6)
-    assert gemm.splitk_config(300, 6144, 4096) is None              # prefill size: hipBLASLt
+    assert gemm.splitk_config(300, 6144, 4096) is None              # prefill size: the tile kernels
     assert gemm.gateup_config(128, 28672, 4096) == 8 and gemm.gateup_config(200, 28672, 4096) == 8
     assert gemm.gateup_config(300, 28672, 4096) is None
     # 70B gate|up: split-K + reduce-SiLU (TP=8 shard tiled, TP=1 row-major at M <= 16 only)

@@ -17,13 +17,24 @@ def test_policy_table_choices(monkeypatch):
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=True) == "S4"
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=False) == "lib"
     assert gemm.prefill_choice(1280, 4096, 14336, None, slabs=True) == "hip"
-    # gate|up + SiLU on the tile kernel from 512 rows
+    # gate|up + SiLU on the tile kernel at every prefill size
     assert gemm.prefill_choice(512, 28672, 4096, "silu") == "hip"
-    assert gemm.prefill_choice(256, 28672, 4096, "silu") == "lib"
-    # 70B TP=8 O shard: the chunked bf16 decode kernel at small prefill steps, then the library
-    assert gemm.prefill_choice(384, 8192, 1024, None) == "K4"
-    assert gemm.prefill_choice(768, 8192, 1024, None) == "lib"
-    assert gemm.prefill_choice(384, 8192, 1024, "silu") == "lib"
+    assert gemm.prefill_choice(257, 28672, 4096, "silu") == "hip"
+    # 70B TP=8 shards (r6): the 128 x 128 tile kernel at small steps, the 256 x 256 one above; no
+    # SURVEY-named shard takes hipBLASLt at any prefill size
+    assert gemm.prefill_choice(384, 8192, 1024, None) == "M1"
+    assert gemm.prefill_choice(4096, 8192, 1024, None) == "hip"
+    assert gemm.prefill_choice(384, 1280, 8192, None, slabs=True) == "M8"
+    assert gemm.prefill_choice(2048, 1280, 8192, None, slabs=True) == "S4"
+    assert gemm.prefill_choice(384, 7168, 8192, "silu") == "M4"
+    assert gemm.prefill_choice(2048, 7168, 8192, "silu") == "hip"
+    assert gemm.prefill_choice(384, 8192, 3584, None) == "M2"
+    assert gemm.prefill_choice(3072, 8192, 3584, None) == "hip"
+    shards = [(1280, 8192, None, True), (8192, 1024, None, False), (7168, 8192, "silu", False),
+              (8192, 3584, None, False), (10240, 8192, None, True)]
+    for n, k, epi, slabs in shards:
+        for m in (257, 384, 512, 768, 1024, 1536, 2048, 3072, 4096, 8192):
+            assert gemm.prefill_choice(m, n, k, epi, slabs=slabs) != "lib", (n, k, m)
     # force: every tile path, the residual epilogue where offered
     monkeypatch.setenv("PENNY_PREFILL_GEMM", "force")
     assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "R"
