@@ -1190,22 +1190,22 @@ __device__ __forceinline__ float lanepair_sum(float v) {
 template <bool QPRE>
 __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, const char* __restrict__ vl,
                                                const Frag (&qf)[8], f32x16 (&o)[4], float& m, float& l,
-                                               bool causal, int j, int ctx, int qpos, float scale_log2, int h,
-                                               bool need_mask) {
+                                               f32x16& ms, bool causal, int j, int ctx, int qpos, float scale_log2,
+                                               int h, bool need_mask) {
   Frag kf[2][8];
 #pragma unroll
   for (int T = 0; T < 2; ++T)
 #pragma unroll
     for (int c = 0; c < 8; ++c) kf[T][c].u = *reinterpret_cast<const uint4*>(kl + 8192 * T + 512 * c);
   const bool fresh = m == -INFINITY;
-  const float m0 = (fresh || !QPRE) ? 0.f : -m;
+  // each S^T chain starts at ms = -m (QPRE; 0 while fresh or exact-Q): its first MFMA reads the
+  // persistent splat as C, so no per-block re-initialisation of the 32 accumulator registers
   f32x16 sc[2];
 #pragma unroll
   for (int T = 0; T < 2; ++T) {
+    sc[T] = mfma32(kf[T][0].v, qf[0].v, ms);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sc[T][r] = m0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) sc[T] = mfma32(kf[T][c].v, qf[c].v, sc[T]);
+    for (int c = 1; c < 8; ++c) sc[T] = mfma32(kf[T][c].v, qf[c].v, sc[T]);
   }
   Frag vf[4][4];
 #pragma unroll
@@ -1252,6 +1252,9 @@ __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, cons
       for (int T = 0; T < 2; ++T)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[T][r] -= rise;
+      const float mn = m == -INFINITY ? 0.f : -m;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ms[r] = mn;
     }
   }
   if constexpr (QPRE) {
@@ -1360,6 +1363,9 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[dt][e] = 0.f;
   float m = -INFINITY, l = 0.f;
+  f32x16 ms;                                  // the S^T chains' start value (attend_block32)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) ms[e] = 0.f;
   // per-lane fragment bases: K key-row pi(r) at 16 (256 r3 + 16 h + 8 r4 + (r & 7)); V dim row r at
   // 2048 (r >> 4) + 256 h + 16 (r & 15)
   const int kbase = 16 * (256 * ((c >> 3) & 1) + 16 * h + 8 * (c >> 4) + (c & 7));
@@ -1377,7 +1383,7 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
     const char* kls = smem + (jj % NBUF) * 2 * TILE;
     const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-    attend_block32<QPRE>(kls + kbase, kls + TILE + vbase, qf, o, m, l, causal, ja, ctx, qpos, scale_log2, h,
+    attend_block32<QPRE>(kls + kbase, kls + TILE + vbase, qf, o, m, l, ms, causal, ja, ctx, qpos, scale_log2, h,
                          __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
