@@ -1375,6 +1375,9 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   const bool wave_live = wave_tok0 < qlen;
   const int wave_last = min(tok0 + (w * 32 + 31) / G, qlen - 1);
   const int wave_kv_end = causal ? ctx - qlen + wave_last + 1 : ctx;
+  // static priority for the second-dispatched half (waves 4-7 lose VALU arbitration to their SIMD
+  // partner on every segment otherwise; cdna_hip_programming.md T5 static form)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int jj = 0; jj < nblk; ++jj) {
     if (jj + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
     else wait_vmcnt_barrier<0>();
@@ -1402,17 +1405,28 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     }
     return;
   }
-  if (!valid) return;
+  if (!valid) return;                         // lanes c and c + 32 share the row: swap partners stay paired
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   bf16* orow = out + ((long)(q0 + tok) * Hq + head) * D;
+  // 16-B stores (cdna_hip_programming.md T21): lane half h holds dims 8rg + 4h .. +3 of each 8-dim
+  // group rg; one permlane32 swap per dword of groups (rg, rg + 1) leaves lanes 0-31 the 8 dims of
+  // group rg and lanes 32-63 those of group rg + 1
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      bf16x4 v4;
+    for (int rg = 0; rg < 4; rg += 2) {
+      union {
+        bf16x4 v;
+        uint2 u;
+      } a, b;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[dt][4 * rg + e] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * rg + 4 * h) = v4;
+      for (int e = 0; e < 4; ++e) {
+        a.v[e] = (bf16)(o[dt][4 * rg + e] * inv);
+        b.v[e] = (bf16)(o[dt][4 * rg + 4 + e] * inv);
+      }
+      const auto x = __builtin_amdgcn_permlane32_swap(a.u.x, b.u.x, false, false);
+      const auto y = __builtin_amdgcn_permlane32_swap(a.u.y, b.u.y, false, false);
+      *reinterpret_cast<uint4*>(orow + 32 * dt + 8 * rg + 8 * h) = make_uint4(x[0], y[0], x[1], y[1]);
     }
   if (lse != nullptr && h == 0)
     lse[(long)(q0 + tok) * Hq + head] = lt > 0.f ? (m + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
