@@ -1484,10 +1484,13 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
 }
 
 // Big-tile prefill variant (PENNY_PREFILL_PP, or penny_attention_prefill_variant for in-process A/B
-// runs): 5 (default) prefill2 with the VALU-lean softmax (ones-MFMA row sums, lean max / grow
-// logic, exact Q; attend_block_fold), 6 = 5 with Q prescaled by scale*log2(e) (no per-score FMA; one
-// extra bf16 rounding of q*c, opt-in), 4 prefill2 with its K/V fragment prefetch pinned ahead of the
-// MFMAs (the r4 default, kept as the fallback with its tests); any other value selects 5.  Removed
+// runs): 7 (default, r6) prefill3 -- the block math on v_mfma_f32_32x32x16_bf16 (head dim 128; 64
+// takes 5): +3-5 % on the workload's mixed respond + decide / spec steps, -1-3 % on long single
+// responds (the 32x32 loop holds a ~6 % lower clock), +0.3-0.7 % end to end in two same-box driver
+// A/Bs (profiles/r6_prefill_attn_32x32_ab.jsonl, r6_bench_prefill_pp7_vs_pp5*.json); 5 prefill2 with
+// the VALU-lean softmax (ones-MFMA row sums, lean max / grow logic, exact Q; attend_block_fold), 6 =
+// 5 with Q prescaled by scale*log2(e) in-kernel (one extra bf16 rounding of q*c, opt-in), 4 prefill2
+// with its K/V fragment prefetch pinned ahead of the MFMAs (kept as the fallback with its tests).  Removed
 // in r5: the ping-pong prefill3 (r4 variants 1-3: 15-20 % slower on every mixed step,
 // profiles/r4_prefill_attn_pingpong_lean_rejected.jsonl), the unpinned prefill2 (variant 0, 4-6 %
 // slower than 4) and the tile-fastest grid order (PENNY_PREFILL_HEAD_FAST=0, 5-47 % slower).
@@ -1495,7 +1498,7 @@ static int g_prefill_variant = -1;
 static int prefill_variant() {
   if (g_prefill_variant < 0) {
     const char* v = getenv("PENNY_PREFILL_PP");
-    g_prefill_variant = v ? atoi(v) : 5;
+    g_prefill_variant = v ? atoi(v) : 7;
   }
   return g_prefill_variant;
 }

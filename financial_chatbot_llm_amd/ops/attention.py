@@ -285,8 +285,9 @@ def _lean_workspace(dev: torch.device, slots: int, Hkv: int, D: int) -> Tuple[to
 
 def prefill_variant(v: int = -1) -> int:
     """Select the big-tile prefill kernel for this process (returns the previous choice; -1 only
-    reads it): 5 = prefill2 with the VALU-lean softmax (default), 6 = 5 with prescaled Q (opt-in),
-    4 = prefill2 with pinned K/V fragment prefetch (r4 default, the fallback); other values select 5
+    reads it): 7 = prefill3, the 32x32x16-MFMA block loop (default from r6, head dim 128), 5 =
+    prefill2 with the VALU-lean softmax (the r5 default; head dim 64 under 7), 6 = 5 with prescaled Q
+    (opt-in), 4 = prefill2 with pinned K/V fragment prefetch (the fallback); other values select 5
     (``PENNY_PREFILL_PP`` sets the initial value).  In-process A/B runs and tests only."""
     return int(N.load().penny_attention_prefill_variant(int(v)))
 
