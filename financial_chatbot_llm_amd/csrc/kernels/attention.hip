@@ -1187,26 +1187,11 @@ __device__ __forceinline__ float lanepair_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// P.V of one block: O^T += V^T . P^T, P^T from the S^T registers (bf16, k-step order of the permutation)
-__device__ __forceinline__ void pv_block32(const char* __restrict__ vl, const Frag (&pf)[4], f32x16 (&o)[4]) {
-  Frag vf[4][4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int st = 0; st < 4; ++st) vf[dt][st].u = *reinterpret_cast<const uint4*>(vl + 4096 * dt + 512 * st);
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int st = 0; st < 4; ++st) o[dt] = mfma32(vf[dt][st].v, pf[st].v, o[dt]);
-}
-
-// PV = false: stop after forming P (pf), leaving its P.V to the caller (the staggered waves of
-// prefill3 run it one block later, after the next barrier)
-template <bool QPRE, bool PV = true>
+template <bool QPRE>
 __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, const char* __restrict__ vl,
                                                const Frag (&qf)[8], f32x16 (&o)[4], float& m, float& l,
-                                               f32x16& ms, Frag (&pf)[4], bool causal, int j, int ctx, int qpos,
-                                               float scale_log2, int h, bool need_mask) {
+                                               f32x16& ms, bool causal, int j, int ctx, int qpos, float scale_log2,
+                                               int h, bool need_mask) {
   Frag kf[2][8];
 #pragma unroll
   for (int T = 0; T < 2; ++T)
@@ -1223,12 +1208,10 @@ __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, cons
     for (int c = 1; c < 8; ++c) sc[T] = mfma32(kf[T][c].v, qf[c].v, sc[T]);
   }
   Frag vf[4][4];
-  if constexpr (PV) {                         // V fragments in flight while the softmax runs
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int st = 0; st < 4; ++st) vf[dt][st].u = *reinterpret_cast<const uint4*>(vl + 4096 * dt + 512 * st);
-  }
+    for (int st = 0; st < 4; ++st) vf[dt][st].u = *reinterpret_cast<const uint4*>(vl + 4096 * dt + 512 * st);
 
   if (need_mask) {
 #pragma unroll
@@ -1295,26 +1278,19 @@ __device__ __forceinline__ void attend_block32(const char* __restrict__ kl, cons
 #pragma unroll
     for (int r = 0; r < w2; ++r) s16[r] = s16[r] + s16[r + w2];
   l += s16[0];
+  Frag pf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st)
 #pragma unroll
     for (int e = 0; e < 8; ++e) pf[st].v[e] = (bf16)sc[st >> 1][8 * (st & 1) + e];
-  if constexpr (PV) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int st = 0; st < 4; ++st) o[dt] = mfma32(vf[dt][st].v, pf[st].v, o[dt]);
-  }
+    for (int st = 0; st < 4; ++st) o[dt] = mfma32(vf[dt][st].v, pf[st].v, o[dt]);
 }
 
 // prefill2_kernel's grid, work lists, lean slots and K/V staging ring with attend_block32 (D = 128)
-// STAG: waves 4-7 run each block's P.V one block late (after the next barrier), so on every SIMD
-// one wave's softmax VALU meets its partner's MFMAs instead of both waves reaching QK^T, softmax
-// and P.V in lockstep behind the per-block barrier (MI355X_MICROARCH.md 'Two waves per SIMD', item
-// 9).  The deferred block's V stays in its LDS slot: the ring is one block deeper (NBUF 4) at the
-// same look-ahead, so a slot is restaged only after the barrier that follows its late P.V.  No
-// rescale hazard: a late wave runs block j-1's P.V before block j's max decision.
-template <int NBUF, bool QPRE, bool STAG = false>
+template <int NBUF, bool QPRE>
 __global__ void __launch_bounds__(512, 1) prefill3_kernel(
     const bf16* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -1363,12 +1339,8 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
                                        16, 0, 0);
     }
   };
-  // LA blocks staged ahead of the one on the MFMAs: NBUF - 1, one fewer when staggered (the deferred
-  // P.V keeps the previous block's slot busy through the next barrier)
-  constexpr int LA = NBUF - 1 - (STAG ? 1 : 0);
-  static_assert(LA >= 2, "at least one block in flight beside the current one");
 #pragma unroll
-  for (int jj = 0; jj < LA; ++jj)
+  for (int jj = 0; jj < NBUF - 1; ++jj)
     if (jj < nblk) stage(jj);
 
   // this lane's query row and its 8 Q fragments (B operand: dims 16c' + 8h .. +7 of the row)
@@ -1406,41 +1378,16 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   // static priority for the second-dispatched half (waves 4-7 lose VALU arbitration to their SIMD
   // partner on every segment otherwise; cdna_hip_programming.md T5 static form)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-  static_assert(!STAG || NBUF >= 4, "the staggered P.V reads the previous block's slot after one more barrier");
-  Frag pf[4];
-  // two copies of the block loop (not one loop branching per block): each keeps its own register
-  // live ranges -- merged, the pending P of the late form pushed the kernel into scratch
-  if (STAG && __builtin_amdgcn_readfirstlane(w) >= 4) {
-    int pend = -1;                            // LDS slot of the block whose P.V is pending
-    for (int jj = 0; jj < nblk; ++jj) {
-      if (jj + LA - 1 < nblk) wait_vmcnt_barrier<(LA - 1) * LOADS>();
-      else wait_vmcnt_barrier<0>();
-      if (jj + LA < nblk) stage(jj + LA);
-      if (pend >= 0) {
-        pv_block32(smem + pend * 2 * TILE + TILE + vbase, pf, o);
-        pend = -1;
-      }
-      const int ja = jb + jj;
-      if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
-      const char* kls = smem + (jj % NBUF) * 2 * TILE;
-      const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-      attend_block32<QPRE, false>(kls + kbase, kls + TILE + vbase, qf, o, m, l, ms, pf, causal, ja, ctx, qpos,
-                                  scale_log2, h, __builtin_amdgcn_readfirstlane((int)!full) != 0);
-      pend = jj % NBUF;
-    }
-    if (pend >= 0) pv_block32(smem + pend * 2 * TILE + TILE + vbase, pf, o);
-  } else {
-    for (int jj = 0; jj < nblk; ++jj) {
-      if (jj + LA - 1 < nblk) wait_vmcnt_barrier<(LA - 1) * LOADS>();
-      else wait_vmcnt_barrier<0>();
-      if (jj + LA < nblk) stage(jj + LA);
-      const int ja = jb + jj;
-      if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
-      const char* kls = smem + (jj % NBUF) * 2 * TILE;
-      const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
-      attend_block32<QPRE, true>(kls + kbase, kls + TILE + vbase, qf, o, m, l, ms, pf, causal, ja, ctx, qpos,
-                                 scale_log2, h, __builtin_amdgcn_readfirstlane((int)!full) != 0);
-    }
+  for (int jj = 0; jj < nblk; ++jj) {
+    if (jj + NBUF - 2 < nblk && NBUF >= 3) wait_vmcnt_barrier<(NBUF - 2) * LOADS>();
+    else wait_vmcnt_barrier<0>();
+    if (jj + NBUF - 1 < nblk) stage(jj + NBUF - 1);
+    const int ja = jb + jj;
+    if (!wave_live || ja * KV_BS >= wave_kv_end) continue;
+    const char* kls = smem + (jj % NBUF) * 2 * TILE;
+    const bool full = (ja + 1) * KV_BS <= ctx && (!causal || (ja + 1) * KV_BS - 1 <= ctx - qlen + wave_tok0);
+    attend_block32<QPRE>(kls + kbase, kls + TILE + vbase, qf, o, m, l, ms, causal, ja, ctx, qpos, scale_log2, h,
+                         __builtin_amdgcn_readfirstlane((int)!full) != 0);
   }
 
   const float lt = lanepair_sum(l);
@@ -1509,16 +1456,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                      (const bf16*)q, cu_q, ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache,       \
                      (bf16*)out, sl2, Hq, Hkv, max_blocks, causal, lse, (const int*)nullptr, lean)
 #define LEAN_VARIANTS(DD)                                   \
-  if (DD == 128 && var == 8) {                              \
-    if (qpre)                                               \
-      hipLaunchKernelGGL((prefill3_kernel<4, true, true>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q,       \
-                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, \
-                         Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);                              \
-    else                                                    \
-      hipLaunchKernelGGL((prefill3_kernel<4, false, true>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q,      \
-                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, \
-                         Hkv, max_blocks, causal, lse, (const int*)nullptr, lean);                              \
-  } else if (DD == 128 && var == 7) {                       \
+  if (DD == 128 && var == 7) {                              \
     if (qpre)                                               \
       hipLaunchKernelGGL((prefill3_kernel<3, true>), grid, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens, \
                          block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,   \
@@ -1599,16 +1537,7 @@ PENNY_API int penny_attention_prefill(const void* q, const int* cu_q, const int*
   const dim3 grid2 = wl ? dim3(Hkv, nwork, 1) : dim3(Hkv, ntiles, num_seqs);
   const int* wp = wl ? work : nullptr;
 #define PREFILL_LAUNCH(DD)                                                                                       \
-  if (big && DD == 128 && pp_env == 8) {                                                                         \
-    if (qpre)                                                                                                    \
-      hipLaunchKernelGGL((prefill3_kernel<4, true, true>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q,      \
-                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,  \
-                         Hkv, max_blocks, causal, lse, wp);                                                      \
-    else                                                                                                         \
-      hipLaunchKernelGGL((prefill3_kernel<4, false, true>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q,     \
-                         ctx_lens, block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq,  \
-                         Hkv, max_blocks, causal, lse, wp);                                                      \
-  } else if (big && DD == 128 && pp_env == 7) {                                                                  \
+  if (big && DD == 128 && pp_env == 7) {                                                                         \
     if (qpre)                                                                                                    \
       hipLaunchKernelGGL((prefill3_kernel<3, true>), grid2, dim3(512), 0, stream, (const bf16*)q, cu_q, ctx_lens,  \
                          block_tables, (const bf16*)k_cache, (const bf16*)v_cache, (bf16*)out, sl2, Hq, Hkv,     \
