@@ -1388,6 +1388,44 @@ def bench_shard_shapes(dev, names=None, Ms=(1, 8, 16, 32, 64, 96, 128, 192, 256)
     return out
 
 
+def bench_mid_decode(dev, Ms=(64, 96, 128, 192, 256)) -> List[Dict]:
+    """The 8B decode projections at B = 64-256: the production decode path
+    (``gemm.linear`` on the tiled weight: split-K slabs / fused gate|up) against the 128 x 128 tile
+    kernel with S K-slices (row-major W), weights rotated over >= 768 MB so every call streams HBM.
+    Reports TB/s of weight bytes."""
+    from ..ops import gemm
+    out = []
+    rnd = lambda *s: ((torch.rand(s, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)  # noqa: E731
+    shapes = {"8b_qkv": (6144, 4096, None), "8b_o": (4096, 4096, None), "8b_down": (4096, 14336, None),
+              "8b_gate_up": (28672, 4096, "silu")}
+    for name, (N, K, epi) in shapes.items():
+        copies = max(2, min(16, (768 << 20) // (N * K * 2)))
+        ws = [rnd(N, K) for _ in range(copies)]
+        wts = [gemm.tile_weight(w) for w in ws]
+        it = [0]
+
+        def nxt():
+            it[0] = (it[0] + 1) % copies
+            return it[0]
+        for M in Ms:
+            x = rnd(M, K)
+            fns = {"prod": lambda: gemm.linear(x, ws[it[0]], epilogue=epi, wt=wts[nxt()], slabs=epi is None)}
+            for S in (1, 2, 4, 8):
+                if K % (64 * S):
+                    continue
+                fns[f"mid{S}"] = lambda S=S: gemm.mid_linear(x, ws[nxt()], S, epi, slabs=epi is None)
+            t = interleaved(fns, rounds=5, iters=copies)
+            best = min((k for k in t if k != "prod"), key=lambda k: t[k])
+            row = {"op": "mid_decode", "name": name, "N": N, "K": K, "M": M, **{k: round(v, 1) for k, v in t.items()},
+                   "prod_TBps": round(N * K * 2 / t["prod"] / 1e6, 2), "best_mid": best,
+                   "best_mid_TBps": round(N * K * 2 / t[best] / 1e6, 2)}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        del ws, wts
+        torch.cuda.empty_cache()
+    return out
+
+
 def bench_lm_head_stream(dev, V: int = 128256, K: int = 4096,
                          Ms=(1, 2, 4, 8, 16, 32, 48, 64, 96, 127)) -> List[Dict]:
     """LM head + sampler at decode sizes: hipBLASLt logits + the HIP sampler vs the 256x256 tile
@@ -1460,6 +1498,7 @@ def main(argv=None) -> int:
                 "splitk70b_tp8": lambda d: bench_splitk(d, ("qkv", "o", "down"), SHAPES_70B_TP8),
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
                 "shard_shapes": bench_shard_shapes,
+                "mid_decode": bench_mid_decode,
                 "mid_shards": lambda d: bench_shard_shapes(d, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_up",
                                                                      "70b_tp8_down", "70b_tp1_qkv"), Ms=()), "rm_pair": bench_rm_pair, "gemm_tiled_w": bench_gemm_tiled_w, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",

@@ -15,9 +15,9 @@ import re
 from collections import defaultdict
 
 CLASSES = [
-    ("gemm-prefill tile (HIP)", r"gemm_prefill_kernel"),
+    ("gemm-prefill tile (HIP)", r"gemm_prefill_kernel|gemm_mid_kernel"),
     ("attention-decode", r"decode_kernel|decode_reduce|decode_lean"),
-    ("attention-prefill", r"prefill_kernel|prefill2_kernel"),
+    ("attention-prefill", r"prefill_kernel|prefill2_kernel|prefill3_kernel|prefill_merge"),
     ("gemm-skinny (HIP)", r"skinny"),
     ("gemm-splitk (HIP)", r"splitk"),
     ("moe (HIP)", r"moe_|quant_rows"),
