@@ -1499,6 +1499,8 @@ def main(argv=None) -> int:
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
                 "shard_shapes": bench_shard_shapes,
                 "mid_decode": bench_mid_decode,
+                "mid_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up"), Ms=(),
+                                                       prefill_Ms=(320, 384, 512, 768, 1024, 1536, 2048)),
                 "mid_shards": lambda d: bench_shard_shapes(d, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_up",
                                                                      "70b_tp8_down", "70b_tp1_qkv"), Ms=()), "rm_pair": bench_rm_pair, "gemm_tiled_w": bench_gemm_tiled_w, "gemm_group": bench_gemm_group,
                 "rm_pair_wide": lambda d: bench_rm_pair(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up", "70b_tp8_qkv",

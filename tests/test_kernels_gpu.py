@@ -240,6 +240,43 @@ def test_prefill_attention_late_max_spike_forces_rescale(variant, spike_block):
     close(out[90, 5], ref[90, 5], atol=1e-2)
 
 
+@pytest.mark.parametrize("variant", [5, 7])
+@pytest.mark.parametrize("spike_block", [0, 1, 4, 9])
+def test_prefill_prescaled_late_spike(variant, spike_block):
+    """The production prescaled-Q path (7: the 32x32x16 kernel whose S^T chains start at -m; 5: the
+    16x16 fold) on a FORCED late rescale: one query row matched to a key of block `spike_block`, plain
+    and lean (split-KV) work lists."""
+    from financial_chatbot_llm_amd.ops.attention import gather_kv_ref
+    g = torch.Generator().manual_seed(90 + spike_block)
+    Hq, Hkv, D = 32, 8, 128
+    lens = [(96, 12 * 64), (40, 40), (33, 700)]
+    qlens = [a for a, _ in lens]
+    ctx = [b for _, b in lens]
+    tables, kc, vc = _paged_setup(ctx, Hkv, D, gen=g)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    qf = torch.randn(int(cu[-1]), Hq, D, generator=g) * 0.3
+    kfull, _ = gather_kv_ref(kc, vc, tables[0], ctx[0])
+    qf[90, 5] = kfull[64 * spike_block + 7, 1].float() * 3.5
+    ctx_t = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ref = ops.prefill(qf, cu, ctx_t, tables, kc, vc, scale, True)
+    qp = (qf * (scale * 1.4426950408889634)).to(torch.bfloat16)
+    args = (cu.to(DEV), ctx_t.to(DEV), tables.to(DEV), kc.to(DEV), vc.to(DEV))
+    old = ops.attention.prefill_variant(variant)
+    try:
+        out = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, True, max_q_len=max(qlens), q_prescaled=True)
+        wl = ops.attention.prefill_lean_list(cu.numpy(), ctx_t.numpy(), Hq // Hkv, Hkv, True, cus=100000,
+                                             min_chunk=1)
+        outl = ops.prefill(qp.to(DEV), *args, 1 / 1.4426950408889634, True, max_q_len=max(qlens),
+                           work=torch.from_numpy(wl).to(DEV), lean=(int(wl[0, 1]), int(wl[0, 2]), int(wl[0, 3])),
+                           q_prescaled=True)
+    finally:
+        ops.attention.prefill_variant(old)
+    for o in (out, outl):
+        close(o, ref, atol=3e-2)
+        close(o[90, 5], ref[90, 5], atol=2e-2)
+
+
 @pytest.mark.parametrize("Hq,Hkv,ctxs", [(32, 8, [1, 63, 64, 65, 700, 2100]), (8, 1, [5, 1500]), (64, 8, [333]),
                                          # B >= 96 / >= 192: longer partitions (pb 16 / 32)
                                          (32, 8, [(37 * i) % 3000 + 1 for i in range(100)]),
