@@ -518,9 +518,14 @@ PREFILL_EPI = {None: 0, "silu": 1, "slabs": 2, "residual": 3, "bias": 5, "bias_g
 # an entry use ``_default_choice``.
 PREFILL_POLICY: Dict[Tuple[int, int], List[Tuple[int, str]]] = {
     (6144, 4096): [(1 << 30, "fused")],                                                   # QKV
-    (4096, 4096): [(1024, "S4"), (2048, "S2"), (1 << 30, "R")],                           # O
+    # r6: the 8B O / down at small steps (decide-only and short respond steps) on the 128 x 128 tile's
+    # slabs (bench/kernels.py --only mid_8b, profiles/r6_mid_8b_prefill.jsonl, GEMM + the consumer's
+    # slab read at ~5 TB/s): O 26.5-27.1 vs 36.1-36.6 us at 320-384 rows (M4), 29.9-44.2 vs 38.6-50.5 at
+    # 512-1024 (M2); down 58.6-66.3 vs 78.6-80.8 us at 320-512 rows (M4).  QKV keeps the fused
+    # RoPE / KV-write tile (mid2 slabs + the separate RoPE pass: within a few us of it)
+    (4096, 4096): [(384, "M4"), (1024, "M2"), (2048, "S2"), (1 << 30, "R")],             # O
     (28672, 4096): [(1 << 30, "hip")],                                                    # gate|up + SiLU
-    (4096, 14336): [(1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],           # down
+    (4096, 14336): [(512, "M4"), (1024, "S4"), (1280, "hip"), (2048, "S2"), (1 << 30, "R")],   # down
     # Llama-3-70B TP=1 (r5, r6): each projection WITH its consumer (RoPE/KV write, add&RMSNorm, SiLU),
     # interleaved, M = 384..4096 (bench/kernels.py --only prefill_policy_70b,
     # profiles/r5_prefill_policy_70b_tp1_with_consumers.jsonl; QKV small steps on the 128 x 128 tile,

@@ -1640,6 +1640,22 @@ def _mid_case(gemm, name, M, S, N_, K):
     close(y, ref, atol=2e-2 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("N_,K,M,S", [(4096, 4096, 320, 4), (4096, 4096, 700, 2), (4096, 14336, 384, 4)])
+def test_linear_8b_small_prefill_steps_take_mid_slabs(N_, K, M, S):
+    """Llama-3-8B O / down at small prefill steps through ``linear`` (the production call, slabs for
+    the add&RMSNorm consumer): the policy's 128 x 128 tile slabs, equal to the fp32 product."""
+    from financial_chatbot_llm_amd.ops import gemm
+    assert gemm.prefill_choice(M, N_, K, None, True, fused_residual=True) == f"M{S}"
+    g = torch.Generator(device=DEV).manual_seed(M)
+    x = torch.randn((M, K), generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((N_, K), generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    r = torch.randn((M, N_), generator=g, device=DEV).to(torch.bfloat16)
+    out = gemm.linear(x, w, slabs=True, fuse_residual=r)
+    assert isinstance(out, gemm.Slabs) and out.P.shape == (S, M, N_)
+    ref = x.float() @ w.float().t()
+    close(out.P.sum(0), ref, atol=1e-3 * ref.abs().max().item(), rtol=1e-3)
+
+
 def test_mid_gemm_residual_epilogue_and_slab_exactness():
     """Residual epilogue (bf16(acc) + R, like GEMM-then-add) and split-K slabs equal to the f32
     per-slice products."""

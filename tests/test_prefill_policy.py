@@ -7,13 +7,16 @@ from financial_chatbot_llm_amd.ops import gemm
 
 def test_policy_table_choices(monkeypatch):
     monkeypatch.delenv("PENNY_PREFILL_GEMM", raising=False)
-    # O: split-K slabs, then the residual epilogue, where the caller can take them, else the library
+    # O: the 128 x 128 tile's slabs at small steps, 256 x 256 split-K slabs, then the residual
+    # epilogue, where the caller can take them, else the library
     assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=True) == "R"
     assert gemm.prefill_choice(4096, 4096, 4096, None, True, fused_residual=False) == "lib"
     assert gemm.prefill_choice(2048, 4096, 4096, None, True, fused_residual=True) == "S2"
-    assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "S4"
-    assert gemm.prefill_choice(512, 4096, 4096, None, False) == "lib"
-    # down: split-K slabs only when the consumer reads slabs
+    assert gemm.prefill_choice(1536, 4096, 4096, None, True, fused_residual=True) == "S2"
+    assert gemm.prefill_choice(512, 4096, 4096, None, True, fused_residual=True) == "M2"
+    assert gemm.prefill_choice(320, 4096, 4096, None, True, fused_residual=True) == "M4"
+    # down: 128 x 128 slabs to 512 rows, 256 x 256 slabs only when the consumer reads slabs
+    assert gemm.prefill_choice(384, 4096, 14336, None, slabs=True) == "M4"
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=True) == "S4"
     assert gemm.prefill_choice(1024, 4096, 14336, None, slabs=False) == "lib"
     assert gemm.prefill_choice(1280, 4096, 14336, None, slabs=True) == "hip"
