@@ -933,11 +933,14 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
 }
 
 // Lean (KV-split) prefill work: a tile's KV walk can be cut into chunks run by different
-// workgroups; a chunk writes flash-decoding partial state (unnormalised O, running max m, row sum
-// l) to slot `slot`, and prefill_merge_kernel combines a tile's slots in chunk order.
+// workgroups; a chunk writes flash-decoding partial state (its normalised O / l, running max m, row
+// sum l) to slot `slot`, and prefill_merge_kernel combines a tile's slots in chunk order.  The
+// partial O is bf16 (r6): half the f32 round trip through HBM and half the chunk's store tail; O / l
+// is a convex combination of V rows, so the bf16 rounding is relative to |V| (the same as the
+// unsplit kernel's own output rounding), and the merge weights l * 2^(m - M) stay f32.
 struct PrefillLean {
   const int* items;     // [n, 6]: sequence, tile, first block, end block, slot (< 0: whole tile), 0
-  float* part_o;        // [slots, Hkv, 256 rows, D] f32
+  bf16* part_o;         // [slots, Hkv, 256 rows, D] bf16: O / l (0 where l = 0)
   float* part_ml;       // [slots, Hkv, 256 rows, 2] f32: m (log2 units of the scaled scores), l
 };
 
@@ -1077,8 +1080,14 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
     const float lt = FOLD != 0 ? la[ct][0] : rowgroup_sum(l[ct]);
     if (slot >= 0) {                          // a chunk of a split walk: partial state for the merge
       const long pr = ((long)slot * Hkv + h) * 256 + w * 32 + ct * 16 + col;
+      const float pinv = lt > 0.f ? 1.f / lt : 0.f;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = o[ct][dt];
+      for (int dt = 0; dt < DT; ++dt) {
+        bf16x4 v4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v4[r] = (bf16)(o[ct][dt][r] * pinv);
+        *reinterpret_cast<bf16x4*>(lean.part_o + pr * D + 16 * dt + 4 * g) = v4;
+      }
       if (g == 0) {
         lean.part_ml[2 * pr] = m[ct];
         lean.part_ml[2 * pr + 1] = lt;
@@ -1109,7 +1118,7 @@ __global__ void __launch_bounds__(NW * 64, 1) prefill2_kernel(
 // merge [n, 6]: sequence, tile, first slot, number of slots, 0, 0 (chunk order = slot order).
 template <int D>
 __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restrict__ merge, const int* __restrict__ cu_q,
-                                                            const float* __restrict__ part_o,
+                                                            const bf16* __restrict__ part_o,
                                                             const float* __restrict__ part_ml, bf16* __restrict__ out,
                                                             float* __restrict__ lse, int Hq, int Hkv) {
   static_assert(D == 128 || D == 64, "head dim");
@@ -1136,9 +1145,11 @@ __global__ void __launch_bounds__(256) prefill_merge_kernel(const int* __restric
   for (int i = 0; i < np; ++i) {
     const long pr = pr0 + i * stride;
     const float mi = part_ml[2 * pr];
-    const float f = mi == -INFINITY ? 0.f : exp2f(mi - M);
-    L += part_ml[2 * pr + 1] * f;
-    O += *reinterpret_cast<const f32x4*>(part_o + pr * D + d) * f;
+    const float wl = mi == -INFINITY ? 0.f : part_ml[2 * pr + 1] * exp2f(mi - M);   // l_i 2^(m_i - M)
+    L += wl;
+    const bf16x4 p4 = *reinterpret_cast<const bf16x4*>(part_o + pr * D + d);       // O_i / l_i
+#pragma unroll
+    for (int k = 0; k < 4; ++k) O[k] += (float)p4[k] * wl;
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   const int head = h * G + r % G;
@@ -1391,23 +1402,19 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
   }
 
   const float lt = lanepair_sum(l);
+  long pr = 0;
   if (slot >= 0) {                            // a chunk of a split walk: partial state for the merge
-    const long pr = ((long)slot * Hkv + hk) * 256 + r;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg)
-        *reinterpret_cast<f32x4*>(lean.part_o + pr * D + 32 * dt + 8 * rg + 4 * h) =
-            f32x4{o[dt][4 * rg], o[dt][4 * rg + 1], o[dt][4 * rg + 2], o[dt][4 * rg + 3]};
+    pr = ((long)slot * Hkv + hk) * 256 + r;
     if (h == 0) {
       lean.part_ml[2 * pr] = m;
       lean.part_ml[2 * pr + 1] = lt;
     }
-    return;
+  } else if (!valid) {
+    return;                                   // lanes c and c + 32 share the row: swap partners stay paired
   }
-  if (!valid) return;                         // lanes c and c + 32 share the row: swap partners stay paired
+  // O / l as bf16, into the output row or (split walk) the chunk's partial row: the same stores
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  bf16* orow = out + ((long)(q0 + tok) * Hq + head) * D;
+  bf16* orow = slot >= 0 ? lean.part_o + pr * D : out + ((long)(q0 + tok) * Hq + head) * D;
   // 16-B stores (cdna_hip_programming.md T21): lane half h holds dims 8rg + 4h .. +3 of each 8-dim
   // group rg; one permlane32 swap per dword of groups (rg, rg + 1) leaves lanes 0-31 the 8 dims of
   // group rg and lanes 32-63 those of group rg + 1
@@ -1428,7 +1435,7 @@ __global__ void __launch_bounds__(512, 1) prefill3_kernel(
       const auto y = __builtin_amdgcn_permlane32_swap(a.u.y, b.u.y, false, false);
       *reinterpret_cast<uint4*>(orow + 32 * dt + 8 * rg + 8 * h) = make_uint4(x[0], y[0], x[1], y[1]);
     }
-  if (lse != nullptr && h == 0)
+  if (slot < 0 && lse != nullptr && h == 0)
     lse[(long)(q0 + tok) * Hq + head] = lt > 0.f ? (m + __log2f(lt)) * 0.6931471805599453f : -INFINITY;
 }
 
@@ -1440,7 +1447,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
                                            const void* k_cache, const void* v_cache, void* out, int Hq, int Hkv,
                                            int D, int max_blocks, float scale, int causal, float* lse,
                                            const int* items, int nitems, const int* merge, int nmerge,
-                                           float* part_o, float* part_ml, hipStream_t stream) {
+                                           void* part_o, float* part_ml, hipStream_t stream) {
   if (nitems <= 0) return 0;
   if (Hq % Hkv || (256 % (Hq / Hkv)) || !items || (nmerge > 0 && (!merge || !part_o || !part_ml)))
     return (int)hipErrorInvalidValue;
@@ -1448,7 +1455,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   const bool qpre = causal & 2;
   causal &= 1;
   const float sl2 = qpre ? 1.f : scale * LOG2E;
-  const PrefillLean lean{items, part_o, part_ml};
+  const PrefillLean lean{items, static_cast<bf16*>(part_o), part_ml};
   const int var = prefill_variant();
   const dim3 grid(Hkv, nitems, 1);
 #define LEAN_LAUNCH(DD, PREF_, SB_, FOLD_)                                                                        \
@@ -1470,7 +1477,7 @@ PENNY_API int penny_attention_prefill_lean(const void* q, const int* cu_q, const
   else LEAN_LAUNCH(DD, true, true, 1);                      \
   if (nmerge > 0)                                           \
     hipLaunchKernelGGL(prefill_merge_kernel<DD>, dim3(nmerge, Hkv, 256 / (4 * (64 / (DD / 4)))), dim3(256), 0, stream, \
-                       merge, cu_q, part_o, part_ml, (bf16*)out, lse, Hq, Hkv);
+                       merge, cu_q, static_cast<const bf16*>(part_o), part_ml, (bf16*)out, lse, Hq, Hkv);
   if (D == 128) {
     LEAN_VARIANTS(128)
   } else if (D == 64) {

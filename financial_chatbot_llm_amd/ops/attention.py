@@ -277,7 +277,7 @@ def _lean_workspace(dev: torch.device, slots: int, Hkv: int, D: int) -> Tuple[to
     need_o, need_ml = slots * Hkv * 256 * D, slots * Hkv * 256 * 2
     if ws is None or ws[0].numel() < need_o or ws[1].numel() < need_ml:
         grow = max(slots, 64)
-        ws = (torch.empty(grow * Hkv * 256 * D, dtype=torch.float32, device=dev),
+        ws = (torch.empty(grow * Hkv * 256 * D, dtype=torch.bfloat16, device=dev),     # O / l (bf16)
               torch.empty(grow * Hkv * 256 * 2, dtype=torch.float32, device=dev))
         _LEAN_WS[key] = ws
     return ws
