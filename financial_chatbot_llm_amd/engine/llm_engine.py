@@ -647,6 +647,12 @@ class LLMEngine:
                 **(self.cp.stats if self.cp is not None else {}),
                 "prefill_step_tokens_mean": round(self.runner.stats["prefill_step_tokens"]
                                                   / max(1, self.runner.stats["prefill_steps"]), 1),
+                # share of the prefill steps' GEMM rows that are 256-row tile padding
+                "prefill_tile_pad_frac": round(self.runner.stats["prefill_tile_pad_rows"]
+                                               / max(1, self.runner.stats["prefill_step_tokens"]
+                                                     + self.runner.stats["prefill_tile_pad_rows"]), 4),
+                "prefill_m_hist": dict(zip(("le256", "le512", "le1k", "le2k", "le3k", "le4k", "gt4k"),
+                                           self.runner.stats["prefill_m_hist"])),
                 # device time per step (PENNY_STEP_GPU_TIMING=1): compare with step_p50_ms (host cadence)
                 "gpu_graph_ms_mean": round(1e3 * self.runner.stats["gpu_graph_s"]
                                            / max(1, self.runner.stats["graph_steps"]), 3),

@@ -33,6 +33,10 @@ from .sequence import Sequence
 logger = get_logger(__name__)
 
 
+# prefill-step GEMM M histogram bucket upper bounds (engine stats / bench record)
+PREFILL_M_BUCKETS = (256, 512, 1024, 2048, 3072, 4096, 1 << 30)
+
+
 @dataclass
 class StepInputs:
     """Host-side description of one forward (also what the TP leader broadcasts, C4)."""
@@ -279,7 +283,8 @@ class ModelRunner:
         self._filt_failed: set = set()                    # buckets whose filtered twin could not be captured
         self._static = None
         self.graph_pool = None
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "prefill_steps": 0, "prefill_step_tokens": 0, "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "prefill_steps": 0, "prefill_step_tokens": 0,
+                      "prefill_tile_pad_rows": 0, "prefill_m_hist": [0] * len(PREFILL_M_BUCKETS), "gpu_graph_s": 0.0, "gpu_eager_s": 0.0,
                       "gpu_idle_s": 0.0, "gpu_idle_gaps": 0, "_prev_end_ev": None, "overlap_steps": 0}
         # TP prefill steps of >= overlap_min_rows rows run as two micro-batches whose all-reduces
         # overlap the other half's compute (PENNY_TP_OVERLAP=0 disables)
@@ -486,8 +491,14 @@ class ModelRunner:
         self.stats["steps"] += 1
         self.stats["tokens"] += len(si.ids)
         if si.num_prefill_tokens:   # GEMM M of the steps that run the prefill (library) GEMMs
+            M = len(si.ids)
             self.stats["prefill_steps"] += 1
-            self.stats["prefill_step_tokens"] += len(si.ids)
+            self.stats["prefill_step_tokens"] += M
+            # rows the 256-row prefill tiles pad (M > 256: the tile kernels' M quantisation) and the
+            # step-size histogram, for the bench record
+            self.stats["prefill_tile_pad_rows"] += (-M) % 256 if M > 256 else 0
+            b = next(i for i, hi in enumerate(PREFILL_M_BUCKETS) if M <= hi)
+            self.stats["prefill_m_hist"][b] += 1
         if len(si.logits_idx) == 0:
             self._stage_inputs(si)
             try:
