@@ -163,6 +163,9 @@ def test_overlap_scheduling_matches_synchronous():
                 steps += 1
             assert all(s.finished for s in seqs) and not eng.has_work()
             assert all(-1 not in s.output_ids for s in seqs)
+            st = eng.stats()                              # the bench record's prefill-step anatomy
+            assert sum(st["prefill_m_hist"].values()) == st["prefill_steps"] > 0
+            assert 0.0 <= st["prefill_tile_pad_frac"] < 1.0
             outs[(mode, blocks)] = ([s.output_ids for s in seqs], [s.finish_reason for s in seqs],
                                     eng.scheduler.num_preemptions, eng.bm.num_free())
     for blocks in (64, 12):
