@@ -222,6 +222,9 @@ MIXED_STEPS = {
     "1decide": [(220, 4600)],
     "2decides": [(230, 4700), (210, 4500)],
     "1respond-short": [(600, 4200)],
+    # lean split-KV steps with more merges (16-20 split tiles)
+    "4decides+16spec": [(220, 4600)] * 4 + [(9, 5200)] * 16,
+    "respond-short+4decides": [(600, 3600)] + [(220, 4600)] * 4,
 }
 
 

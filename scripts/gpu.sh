@@ -12,6 +12,7 @@
 #   bench[:ARGS]            bench.py (driver config unless ARGS), JSON to gpurun_out/TAG_bench.json
 #   prof[:ARGS]             bench.py under rocprofv3 --kernel-trace --stats -> TAG_prof_kernel_stats.md
 #   kbench:ONLY             bench.kernels --only ONLY -> TAG_kbench.jsonl
+#   kprof:ONLY              bench.kernels --only ONLY under rocprofv3 --kernel-trace --stats -> TAG_kprof_*
 #   pmc:ONLY:C1+C2+...      bench.kernels --only ONLY under rocprofv3 --pmc (one pass) -> TAG_pmc.md
 #   py:MODULE[,ARGS]        python -m MODULE ARGS
 #   env:K=V[,K=V]           export for the following steps (e.g. env:PENNY_DIST_BACKEND=gloo,PENNY_KV_FRACTION=0.4
@@ -49,9 +50,20 @@ for spec in "$@"; do
           tr=$(find /tmp/prof_$TAG -name '*kernel_trace.csv' | head -1)
           python3 -m financial_chatbot_llm_amd.bench.profsum "$st" --trace "$tr" --title "$TAG: bench ${args[*]}" \
               > "gpurun_out/${TAG}_prof_kernel_stats.md" 2>&1
+          # PROF_KEEP=<regex>: keep the trace rows (grid sizes, timestamps) of the matching kernels
+          [ -n "${PROF_KEEP:-}" ] && grep -E "Kernel_Name|${PROF_KEEP}" "$tr" > "gpurun_out/${TAG}_prof_kept_trace.csv"
           rm -rf /tmp/prof_$TAG ;;
     kbench) run "kbench_${rest//[^a-zA-Z0-9]/_}" 600 python -u -m financial_chatbot_llm_amd.bench.kernels --only "$rest" \
               --out "gpurun_out/${TAG}_kbench_${rest//[^a-zA-Z0-9]/_}.jsonl" || exit $? ;;
+    kprof) rm -rf /tmp/kprof_$TAG
+           run "kprof_${rest//[^a-zA-Z0-9]/_}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kprof_$TAG \
+               -o run -- python3 -m financial_chatbot_llm_amd.bench.kernels --only "$rest" || exit $?
+           st=$(find /tmp/kprof_$TAG -name '*kernel_stats.csv' | head -1)
+           tr=$(find /tmp/kprof_$TAG -name '*kernel_trace.csv' | head -1)
+           cp "$tr" "gpurun_out/${TAG}_kprof_trace.csv"
+           python3 -m financial_chatbot_llm_amd.bench.profsum "$st" --trace "$tr" --title "$TAG: kernels $rest" \
+               > "gpurun_out/${TAG}_kprof_kernel_stats.md" 2>&1
+           rm -rf /tmp/kprof_$TAG ;;
     pmc) only=${rest%%:*}; ctrs=${rest#*:}; ctrs=${ctrs//+/ }
          rm -rf /tmp/pmc_$TAG
          run "pmc_${only//[^a-zA-Z0-9]/_}" 240 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d /tmp/pmc_$TAG \
