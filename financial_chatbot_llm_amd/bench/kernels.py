@@ -296,6 +296,99 @@ def bench_prefill_mixed(dev) -> List[Dict]:
     return out
 
 
+def bench_attn_overlap(dev) -> List[Dict]:
+    """A mixed step's two attention kernels -- the prefill rows' (MFMA-bound, one 512-thread
+    workgroup per CU) and the decode rows' (HBM-bound) -- serial on one stream vs concurrent on two
+    (models/llama.py ATTN_OVERLAP): decode launched first (production through r6 s21), prefill
+    launched first, and prefill first on a high-priority stream.  Interleaved rounds; each form
+    ends joined on the current stream."""
+    out = []
+    g = torch.Generator(device=dev).manual_seed(5)
+    Hq, Hkv, D = 32, 8, 128
+    steps = {"respond+8decides|B96": (MIXED_STEPS["respond+8decides"], 96),
+             "2respond|B112": (MIXED_STEPS["2respond"], 112),
+             "respond-short+4decides|B100": (MIXED_STEPS["respond-short+4decides"], 100),
+             "1decide|B120": (MIXED_STEPS["1decide"], 120)}
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev)
+    hi = torch.cuda.Stream(device=dev, priority=-1)
+    for name, (shape, B) in steps.items():
+        tables, kc, vc = _paged_varlen(shape, Hkv, D, dev, g)
+        qlens = [q for q, _ in shape]
+        T = sum(qlens)
+        cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=dev)
+        lens = torch.tensor([c for _, c in shape], dtype=torch.int32, device=dev)
+        qp = (torch.randn((T, Hq, D), generator=g, device=dev) * (0.088 * 1.4426950408889634)).to(torch.bfloat16)
+        op = torch.empty_like(qp)
+        plan = ops.attention.prefill_plan(cu.cpu().numpy(), lens.cpu().numpy(), Hq // Hkv, Hkv)
+        pw = torch.from_numpy(plan).to(dev) if plan is not None else None
+        lean = (int(plan[0, 1]), int(plan[0, 2]), int(plan[0, 3])) if plan is not None and plan.shape[1] == 6 else None
+        # decode rows: their own contexts (1.5k-6.5k), separate cache
+        rng = torch.Generator().manual_seed(B)
+        ctxs = torch.randint(1500, 6500, (B,), generator=rng).tolist()
+        W = max((c + KV_BS - 1) // KV_BS for c in ctxs)
+        dt = torch.zeros((B, W), dtype=torch.int32)
+        nxt = 0
+        for b, c in enumerate(ctxs):
+            nb = (c + KV_BS - 1) // KV_BS
+            dt[b, :nb] = torch.arange(nxt, nxt + nb, dtype=torch.int32)
+            nxt += nb
+        dkc = torch.randn((nxt, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        dvc = torch.randn((nxt, Hkv, KV_BS * D), generator=g, device=dev).to(torch.bfloat16)
+        dt, dl = dt.to(dev), torch.tensor(ctxs, dtype=torch.int32, device=dev)
+        qd = torch.randn((B, Hq, D), generator=g, device=dev).to(torch.bfloat16)
+        od = torch.empty_like(qd)
+        ws = ops.DecodeWorkspace.create(B, Hq, D, 8192, dev)
+
+        def pf():
+            ops.prefill(qp, cu, lens, tables, kc, vc, 1 / 1.4426950408889634, True, max(qlens), out=op, work=pw,
+                        lean=lean, q_prescaled=True)
+
+        def dc(st=None):
+            ops.decode(qd, dl, dt, dkc, dvc, 0.088, workspace=ws, out=od, stream=st)
+
+        def serial():
+            pf()
+            dc()
+
+        def fork(st):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            st.wait_event(ev)
+
+        def join(st):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            main.wait_event(ev)
+
+        def dfirst():
+            fork(side)
+            dc(side.cuda_stream)
+            pf()
+            join(side)
+
+        def pfirst():
+            fork(side)
+            pf()
+            dc(side.cuda_stream)
+            join(side)
+
+        def pfirst_hi():
+            fork(hi)
+            with torch.cuda.stream(hi):
+                pf()
+            dc()
+            join(hi)
+
+        fns = {"serial": serial, "dfirst": dfirst, "pfirst": pfirst, "pfirst_hi": pfirst_hi,
+               "prefill_only": pf, "decode_only": dc}
+        t = interleaved(fns, rounds=7, iters=5)
+        row = {"op": "attn_overlap", "step": name, "T": T, "B": B, **{k: round(v, 1) for k, v in t.items()}}
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    return out
+
+
 def bench_prefill_spec_split(dev) -> List[Dict]:
     """Mixed steps with speculative chunks (9 query tokens behind 5k-token contexts): one launch of
     the 8-wave kernel over every sequence (LPT work list; a spec chunk's 36 rows fill one 256-row
@@ -1502,6 +1595,7 @@ def main(argv=None) -> int:
                 "gateup70b_tp8": lambda d: bench_gateup(d, 7168, 8192),
                 "shard_shapes": bench_shard_shapes,
                 "mid_decode": bench_mid_decode,
+                "attn_overlap": bench_attn_overlap,
                 "mid_8b": lambda d: bench_shard_shapes(d, names=("8b_qkv", "8b_o", "8b_down", "8b_gate_up"), Ms=(),
                                                        prefill_Ms=(320, 384, 512, 768, 1024, 1536, 2048)),
                 "mid_shards": lambda d: bench_shard_shapes(d, names=("70b_tp8_qkv", "70b_tp8_o", "70b_tp8_gate_up",

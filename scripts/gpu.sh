@@ -10,6 +10,7 @@
 #   smoke                   __graft_entry__.smoke()
 #   test:EXPR               pytest -m gpu -k EXPR
 #   bench[:ARGS]            bench.py (driver config unless ARGS), JSON to gpurun_out/TAG_bench.json
+#                           (the n-th bench step of a call: TAG_bench<n>.json)
 #   prof[:ARGS]             bench.py under rocprofv3 --kernel-trace --stats -> TAG_prof_kernel_stats.md
 #   kbench:ONLY             bench.kernels --only ONLY -> TAG_kbench.jsonl
 #   kprof:ONLY              bench.kernels --only ONLY under rocprofv3 --kernel-trace --stats -> TAG_kprof_*
@@ -41,7 +42,8 @@ for spec in "$@"; do
     test) run "test_${rest//[^a-zA-Z0-9]/_}" 600 python -u -m pytest tests/ -x -v -m gpu -k "$rest" --timeout 300 \
             --timeout-method thread || exit $? ;;
     bench) [ ${#args[@]} -eq 0 ] && args=(--steps 20 --warmup 5)
-           run bench 900 python -u bench.py "${args[@]}" --json-out "gpurun_out/${TAG}_bench.json" || exit $? ;;
+           NB=$(( ${NB:-0} + 1 )); bn=bench; [ "$NB" -gt 1 ] && bn=bench$NB    # A/B: bench, bench2, ...
+           run $bn 900 python -u bench.py "${args[@]}" --json-out "gpurun_out/${TAG}_${bn}.json" || exit $? ;;
     prof) [ ${#args[@]} -eq 0 ] && args=(--steps 20 --warmup 5)
           rm -rf /tmp/prof_$TAG
           run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$TAG -o run -- \
