@@ -275,7 +275,8 @@ def bench_prefill_mixed(dev) -> List[Dict]:
             return f
         variants = {"pf2_sb": (4, False, False), "pf2_fold": (5, False, False), "pf3": (7, False, False),
                     "pf2_fold_lean": (5, True, False), "pf3_lean": (7, True, False),
-                    "pf2_prod": (5, True, True), "pf3_prod": (7, True, True)}
+                    "pf2_prod": (5, True, True), "pf3_prod": (7, True, True),
+                    "pf3_q": (7, False, True)}
         old = ops.attention.prefill_variant()
         outs = {}
         for k, v in variants.items():

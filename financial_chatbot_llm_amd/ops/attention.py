@@ -11,6 +11,7 @@ math on the same bf16 inputs) and the CPU path used by the CI tests.
 """
 from __future__ import annotations
 
+import heapq
 import math
 import os
 from dataclasses import dataclass
@@ -213,6 +214,30 @@ def prefill_work_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, causal: bo
 # LPT over chunks instead of whole tiles.  PENNY_PREFILL_LEAN=0 keeps whole tiles.
 PREFILL_LEAN = os.environ.get("PENNY_PREFILL_LEAN", "1") != "0"
 LEAN_MIN_CHUNK = 8          # KV blocks: below that a chunk's partial write + merge outweigh the balance
+# r6 cost gate, in KV-block units of one workgroup's walk: a split is kept only if its LPT makespan
+# (+ per-workgroup prologue / epilogue, + a chunk's partial write, + the merge launch) beats the
+# whole-tile plan's.  Splitting into MORE workgroups than CUs can leave the makespan where it was
+# (a second round of chunks behind the longest whole tiles): on the kbench steps
+# "respond-short+4decides" / "4decides+16spec" the split ran 10 % / 2.5 % slower than whole tiles
+# (profiles/r6_prefill_attn_pair_barrier_rejected.jsonl pf3_prod vs pf3_q), while 1-2 decides and
+# a short respond alone keep their 1.4-3x gain.  Calibrated on those five steps.
+LEAN_ITEM_BLOCKS = 3        # prologue (Q load, first K/V wait) + epilogue of one workgroup
+LEAN_CHUNK_BLOCKS = 1       # a chunk's partial O / (m, l) write
+LEAN_MERGE_BLOCKS = 6       # prefill_merge_kernel launch + its pass
+LEAN_COST_GATE = os.environ.get("PENNY_PREFILL_LEAN_GATE", "1") != "0"
+
+
+def _lpt_makespan(lengths, machines: int) -> float:
+    """Makespan of longest-processing-time-first list scheduling of ``lengths`` on ``machines``."""
+    ls = sorted(lengths, reverse=True)
+    if machines <= 0 or not ls:
+        return float(sum(ls))
+    if len(ls) <= machines:
+        return float(ls[0])
+    loads = sorted(ls[:machines])            # a sorted list is a valid min-heap
+    for x in ls[machines:]:
+        heapq.heapreplace(loads, loads[0] + x)
+    return float(max(loads))
 
 
 def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causal: bool = True,
@@ -249,6 +274,14 @@ def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, 
         items += [(s_, t, cuts[i], cuts[i + 1], slot + i, 0) for i in range(k)]
         slot += k
     items.sort(key=lambda r: -(r[3] - r[2]))                  # LPT over chunks
+    if LEAN_COST_GATE:
+        # every item runs once per kv head: the heads' identical lists share the CUs evenly
+        mach = max(cus // max(Hkv, 1), 1)
+        whole = _lpt_makespan([nb + LEAN_ITEM_BLOCKS for _, _, nb in tiles], mach)
+        lean = _lpt_makespan([e - b + LEAN_ITEM_BLOCKS + (LEAN_CHUNK_BLOCKS if sl >= 0 else 0)
+                              for _, _, b, e, sl, _ in items], mach) + LEAN_MERGE_BLOCKS
+        if lean >= whole:
+            return None
     out = np.zeros((1 + len(items) + len(merges), 6), np.int32)
     out[0, :4] = (-1, len(items), len(merges), slot)
     out[1:1 + len(items)] = np.asarray(items, np.int32)

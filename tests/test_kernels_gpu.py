@@ -176,10 +176,11 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
     (8, 1, 128, True, [(40, 1500), (33, 500)]),
     (12, 12, 64, False, [(200, 700), (33, 33)]),
 ])
-def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal, lens):
+def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal, lens, monkeypatch):
     """Lean prefill: the KV walks of long tiles cut into chunks on different workgroups, partial
     (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse), on every prefill2
-    variant."""
+    variant (the planner's cost gate off: these small steps exercise the split path by force)."""
+    monkeypatch.setattr(ops.attention, "LEAN_COST_GATE", False)
     g = torch.Generator().manual_seed(50 + min_chunk)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
@@ -242,11 +243,12 @@ def test_prefill_attention_late_max_spike_forces_rescale(variant, spike_block):
 
 @pytest.mark.parametrize("variant", [5, 7])
 @pytest.mark.parametrize("spike_block", [0, 1, 4, 9])
-def test_prefill_prescaled_late_spike(variant, spike_block):
+def test_prefill_prescaled_late_spike(variant, spike_block, monkeypatch):
     """The production prescaled-Q path (7: the 32x32x16 kernel whose S^T chains start at -m; 5: the
     16x16 fold) on a FORCED late rescale: one query row matched to a key of block `spike_block`, plain
     and lean (split-KV) work lists."""
     from financial_chatbot_llm_amd.ops.attention import gather_kv_ref
+    monkeypatch.setattr(ops.attention, "LEAN_COST_GATE", False)
     g = torch.Generator().manual_seed(90 + spike_block)
     Hq, Hkv, D = 32, 8, 128
     lens = [(96, 12 * 64), (40, 40), (33, 700)]
@@ -973,11 +975,12 @@ def test_prefill_qkv_rope_kv_write_fused(M, Hq, Hkv):
     (32, 8, 128, True, [(257, 257), (64, 3000)], 12.0),      # peaky rows
     (8, 1, 128, True, [(40, 40), (33, 500)], 1.0),
 ])
-def test_prefill_attention_prescaled_q(variant, Hq, Hkv, D, causal, lens, qscale):
+def test_prefill_attention_prescaled_q(variant, Hq, Hkv, D, causal, lens, qscale, monkeypatch):
     """q handed over prescaled by scale * log2(e) at its ONE bf16 rounding (what the fused QKV epilogue
     does with qscale) on the prescaled-Q fold, with scale 1 / log2(e): as close to the fp32 reference
     as the exact-Q variant 5 fed bf16(q) -- the in-kernel prescale's second rounding (variant 6) is
     what costs precision on peaky rows -- plain and lean work lists."""
+    monkeypatch.setattr(ops.attention, "LEAN_COST_GATE", False)
     g = torch.Generator().manual_seed(70)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]

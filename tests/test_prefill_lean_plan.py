@@ -28,7 +28,8 @@ def _walks(cu, ctx, G, causal=True):
     [(4096, 4096)],
 ])
 @pytest.mark.parametrize("causal", [True, False])
-def test_lean_list_covers_every_block_once(shape, causal):
+def test_lean_list_covers_every_block_once(shape, causal, monkeypatch):
+    monkeypatch.setattr(A, "LEAN_COST_GATE", False)      # the list's structure; the gate is below
     G, Hkv = 4, 8
     cu = np.array([0] + list(np.cumsum([q for q, _ in shape])), np.int64)
     ctx = [c for _, c in shape]
@@ -62,3 +63,24 @@ def test_lean_list_covers_every_block_once(shape, causal):
     whole = [(s, t) for s, t, b0, b1, slot, _ in items.tolist() if slot < 0]
     assert all(b0 == 0 and b1 == walks[(s, t)] for s, t, b0, b1, slot, _ in items.tolist() if slot < 0)
     assert len(set(whole)) == len(whole)
+
+
+def test_lpt_makespan():
+    assert A._lpt_makespan([5, 4, 3, 3, 3], 2) == 10.0      # LPT: 5 | 4, 3 -> 4+3 | 5+3 | 7+3
+    assert A._lpt_makespan([7, 1], 4) == 7.0
+    assert A._lpt_makespan([2] * 8, 4) == 4.0
+
+
+@pytest.mark.parametrize("shape,split", [
+    ([(220, 4600)], True),                            # one decide: 4 tiles x 8 heads on 256 CUs
+    ([(230, 4700), (210, 4500)], True),
+    ([(600, 4200)], True),
+    # more chunks than CUs: a second round behind the longest whole tiles -- measured slower split
+    # (profiles/r6_prefill_attn_pair_barrier_rejected.jsonl pf3_prod vs pf3_q)
+    ([(600, 3600)] + [(220, 4600)] * 4, False),
+    ([(220, 4600)] * 4 + [(9, 5200)] * 16, False),
+])
+def test_lean_cost_gate_decisions(shape, split):
+    cu = np.array([0] + list(np.cumsum([q for q, _ in shape])), np.int64)
+    ln = A.prefill_lean_list(cu, np.array([c for _, c in shape]), 4, 8)
+    assert (ln is not None) == split
