@@ -261,27 +261,45 @@ def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, 
             tiles.append((s_, t, (kv_end + KV_BS - 1) // KV_BS))
     total = sum(nb for _, _, nb in tiles)
     C = max(min_chunk, -(-total * Hkv // max(cus, 1)))       # balanced per-CU share of block units
-    if max(nb for _, _, nb in tiles) <= C:
+    longest = max(nb for _, _, nb in tiles)
+    if longest <= C:
         return None
-    items, merges, slot = [], [], 0
-    for s_, t, nb in tiles:
-        if nb <= C:
-            items.append((s_, t, 0, nb, -1, 0))
-            continue
-        k = -(-nb // C)
-        cuts = [round(i * nb / k) for i in range(k + 1)]
-        merges.append((s_, t, slot, k, 0, 0))
-        items += [(s_, t, cuts[i], cuts[i + 1], slot + i, 0) for i in range(k)]
-        slot += k
-    items.sort(key=lambda r: -(r[3] - r[2]))                  # LPT over chunks
+
+    def plan(C):
+        items, merges, slot = [], [], 0
+        for s_, t, nb in tiles:
+            if nb <= C:
+                items.append((s_, t, 0, nb, -1, 0))
+                continue
+            k = -(-nb // C)
+            cuts = [round(i * nb / k) for i in range(k + 1)]
+            merges.append((s_, t, slot, k, 0, 0))
+            items += [(s_, t, cuts[i], cuts[i + 1], slot + i, 0) for i in range(k)]
+            slot += k
+        items.sort(key=lambda r: -(r[3] - r[2]))              # LPT over chunks
+        return items, merges, slot
+
     if LEAN_COST_GATE:
-        # every item runs once per kv head: the heads' identical lists share the CUs evenly
+        # every item runs once per kv head: the heads' identical lists share the CUs evenly.  The
+        # chunk size is the balanced share or a coarser cut of the longest walk into k = 2..8
+        # pieces, whichever the model's makespan prefers (finer than the balanced share never won
+        # on the kbench steps and costs milliseconds of host LPT); whole tiles unless a split's
+        # makespan + merge beats them
         mach = max(cus // max(Hkv, 1), 1)
         whole = _lpt_makespan([nb + LEAN_ITEM_BLOCKS for _, _, nb in tiles], mach)
-        lean = _lpt_makespan([e - b + LEAN_ITEM_BLOCKS + (LEAN_CHUNK_BLOCKS if sl >= 0 else 0)
-                              for _, _, b, e, sl, _ in items], mach) + LEAN_MERGE_BLOCKS
-        if lean >= whole:
+        best, best_c = whole, None
+        for c in sorted({C} | {-(-longest // k) for k in range(2, 9)}):
+            if c < C or c >= longest:
+                continue
+            items, _, _ = plan(c)
+            ms = _lpt_makespan([e - b + LEAN_ITEM_BLOCKS + (LEAN_CHUNK_BLOCKS if sl >= 0 else 0)
+                                for _, _, b, e, sl, _ in items], mach) + LEAN_MERGE_BLOCKS
+            if ms < best:
+                best, best_c = ms, c
+        if best_c is None:
             return None
+        C = best_c
+    items, merges, slot = plan(C)
     out = np.zeros((1 + len(items) + len(merges), 6), np.int32)
     out[0, :4] = (-1, len(items), len(merges), slot)
     out[1:1 + len(items)] = np.asarray(items, np.int32)
