@@ -225,6 +225,10 @@ MIXED_STEPS = {
     # lean split-KV steps with more merges (16-20 split tiles)
     "4decides+16spec": [(220, 4600)] * 4 + [(9, 5200)] * 16,
     "respond-short+4decides": [(600, 3600)] + [(220, 4600)] * 4,
+    # tiny chunks only (<= 32 tokens): speculative verify rows / known runs behind long contexts
+    "16spec": [(9, 5200)] * 16,
+    "4runs": [(2, 4600), (3, 3900), (2, 5100), (4, 4400)],
+    "1run": [(2, 4600)],
 }
 
 

@@ -249,7 +249,11 @@ def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, 
         return None
     cu = np.asarray(cu_q, np.int64)
     ql = cu[1:] - cu[:-1]
-    if len(ql) == 0 or int(ql.max()) * G <= 128:
+    # tiny chunks only (speculative / known-run rows: <= 128 rows per (sequence, kv head)) take the
+    # 4-wave 128-row kernel, which walks each context whole on one workgroup; with the cost gate
+    # they may instead split their walks on the 8-wave kernel (its whole-tile makespan stands in
+    # for the 4-wave kernel's)
+    if len(ql) == 0 or (int(ql.max()) * G <= 128 and not LEAN_COST_GATE):
         return None
     ctx = np.asarray(ctx_lens, np.int64)
     TQ = 256 // G

@@ -173,14 +173,17 @@ def test_prefill_attention_big_tile_variants(variant, Hq, Hkv, D, causal, lens, 
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 @pytest.mark.parametrize("Hq,Hkv,D,causal,lens", [
     (32, 8, 128, True, [(300, 1100), (9, 900), (70, 70), (130, 2000)]),   # respond / spec / first turn / decide
+    (32, 8, 128, True, [(9, 3000), (2, 2100), (5, 700), (1, 1300)]),      # tiny chunks only (spec / known runs)
     (8, 1, 128, True, [(40, 1500), (33, 500)]),
     (12, 12, 64, False, [(200, 700), (33, 33)]),
 ])
 def test_prefill_attention_lean_split_kv(variant, min_chunk, Hq, Hkv, D, causal, lens, monkeypatch):
     """Lean prefill: the KV walks of long tiles cut into chunks on different workgroups, partial
     (O, m, l) merged in chunk order -- vs the fp32 reference (output and lse), on every prefill2
-    variant (the planner's cost gate off: these small steps exercise the split path by force)."""
-    monkeypatch.setattr(ops.attention, "LEAN_COST_GATE", False)
+    variant (the planner's cost gate off: these small steps exercise the split path by force; a
+    tiny-chunks-only step reaches the split path only through the gate, which takes it here)."""
+    if max(a for a, _ in lens) * (Hq // Hkv) > 128:
+        monkeypatch.setattr(ops.attention, "LEAN_COST_GATE", False)
     g = torch.Generator().manual_seed(50 + min_chunk)
     qlens = [a for a, _ in lens]
     ctx = [b for _, b in lens]
