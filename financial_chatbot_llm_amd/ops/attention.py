@@ -242,9 +242,10 @@ def _lpt_makespan(lengths, machines: int) -> float:
 
 def prefill_lean_list(cu_q: np.ndarray, ctx_lens: np.ndarray, G: int, Hkv: int, causal: bool = True,
                       cus: int = 256, min_chunk: int = LEAN_MIN_CHUNK) -> Optional[np.ndarray]:
-    """Lean work list of one step, or None when no tile needs splitting: int32 [1 + n + m, 6] =
-    header (-1, n items, m merges, slots, 0, 0), n items (sequence, tile, first block, end block,
-    slot or -1, 0) longest first, m merges (sequence, tile, first slot, slots, 0, 0)."""
+    """Lean work list of one step, or None when no tile needs splitting or (``LEAN_COST_GATE``)
+    the makespan model prefers whole tiles: int32 [1 + n + m, 6] = header (-1, n items, m merges,
+    slots, 0, 0), n items (sequence, tile, first block, end block, slot or -1, 0) longest first,
+    m merges (sequence, tile, first slot, slots, 0, 0)."""
     if not PREFILL_LEAN or G <= 0 or 256 % G:
         return None
     cu = np.asarray(cu_q, np.int64)
